@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X unfolded D-ADMM forward (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1..3] name the single-GPU shapes; the metric is quoted on
+B=4096, P=5, n=256, K=25, m=64): one "step" = one DLASSO_unfolded.forward over a batch of 4096
+synthetic problems resident in HBM: the reference's random inits (randn x 3), the hyper-parameter
+table and the fused K-iteration HIP kernel. Unit of work = one ADMM iteration of one problem
+(all P agents); value = B * K * steps * n_gpus / max-over-ranks wall time (weak scaling: every
+rank runs its own 4096-problem batch; no collective inside the step).
+
+Extra fields: "roofline" (dominant kernel: fused_forward_kernel, timed with HIP events on its
+stream; FP32 MFMA roofline), "cpu_baseline" (the C oracle — a port of the reference forward —
+on the host cores, bounded sample), "parity" (bit-exactness vs the order-matched fp32 oracle and
+final-iterate MSE vs the fp64 restatement, on a slice of the batch; outside the timed region).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "hyperparameter-gnn_unfolded-d-admm-main_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
+    ap.add_argument("--P", type=int, default=5)
+    ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--m", type=int, default=64)
+    ap.add_argument("--K", type=int, default=25)
+    ap.add_argument("--graph-prob", type=float, default=0.5)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (written from a rocprofv3 --pmc pass)")
+    return ap.parse_args()
+
+
+def make_args(K):
+    return argparse.Namespace(GHN_iter_num=K, DADMM_mode="diff", alpha_max=0.1, tau_max=0.99,
+                              rho_max=0.99, eta_max=0.99, max_penalty_threshold=0.8,
+                              penalty_reduction_factor=0.95)
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import oracle as O   # input generator (reference distribution) and checker only
+    import unfolded_DLASSO
+    from dadmm_hip import _lib
+
+    P, n, m, K, B = a.P, a.n, a.m, a.K, a.batch
+    # A is shared by every rank (one sensing operator per agent); each rank draws its own shard
+    A, _, _ = O.make_problem(P, m, n, 1, seed=1234)
+    gen = torch.Generator().manual_seed(4321 + rank)
+    x = 2 * torch.randn(B, n, generator=gen) * (torch.rand(B, n, generator=gen) <= 0.25)
+    b = torch.einsum("pmn,bn->bpm", torch.from_numpy(A), x)
+    At = torch.from_numpy(A)[None].to(dev)
+    bt = b[..., None].to(dev)
+    G = O.er_graph(P, a.graph_prob, seed=7)
+    graph_list = [G] * B
+    model = unfolded_DLASSO.DLASSO_unfolded(At, make_args(K)).to(dev)
+    param = np.load(os.path.join(ROOT, "tests", "golden",
+                                 "fixture_25_iter_general_learning_seq_hyp_param.npy"))
+    if param.shape == (K, P, 4):
+        with torch.no_grad():
+            model.seq_hyp.param.copy_(torch.from_numpy(param))
+    model.eval()
+
+    # --- kernel-level timing hook: HIP events around every fused launch, on its stream ------
+    from dadmm_hip import ops
+    ev_pairs = []
+    orig_forward = _lib.load().dadmm_forward
+
+    class _Timed:
+        def __call__(self, *args):
+            s = torch.cuda.current_stream(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            rc = orig_forward(*args)
+            e1.record(s)
+            ev_pairs.append((e0, e1))
+            return rc
+
+    timed = _Timed()
+
+    def step():
+        with torch.no_grad():
+            Y, _ = model(bt, graph_list)
+        return Y
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # patch the library entry point only for the timed region's event bookkeeping
+    L = _lib.load()
+    L.dadmm_forward = timed
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    L.dadmm_forward = orig_forward
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev_pairs]))
+
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        # the reference's one collective: the epoch loss (a scalar all-reduce over RCCL)
+        with torch.no_grad():
+            Y, _ = model(bt, graph_list)
+            lf = ((Y[-1, ..., 0] - x.to(dev)[:, None, :]) ** 2).mean()
+        red = torch.stack([lf, torch.ones((), device=dev)])
+        dist.all_reduce(red)
+
+    units_per_step = B * K
+    value = units_per_step * a.steps * world / elapsed
+    ms_per_step = 1e3 * elapsed / a.steps
+
+    if rank == 0:
+        # roofline of the dominant kernel (algorithmic flops: SURVEY.md §8(d))
+        deg_avg = float(sum(d for _, d in G.degree())) / P
+        flop_unit = P * (4 * m * n + 14 * n) + 2 * P * n * deg_avg
+        flops = flop_unit * units_per_step
+        achieved = flops / (kern_ms * 1e-3) / 1e12
+        # HBM view: bytes the fused launch must move (inputs once, every iterate once)
+        hbm_bytes = 4 * (K * B * P * n + 3 * B * P * n + B * P * m) + 2 * 4 * P * 64 * n
+        traffic = None
+        if os.path.exists(a.traffic_file):
+            try:
+                tr = json.load(open(a.traffic_file))
+                key = f"B{B}_P{P}_n{n}_m{m}_K{K}"
+                traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+
+        parity = check_parity(O, model, A, b, G, dev, P, n, m, K)
+        cpu = None if a.no_cpu_baseline else cpu_baseline(O, A, b, G, model, P, n, m, K,
+                                                          a.cpu_baseline_seconds)
+        out = {
+            "metric": "ADMM-iters/sec (node), batch=4096 P=5 n=256 K=25; final-iter MSE vs ref",
+            "value": value,
+            "unit": "ADMM-iters/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (reference distribution: A_p = U clamp(S,0.1,10) V^T, "
+                    "x* = 2 N(0,1) Bernoulli(0.25), b_p = A_p x*; trained seq_hyp fixture)",
+            "config": {"workload": f"DLASSO_unfolded.forward B={B}/GPU P={P} n={n} m={m} K={K} "
+                                   f"ER(p={a.graph_prob}) shared graph",
+                       "global_batch": B * world, "P": P, "n": n, "m": m, "K": K,
+                       "parallelism": f"batch-sharded dp{world}"},
+            "agent_iters_per_s": value * P,
+            "kernel_ms": kern_ms,
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS,
+                         "traffic": traffic,
+                         "flop_per_unit": flop_unit, "units_per_launch": units_per_step,
+                         "hbm_algorithmic_bytes": hbm_bytes,
+                         "hbm_achieved_GBs": hbm_bytes / (kern_ms * 1e-3) / 1e9,
+                         "hbm_frac": hbm_bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def check_parity(O, model, A, b, G, dev, P, n, m, K, Bs=32):
+    """Bit-exactness vs the order-matched fp32 oracle and final-iterate MSE vs fp64 on the
+    first Bs problems of the batch (same A, b, graph, inits, hyper-parameters)."""
+    rng = np.random.default_rng(99)
+    y0, U0, d0 = (1e-2 * rng.standard_normal((3, Bs, P, n))).astype(np.float32)
+    bs = b[:Bs].numpy()
+    with torch.no_grad():
+        Y, _ = model(torch.from_numpy(bs).to(dev)[..., None], [G] * Bs,
+                     inits=tuple(torch.from_numpy(v).to(dev) for v in (y0, U0, d0)))
+        table = model.hyp_table(K).cpu().numpy()
+    Y = Y[..., 0].cpu().numpy()
+    Y32, _, _ = O.forward_f32(A, bs, [G] * Bs, table, y0, U0, d0)
+    Y64, _, _ = O.forward_f64(A, bs, [G] * Bs, table, y0, U0, d0)
+    return {"samples": Bs, "bit_exact_vs_fp32_oracle": bool(np.array_equal(Y, Y32)),
+            "max_abs_diff_vs_fp32_oracle": float(np.abs(Y - Y32).max()),
+            "final_iter_mse_vs_fp64": float(((Y[-1] - Y64[-1]) ** 2).mean())}
+
+
+def cpu_baseline(O, A, b, G, model, P, n, m, K, seconds):
+    """The C oracle (a port of the reference forward, fp32, OpenMP over samples) on the host
+    cores, on a bounded sample of the same workload, scaled to ADMM-iters/s."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    with torch.no_grad():
+        table = model.hyp_table(K).cpu().numpy()
+    rng = np.random.default_rng(7)
+    Bs = 16
+    done_units, t_total = 0, 0.0
+    while t_total < seconds:
+        y0, U0, d0 = (1e-2 * rng.standard_normal((3, Bs, P, n))).astype(np.float32)
+        t0 = time.perf_counter()
+        O.forward_f32(A, b[:Bs].numpy(), [G] * Bs, table, y0, U0, d0)
+        dt = time.perf_counter() - t0
+        t_total += dt
+        done_units += Bs * K
+        if dt < 0.25 * seconds and Bs < b.shape[0]:
+            Bs = min(Bs * 2, b.shape[0])
+    return {"value": done_units / t_total, "unit": "ADMM-iters/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle_forward_f32 (C port of DLASSO_unfolded.forward, OpenMP over "
+                      f"samples) on {done_units // K} problems of the same shape, "
+                      f"{t_total:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

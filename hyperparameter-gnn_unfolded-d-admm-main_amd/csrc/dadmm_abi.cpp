@@ -1,0 +1,130 @@
+// dadmm_abi.cpp — the extern "C" boundary declared in include/dadmm.h.
+//
+// Validates arguments, picks the compiled kernel configuration and enqueues it. No allocation,
+// no synchronisation, no global mutable state (the error message is thread-local), so every
+// entry point can be captured into a hipGraph by the caller.
+
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/dadmm.h"
+#include "dadmm_internal.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int ok() {
+    g_err[0] = '\0';
+    return DADMM_OK;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int check_dims(const dadmm_dims* d) {
+    if (d == nullptr) return fail(DADMM_EINVAL, "dims is NULL");
+    if (d->B < 0 || d->P < 1 || d->m < 1 || d->n < 1 || d->K < 0)
+        return fail(DADMM_EINVAL, "bad dims B=%d P=%d m=%d n=%d K=%d", d->B, d->P, d->m, d->n,
+                    d->K);
+    if (d->P > 64) return fail(DADMM_EINVAL, "P=%d > 64 does not fit the uint64 neighbour mask", d->P);
+    if (d->variant != DADMM_VARIANT_UNFOLDED && d->variant != DADMM_VARIANT_GNN)
+        return fail(DADMM_EINVAL, "unknown variant %d", d->variant);
+    if (d->hyp_rows != 1 && d->hyp_rows != d->P)
+        return fail(DADMM_EINVAL, "hyp_rows=%d must be 1 ('same') or P=%d ('diff')", d->hyp_rows,
+                    d->P);
+    if (d->graph_shared != 0 && d->graph_shared != 1)
+        return fail(DADMM_EINVAL, "graph_shared must be 0 or 1");
+    return DADMM_OK;
+}
+
+int n_pad_of(const dadmm_dims* d) { return 64 * dadmm::fused_nt(d->n); }
+
+}  // namespace
+
+extern "C" {
+
+int dadmm_abi_version(void) { return DADMM_ABI_VERSION; }
+
+const char* dadmm_last_error(void) { return g_err; }
+
+size_t dadmm_operator_bytes(const dadmm_dims* d) {
+    if (check_dims(d) != DADMM_OK) return 0;
+    return 2 * sizeof(float) * (size_t)d->P * dadmm::M_PAD * (size_t)n_pad_of(d);
+}
+
+int dadmm_prepare_operator(const dadmm_dims* d, const float* A, void* op, void* stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (A == nullptr || op == nullptr) return fail(DADMM_EINVAL, "A/op is NULL");
+    if (!aligned16(op)) return fail(DADMM_EINVAL, "op workspace must be 16-byte aligned");
+    if (d->m > dadmm::M_PAD)
+        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
+                    dadmm::M_PAD);
+    const int np = n_pad_of(d);
+    float* Apad = (float*)op;
+    float* Atpad = Apad + (size_t)d->P * dadmm::M_PAD * np;
+    hipError_t e = dadmm::launch_prepare(A, Apad, Atpad, d->P, d->m, d->n, np, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "prepare launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
+                  const float* deg, const float* hyp, const float* y0, const float* U0,
+                  const float* d0, float* Y, float* U_out, int32_t* status, void* stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (d->B == 0 || d->K == 0) return ok();
+    if (!op || !b || !nbr || !deg || !hyp || !y0 || !U0 || !d0 || !Y)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(op)) return fail(DADMM_EINVAL, "op workspace must be 16-byte aligned");
+    if (!aligned16(Y) || !aligned16(y0) || !aligned16(U0) || !aligned16(d0) ||
+        (U_out != nullptr && !aligned16(U_out)))
+        return fail(DADMM_EINVAL, "Y, y0, U0, d0 and U_out must be 16-byte aligned");
+    if (d->m > dadmm::M_PAD)
+        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
+                    dadmm::M_PAD);
+    if ((d->n & 3) != 0)
+        return fail(DADMM_EUNSUPPORTED, "n=%d: the fused kernel needs n %% 4 == 0 (zero-pad n)", d->n);
+    if ((size_t)d->B * d->P * d->n * 4 >= ((size_t)1 << 31))
+        return fail(DADMM_EUNSUPPORTED, "B*P*n*4 >= 2^31 bytes per iterate (split the batch)");
+    const int nt = dadmm::fused_nt(d->n);
+    dadmm::fused_fn_ptr fn = dadmm::find_fused(d->P, nt, d->graph_shared != 0);
+    if (fn == nullptr)
+        return fail(DADMM_EUNSUPPORTED, "no fused kernel for P=%d n=%d (n_pad=%d)", d->P, d->n,
+                    64 * nt);
+    const int np = 64 * nt;
+    dadmm::FusedArgs a;
+    a.A = (const float*)op;
+    a.At = a.A + (size_t)d->P * dadmm::M_PAD * np;
+    a.b = b;
+    a.nbr = nbr;
+    a.deg = deg;
+    a.hyp = hyp;
+    a.y0 = y0;
+    a.U0 = U0;
+    a.d0 = d0;
+    a.Y = Y;
+    a.U_out = U_out;
+    a.status = status;
+    a.B = d->B;
+    a.m = d->m;
+    a.n = d->n;
+    a.K = d->K;
+    a.hyp_rows = d->hyp_rows;
+    a.variant = d->variant;
+    hipError_t e = fn(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "fused launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+}  // extern "C"

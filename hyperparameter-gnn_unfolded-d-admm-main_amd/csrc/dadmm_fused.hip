@@ -1,0 +1,499 @@
+// dadmm_fused.hip — fused K-iteration unfolded D-ADMM forward for gfx950 (MI355X).
+//
+// Reference semantics: unfolded_DLASSO.py:34-140 (DLASSO_unfolded.forward / compute_delta) and,
+// for the GNN variant, the fixed clamps of gnn_dlasso_models_progressive.py:205-232.
+//
+// Design:
+//   * one workgroup = BT = 16 problem instances ("samples") x all P agents x all K iterations;
+//     y_k and U_k never leave the CU: they live in VGPRs (lane = one sample and 4 rows of one
+//     16-row n-tile); y_k is mirrored into LDS as the B operand of the next gradient GEMM, and
+//     delta_k = 2 L y_k is recomputed from the y rows the lane already holds;
+//   * the primal gradient is factored, G_p = A_p^T (A_p y_p - b_p), as two f32 MFMA GEMMs with
+//     the batch as the N dimension (v_mfma_f32_16x16x4_f32: exact f32, one fma per product):
+//       GEMM1  R_p[64 x 16] = A_p[64 x n] . Y_p[n x 16] - b_p   (wave w: m-block w%4, agents
+//                                                                 w/4, w/4+2, ...)
+//       GEMM2  G_p[n x 16]  = A_p^T[n x 64] . R_p[64 x 16]       (wave w: n/8 rows, all agents)
+//     A_p and A_p^T (the prepared operator, 64 KB each per agent at n = 256) stream from L2;
+//   * the gradient assembly, clamps, primal update, the neighbour consensus delta = 2 L y (in the
+//     reference's accumulation order) and the dual update run on the GEMM2 accumulators in
+//     registers; each iterate is written to Y[k] exactly once, 16 B per lane.
+//
+// Reduction order (restated bit-for-bit by oracle/dadmm_oracle.c): every dot product is ONE fma
+// chain. Within each block of 16 reduction indices the chain visits 0,4,8,12, 1,5,9,13, 2,6,10,14,
+// 3,7,11,15 (4 MFMAs, each folding k = 4h + r for h = 0..3); blocks ascend; GEMM1's chain starts
+// from -b, GEMM2's from +0. Everything else is evaluated operation by operation like the
+// reference's torch eager ops (built with -ffp-contract=off: no fma outside the MFMA chains).
+//
+// Global memory goes through buffer descriptors: 32-bit per-lane offsets, and the hardware range
+// check returns 0 for loads / drops stores of the samples past B in the last workgroup.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dadmm_internal.h"
+
+namespace dadmm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore4(f32x4 v, rsrc_t r, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, voff, soff, 0);
+}
+
+// torch.clamp(x, lo, hi) == min(max(x, lo), hi) for every non-NaN x. A NaN never needs to be
+// propagated here: the kernel flags (status bits) every case in which a NaN would reach one of the
+// reference's guards, and the caller then re-runs the batch through the guarded path.
+__device__ __forceinline__ float tclamp(float x, float lo, float hi) {
+    return fminf(fmaxf(x, lo), hi);
+}
+// torch.sign for float: (0 < x) - (x < 0)
+__device__ __forceinline__ float tsign(float x) { return (float)((0.0f < x) - (x < 0.0f)); }
+__device__ __forceinline__ bool finitef(float x) { return __builtin_isfinite(x); }
+// Compiler-only memory barrier: bounds how far the scheduler hoists operand loads.
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
+// delta_p = 2 (L y)_p accumulated exactly as compute_delta (unfolded_DLASSO.py:127-140) does for
+// one sample: the agents' loops run p' = 0..P-1 over graph.neighbors(p') in ascending order,
+// each visit (p', q) doing delta[p'] += (y_p' - y_q); delta[q] -= (y_p' - y_q). Restricted to the
+// updates of delta[p], in order: every q < p with p in N(q) (-=), then p's own neighbours
+// (+=, a self-loop also takes its -= there), then every q > p with p in N(q) (-=).
+// `bit(q, p)` = p in N(q).
+template <int P, int E, typename BitFn>
+__device__ __forceinline__ void consensus(const float (&yy)[P][E], float (&dl)[P][E], BitFn bit) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        float acc[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = 0.0f;
+#pragma unroll
+        for (int q = 0; q < p; ++q)
+            if (bit(q, p)) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) acc[e] = acc[e] - (yy[q][e] - yy[p][e]);
+            }
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+            if (bit(p, q)) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    acc[e] = acc[e] + (yy[p][e] - yy[q][e]);
+                    if (q == p) acc[e] = acc[e] - (yy[p][e] - yy[p][e]);
+                }
+            }
+#pragma unroll
+        for (int q = p + 1; q < P; ++q)
+            if (bit(q, p)) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) acc[e] = acc[e] - (yy[q][e] - yy[p][e]);
+            }
+#pragma unroll
+        for (int e = 0; e < E; ++e) dl[p][e] = acc[e];
+    }
+}
+
+// Per-lane (per-sample graph) form: the conditional adds become selects.
+template <int P, int E>
+__device__ __forceinline__ void consensus_lane(const float (&yy)[P][E], float (&dl)[P][E],
+                                               const uint32_t (&msk)[P]) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        float acc[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = 0.0f;
+#pragma unroll
+        for (int q = 0; q < p; ++q) {
+            const bool on = (msk[q] >> p) & 1u;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float t = acc[e] - (yy[q][e] - yy[p][e]);
+                acc[e] = on ? t : acc[e];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const bool on = (msk[p] >> q) & 1u;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                float t = acc[e] + (yy[p][e] - yy[q][e]);
+                if (q == p) t = t - (yy[p][e] - yy[p][e]);
+                acc[e] = on ? t : acc[e];
+            }
+        }
+#pragma unroll
+        for (int q = p + 1; q < P; ++q) {
+            const bool on = (msk[q] >> p) & 1u;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float t = acc[e] - (yy[q][e] - yy[p][e]);
+                acc[e] = on ? t : acc[e];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) dl[p][e] = acc[e];
+    }
+}
+
+template <int P, int NT, bool SHARED_GRAPH>
+__global__ __launch_bounds__(WAVES * 64) void fused_forward_kernel(FusedArgs a) {
+    constexpr int MP = M_PAD;                        // padded m: 4 m-blocks of 16
+    constexpr int NP = NT * 64;                      // padded n
+    constexpr int NB = NP / 16;                      // 16-row n-tiles
+    constexpr int T2 = (NB + WAVES - 1) / WAVES;     // GEMM2 n-tiles per wave
+    constexpr int T1 = (P * 4 + WAVES - 1) / WAVES;  // GEMM1 (agent, m-block) tiles per wave
+    constexpr int E = T2 * 4;                        // state elements per lane per agent
+    constexpr int YS = NP + 4;                       // LDS row strides (floats): +16 B per row
+    constexpr int RS = MP + 4;                       //   breaks the power-of-two bank period
+    __shared__ __attribute__((aligned(16))) float lds[P * BT * (YS + RS)];
+    float* __restrict__ Ylds = lds;                  // [P][BT][YS]   y_k, n contiguous
+    float* __restrict__ Rlds = lds + P * BT * YS;    // [P][BT][RS]   A y - b, m contiguous
+
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave id, in an SGPR
+    const int j = lane & 15;             // sample within the tile (MFMA column)
+    const int h = lane >> 4;             // 4-row group within a 16-row tile
+    const int s0 = blockIdx.x * BT;
+    const int s = s0 + j;                // global sample index
+    const bool sv = s < a.B;
+    const int n = a.n, m = a.m, B = a.B;
+
+    // buffer descriptors (bounds = the tensor, so lanes past B read 0 and never store)
+    const uint32_t state_bytes = (uint32_t)((size_t)B * P * n * 4);
+    const rsrc_t rA = make_rsrc(a.A, (uint32_t)(P * MP * NP * 4));
+    const rsrc_t rAt = make_rsrc(a.At, (uint32_t)(P * MP * NP * 4));
+
+    // ---- graph data --------------------------------------------------------------------------
+    uint32_t msk[P];
+    float dg[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        if (SHARED_GRAPH) {
+            msk[p] = (uint32_t)a.nbr[p];       // kernel-uniform: scalar loads
+            dg[p] = a.deg[p];
+        } else {
+            msk[p] = sv ? (uint32_t)a.nbr[(size_t)s * P + p] : 0u;
+            dg[p] = sv ? a.deg[(size_t)s * P + p] : 0.0f;
+        }
+    }
+
+    // ---- state: this wave owns n-tiles nb = w*T2 + tt; element e = 4*tt + r is row
+    //      nb*16 + 4h + r -------------------------------------------------------------------------
+    float y[P][E], U[P][E];
+    {
+        const rsrc_t ry = make_rsrc(a.y0, state_bytes);
+        const rsrc_t ru = make_rsrc(a.U0, state_bytes);
+#pragma unroll
+        for (int tt = 0; tt < T2; ++tt) {
+            const int nb = w * T2 + tt;
+            const int n0 = nb * 16 + 4 * h;
+            const bool ok = nb < NB && n0 < n;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const uint32_t off = (uint32_t)(((s * P + p) * n + n0) * 4);
+                f32x4 vy = {0, 0, 0, 0}, vu = {0, 0, 0, 0};
+                if (ok) {
+                    vy = bload4(ry, off, 0);
+                    vu = bload4(ru, off, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    y[p][4 * tt + r] = vy[r];
+                    U[p][4 * tt + r] = vu[r];
+                }
+                if (nb < NB) *(f32x4*)(Ylds + (p * BT + j) * YS + n0) = vy;
+            }
+        }
+    }
+    // GEMM1 tiles of this wave: t1 = w + WAVES*i -> agent t1/4, m-block t1%4 = w%4;
+    // b rows m = 16*(w%4) + 4h + r
+    const int mb = w & 3;
+    float bb[T1][4];
+#pragma unroll
+    for (int i = 0; i < T1; ++i) {
+        const int p = (w + WAVES * i) >> 2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int mi = 16 * mb + 4 * h + r;
+            bb[i][r] = (sv && p < P && mi < m) ? a.b[((size_t)s * P + p) * m + mi] : 0.0f;
+        }
+    }
+
+    // Reference guards at the top of an iteration (unfolded_DLASSO.py:55-61) can only fire at
+    // k = 0: with finite y_k, U_k, hyp and no NaN gradient every later y_k, U_k is finite (all
+    // terms are clamped), and a NaN gradient is flagged where it arises.
+    uint32_t status = 0;
+    {
+        bool bad_y = false, bad_u = false;
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                bad_y |= !finitef(y[p][e]);
+                bad_u |= !finitef(U[p][e]);
+            }
+        status |= (bad_y ? 1u : 0u) | (bad_u ? 2u : 0u);
+    }
+    __syncthreads();
+
+    // per-lane byte offsets into the operator and the output
+    const uint32_t voffA = (uint32_t)(((16 * mb + j) * NP + 4 * h) * 4);   // + p*MP*NP*4 + 64*t
+    const uint32_t voffAt = (uint32_t)((j * MP + 4 * h) * 4);             // + (p*NP+16nb)*MP*4 + 64*t
+    const uint32_t voffY = (uint32_t)((s * P * n + 4 * h) * 4);           // + (p*n + nb*16)*4
+
+    for (int k = 0; k < a.K; ++k) {
+        // seq_hyp(k) row(s): (alpha, tau, rho, eta) — kernel-uniform scalars
+        float al[P], ta[P], rh[P], et[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const float* hp = a.hyp + ((size_t)k * a.hyp_rows + (a.hyp_rows == 1 ? 0 : p)) * 4;
+            al[p] = hp[0]; ta[p] = hp[1]; rh[p] = hp[2]; et[p] = hp[3];
+        }
+        float gclip, vclip;
+        if (a.variant == 0) {
+            gclip = fmaxf(1.0f, 30.0f - (float)k);          // unfolded_DLASSO.py:80
+            vclip = fmaxf(10.0f, 200.0f - (float)(k * 3));  // unfolded_DLASSO.py:92
+        } else {
+            gclip = 10.0f;                                   // gnn_dlasso_models_progressive.py:212
+            vclip = 100.0f;                                  // :224, :232
+        }
+
+        // A non-finite hyper-parameter makes y_next NaN (reference guard :102); flag it.
+        {
+            bool bad_h = false;
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+                bad_h |= !(finitef(al[p]) && finitef(ta[p]) && finitef(rh[p]) && finitef(et[p]));
+            status |= bad_h ? 8u : 0u;
+        }
+
+        // ---- GEMM1: R_p = A_p y_p - b_p  (this wave's (agent, m-block) tiles) ------------------
+        // A rows are prefetched one 16-column block ahead; the compiler fence keeps the scheduler
+        // from hoisting further (it would otherwise spill the state registers).
+        {
+            f32x4 acc[T1], ac[T1], an[T1];
+            const float* brow = Ylds + j * YS + 4 * h;
+#pragma unroll
+            for (int i = 0; i < T1; ++i) {
+                acc[i] = (f32x4){-bb[i][0], -bb[i][1], -bb[i][2], -bb[i][3]};
+                const int p = (w + WAVES * i) >> 2;
+                if (p < P) ac[i] = bload4(rA, voffA, (uint32_t)(p * MP * NP * 4));
+            }
+#pragma unroll 1
+            for (int t = 0; t < NB; ++t) {
+                if (t + 1 < NB) {
+#pragma unroll
+                    for (int i = 0; i < T1; ++i) {
+                        const int p = (w + WAVES * i) >> 2;
+                        if (p < P) an[i] = bload4(rA, voffA, (uint32_t)(p * MP * NP * 4 + 64 * (t + 1)));
+                    }
+                }
+                compiler_fence();
+#pragma unroll
+                for (int i = 0; i < T1; ++i) {
+                    const int p = (w + WAVES * i) >> 2;
+                    if (p < P) {
+                        const f32x4 bv = *(const f32x4*)(brow + p * BT * YS + 16 * t);
+                        acc[i] = mfma4(ac[i][0], bv[0], acc[i]);
+                        acc[i] = mfma4(ac[i][1], bv[1], acc[i]);
+                        acc[i] = mfma4(ac[i][2], bv[2], acc[i]);
+                        acc[i] = mfma4(ac[i][3], bv[3], acc[i]);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < T1; ++i) ac[i] = an[i];
+            }
+#pragma unroll
+            for (int i = 0; i < T1; ++i) {
+                const int p = (w + WAVES * i) >> 2;
+                if (p < P) *(f32x4*)(Rlds + (p * BT + j) * RS + 16 * mb + 4 * h) = acc[i];
+            }
+        }
+        __syncthreads();
+
+        // ---- GEMM2 + gradient assembly + primal update + consensus + dual update, tile-major ----
+        // For each of this wave's 16-row n-tiles: G_p for every agent, then (lane-local: the lane
+        // holds the same 4 rows of every agent) delta_k = 2 L y_k from the rows' y_k (k = 0: the
+        // caller's d0), the primal update, delta_{k+1} = 2 L y_{k+1} and the dual update. delta
+        // is recomputed rather than carried: that frees P*4*T2 registers per lane.
+        const rsrc_t rY = make_rsrc(a.Y + (size_t)k * B * P * n, state_bytes);
+        f32x4 gc[MP / 16], gn[MP / 16];
+        if (w * T2 < NB) {
+#pragma unroll
+            for (int t = 0; t < MP / 16; ++t)
+                gc[t] = bload4(rAt, voffAt, (uint32_t)((16 * (w * T2)) * MP * 4 + 64 * t));
+        }
+#pragma unroll
+        for (int tt = 0; tt < T2; ++tt) {
+            const int nb = w * T2 + tt;
+            if (nb >= NB) continue;
+            const int n0 = nb * 16 + 4 * h;
+            f32x4 g[P];
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                // prefetch the next step: (p+1, tt) or (0, tt+1)
+                const int pn = (p + 1 < P) ? p + 1 : 0;
+                const int nbn = (p + 1 < P) ? nb : nb + 1;
+                if ((p + 1 < P || tt + 1 < T2) && nbn < NB) {
+#pragma unroll
+                    for (int t = 0; t < MP / 16; ++t)
+                        gn[t] = bload4(rAt, voffAt, (uint32_t)((pn * NP + 16 * nbn) * MP * 4 + 64 * t));
+                }
+                compiler_fence();
+                const float* rrow = Rlds + (p * BT + j) * RS + 4 * h;
+                g[p] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int t = 0; t < MP / 16; ++t) {
+                    const f32x4 bv = *(const f32x4*)(rrow + 16 * t);
+                    g[p] = mfma4(gc[t][0], bv[0], g[p]);
+                    g[p] = mfma4(gc[t][1], bv[1], g[p]);
+                    g[p] = mfma4(gc[t][2], bv[2], g[p]);
+                    g[p] = mfma4(gc[t][3], bv[3], g[p]);
+                }
+#pragma unroll
+                for (int t = 0; t < MP / 16; ++t) gc[t] = gn[t];
+            }
+
+            // delta_k for these rows
+            float yr[P][4], dr[P][4];
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) yr[p][r] = y[p][4 * tt + r];
+            if (k == 0) {
+                const rsrc_t rd = make_rsrc(a.d0, state_bytes);
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const f32x4 v = bload4(rd, (uint32_t)(((s * P + p) * n + n0) * 4), 0);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dr[p][r] = v[r];
+                }
+            } else {
+                if (SHARED_GRAPH)
+                    consensus<P, 4>(yr, dr, [&](int q, int p) { return ((msk[q] >> p) & 1u) != 0; });
+                else
+                    consensus_lane<P, 4>(yr, dr, msk);
+                if (a.variant != 0) {
+#pragma unroll
+                    for (int p = 0; p < P; ++p)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) dr[p][r] = tclamp(dr[p][r], -20.0f, 20.0f);  // GNN :229
+                }
+            }
+
+            // primal update
+            bool bad_g = false;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                f32x4 yn;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int e = 4 * tt + r;
+                    const float yv = yr[p][r];
+                    // grad = (AtAy - Atb) + sign(y)*tau + U*deg + delta*rho  (:73-77)
+                    float gr = g[p][r];
+                    gr = gr + tsign(yv) * ta[p];
+                    gr = gr + U[p][e] * dg[p];
+                    gr = gr + dr[p][r] * rh[p];
+                    bad_g |= (gr != gr);                            // :84 guard (flag only)
+                    gr = tclamp(gr, -gclip, gclip);                 // :80-81
+                    float v = yv - al[p] * gr;                      // :89
+                    v = tclamp(v, -vclip, vclip);                   // :92-93
+                    y[p][e] = v;
+                    yr[p][r] = v;
+                    yn[r] = v;
+                }
+                *(f32x4*)(Ylds + (p * BT + j) * YS + n0) = yn;
+                if (n0 < n) bstore4(yn, rY, voffY, (uint32_t)((p * n + nb * 16) * 4));  // Y[k][s][p][n0..+3]
+            }
+            status |= bad_g ? 4u : 0u;
+
+            // delta_{k+1} = 2 L y_{k+1} (:95) and the dual update (:98-99)
+            if (SHARED_GRAPH)
+                consensus<P, 4>(yr, dr, [&](int q, int p) { return ((msk[q] >> p) & 1u) != 0; });
+            else
+                consensus_lane<P, 4>(yr, dr, msk);
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float d = dr[p][r];
+                    if (a.variant != 0) d = tclamp(d, -20.0f, 20.0f);  // GNN :229
+                    U[p][4 * tt + r] = tclamp(U[p][4 * tt + r] + d * et[p], -vclip, vclip);
+                }
+        }
+        __syncthreads();
+    }
+
+    if (a.U_out != nullptr) {
+        const rsrc_t rU = make_rsrc(a.U_out, state_bytes);
+#pragma unroll
+        for (int tt = 0; tt < T2; ++tt) {
+            const int nb = w * T2 + tt;
+            const int n0 = nb * 16 + 4 * h;
+            if (nb < NB && n0 < n) {
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const f32x4 v = {U[p][4 * tt], U[p][4 * tt + 1], U[p][4 * tt + 2], U[p][4 * tt + 3]};
+                    bstore4(v, rU, (uint32_t)(((s * P + p) * n + n0) * 4), 0);
+                }
+            }
+        }
+    }
+    if (a.status != nullptr) {
+        // lanes past B carry zero state and never set a bit; one atomic per wave
+        uint32_t wst = status;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) wst |= __shfl_xor(wst, off);
+        if (lane == 0 && wst) atomicOr((unsigned int*)a.status, wst);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+template <int P, int NT, bool SG>
+static hipError_t launch_fused(const FusedArgs& a, hipStream_t stream) {
+    const int grid = (a.B + BT - 1) / BT;
+    hipLaunchKernelGGL((fused_forward_kernel<P, NT, SG>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+    return hipGetLastError();
+}
+
+template <int P, int NT>
+static fused_fn_ptr pick_sg(bool sg) {
+    return sg ? &launch_fused<P, NT, true> : &launch_fused<P, NT, false>;
+}
+
+// Instantiated shapes: P = 1..6, n_pad = 64 * NT with NT in {1, 2, 4} (NT = 4 only for P <= 5:
+// the register budget of 2 waves per SIMD), m_pad = 64.
+template <int P>
+static fused_fn_ptr pick_nt(int nt, bool sg) {
+    if (nt == 1) return pick_sg<P, 1>(sg);
+    if (nt == 2) return pick_sg<P, 2>(sg);
+    if constexpr (P <= 5) {
+        if (nt == 4) return pick_sg<P, 4>(sg);
+    }
+    return nullptr;
+}
+
+fused_fn_ptr find_fused(int P, int nt, bool shared_graph) {
+    switch (P) {
+        case 1: return pick_nt<1>(nt, shared_graph);
+        case 2: return pick_nt<2>(nt, shared_graph);
+        case 3: return pick_nt<3>(nt, shared_graph);
+        case 4: return pick_nt<4>(nt, shared_graph);
+        case 5: return pick_nt<5>(nt, shared_graph);
+        case 6: return pick_nt<6>(nt, shared_graph);
+        default: return nullptr;
+    }
+}
+
+}  // namespace dadmm

@@ -1,0 +1,80 @@
+"""ctypes binding of ``libdadmm.so`` (the C ABI declared in ``include/dadmm.h``).
+
+The library is built in-tree by ``csrc/Makefile`` (``__graft_entry__.build()``). There is no
+fallback: if the library is missing or cannot be loaded, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdadmm.so")
+
+ABI_VERSION = 1
+DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
+VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
+STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
+
+# every symbol include/dadmm.h declares
+EXPORTED_SYMBOLS = (
+    "dadmm_abi_version",
+    "dadmm_last_error",
+    "dadmm_operator_bytes",
+    "dadmm_prepare_operator",
+    "dadmm_forward",
+)
+
+
+class DadmmError(RuntimeError):
+    """A C-ABI call returned a non-zero code."""
+
+    def __init__(self, func: str, code: int, msg: str):
+        super().__init__(f"{func} failed ({code}): {msg}")
+        self.code = code
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("P", ctypes.c_int32), ("m", ctypes.c_int32),
+        ("n", ctypes.c_int32), ("K", ctypes.c_int32), ("variant", ctypes.c_int32),
+        ("hyp_rows", ctypes.c_int32), ("graph_shared", ctypes.c_int32),
+    ]
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libdadmm.so once; raises if it is absent (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the HIP library first (python -c "
+            "'import __graft_entry__ as g; g.build()' or make -C csrc)")
+    # torch (if imported) has already loaded its libamdhip64.so.7; the dynamic linker resolves
+    # this library's DT_NEEDED entry to that same runtime by soname.
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    L.dadmm_abi_version.restype = ctypes.c_int
+    L.dadmm_abi_version.argtypes = []
+    L.dadmm_last_error.restype = ctypes.c_char_p
+    L.dadmm_last_error.argtypes = []
+    L.dadmm_operator_bytes.restype = ctypes.c_size_t
+    L.dadmm_operator_bytes.argtypes = [ctypes.POINTER(Dims)]
+    L.dadmm_prepare_operator.restype = ctypes.c_int
+    L.dadmm_prepare_operator.argtypes = [ctypes.POINTER(Dims), vp, vp, vp]
+    L.dadmm_forward.restype = ctypes.c_int
+    L.dadmm_forward.argtypes = [ctypes.POINTER(Dims)] + [vp] * 12
+    v = L.dadmm_abi_version()
+    if v != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI version {v}, expected {ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(func: str, rc: int) -> None:
+    if rc != DADMM_OK:
+        raise DadmmError(func, rc, load().dadmm_last_error().decode(errors="replace"))

@@ -1,0 +1,225 @@
+"""Python side of the CPU oracle (TEST INFRASTRUCTURE ONLY — see ``oracle/__init__.py``).
+
+Restates, from the reference source text:
+  * ``seq_hyperparam.forward``                       unfolded_DLASSO.py:156-168   -> hyp_table()
+  * ``DLASSO_unfolded.compute_sum_neighbors``        unfolded_DLASSO.py:111-118   -> graph_arrays()
+  * ``DLASSO_unfolded.forward`` + ``compute_delta``  unfolded_DLASSO.py:34-140    -> forward_f32/_f64
+    (C: oracle/dadmm_oracle.c), and a vectorised numpy fp64 form (forward_np64) used as an
+    independent second restatement
+  * ``gnn_dlasso_utils.compute_loss``                gnn_dlasso_utils.py:27-88    -> compute_loss()
+  * ``gnn_dlasso_utils.set_A`` / ``gnn_data.set_Data`` (input distribution)       -> make_problem()
+  * reading the reference's shipped fixtures (A.pt, model.pt) without unpickling  -> load_fixture()
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import zipfile
+
+import numpy as np
+
+__all__ = [
+    "lib", "hyp_table", "graph_arrays", "forward_f32", "forward_f64", "forward_np64",
+    "compute_loss", "make_problem", "load_fixture_tensor", "er_graph", "connected_er_graph",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (building if needed, in this container only) ``oracle/liboracle.so``."""
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.run(["make", "-C", _HERE], check=True, capture_output=True)
+        L = ctypes.CDLL(path)
+        fp = ctypes.c_void_p
+        i = ctypes.c_int
+        for name in ("oracle_forward_f32", "oracle_forward_f64"):
+            f = getattr(L, name)
+            f.restype = ctypes.c_int
+            f.argtypes = [i, i, i, i, i, i, i, i] + [fp] * 12
+        L.oracle_abi_version.restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+# --------------------------------------------------------------------------------------------
+def hyp_table(param, max_param, training=False, threshold=0.8, factor=0.95, dtype=np.float32):
+    """All K rows of seq_hyperparam(k) (unfolded_DLASSO.py:156-168) -> [K, H, 4].
+
+    hyp_k = clamp(sigmoid(sum_{i<=k} param[i]) * max_param, 1e-4, 0.99); in training mode, if the
+    mean of hyp_k over (H, 4) exceeds ``threshold`` the row is multiplied by ``factor`` first.
+    """
+    param = np.asarray(param, dtype=dtype)
+    mx = np.asarray(max_param, dtype=dtype).reshape(1, 4)
+    out = []
+    for k in range(param.shape[0]):
+        s = param[: k + 1].sum(axis=0, dtype=dtype)          # torch.sum(param[:k+1], dim=0)
+        h = (1.0 / (1.0 + np.exp(-s))).astype(dtype) * mx     # sigmoid * max_param
+        if training and h.sum() / (h.shape[0] * h.shape[1]) > threshold:
+            h = h * dtype(factor)
+        out.append(np.clip(h, dtype(1e-4), dtype(0.99)))
+    return np.stack(out).astype(dtype)
+
+
+def graph_arrays(graph_list, P):
+    """Neighbour lists in adjacency order (CSR) and compute_sum_neighbors degrees.
+
+    Returns (nbr_ptr int32 [B*P+1], nbr_idx int32 [E], deg float32 [B, P]); the lists follow
+    ``graph.neighbors(p)`` order, exactly what compute_delta iterates (unfolded_DLASSO.py:136).
+    """
+    ptr, idx = [0], []
+    deg = np.zeros((len(graph_list), P), np.float32)
+    for s, G in enumerate(graph_list):
+        for p in range(P):
+            nb = list(G.neighbors(p))
+            deg[s, p] = len(nb)
+            idx.extend(nb)
+            ptr.append(len(idx))
+    return np.asarray(ptr, np.int32), np.asarray(idx if idx else [0], np.int32), deg
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def _run(fn, out_dt, A, b, graph_list, hyp, y0, U0, d0, variant, hyp_mode):
+    A = _c(A, np.float32).reshape(A.shape[-3:]) if A.ndim == 4 else _c(A, np.float32)
+    P, m, n = A.shape
+    B = y0.shape[0]
+    K = hyp.shape[0]
+    H = hyp.shape[-1] if hyp_mode == 1 else hyp.shape[1]
+    nbr_ptr, nbr_idx, deg = graph_arrays(graph_list, P)
+    b = _c(b, np.float32).reshape(B, P, m)
+    y0, U0, d0 = (_c(x, np.float32).reshape(B, P, n) for x in (y0, U0, d0))
+    hyp = _c(hyp, np.float32)
+    Y = np.empty((K, B, P, n), out_dt)
+    U = np.empty((B, P, n), out_dt)
+    st = np.zeros(1, np.int32)
+    rc = fn(B, P, m, n, K, variant, hyp_mode, H, _ptr(A), _ptr(b), _ptr(nbr_ptr), _ptr(nbr_idx),
+            _ptr(deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U), _ptr(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle returned {rc}")
+    return Y, U, int(st[0])
+
+
+def forward_f32(A, b, graph_list, hyp, y0, U0, d0, variant=0, hyp_mode=0):
+    """Order-matched fp32 restatement (bit-exact target of the HIP kernel).
+
+    Returns (Y [K,B,P,n] float32, U_K [B,P,n] float32, guard status bits)."""
+    return _run(lib().oracle_forward_f32, np.float32, A, b, graph_list, hyp, y0, U0, d0, variant,
+                hyp_mode)
+
+
+def forward_f64(A, b, graph_list, hyp, y0, U0, d0, variant=0, hyp_mode=0):
+    """The reference's algorithm (Gram form) in double precision. Same return layout, float64."""
+    return _run(lib().oracle_forward_f64, np.float64, A, b, graph_list, hyp, y0, U0, d0, variant,
+                hyp_mode)
+
+
+def forward_np64(A, b, graph_list, hyp, y0, U0, d0, variant=0):
+    """Independent vectorised fp64 restatement (Gram form, Laplacian as a matrix, no guards).
+
+    delta = 2 (D - Adj) y holds for every nx.Graph (each undirected edge is visited from both
+    ends in compute_delta, unfolded_DLASSO.py:132-139)."""
+    A = np.asarray(A, np.float64).reshape(np.shape(A)[-3:])
+    P, m, n = A.shape
+    B = y0.shape[0]
+    AtA = np.einsum("pri,prj->pij", A, A)
+    Atb = np.einsum("pri,bpr->bpi", A, np.asarray(b, np.float64).reshape(B, P, m))
+    L = np.zeros((B, P, P))
+    deg = np.zeros((B, P))
+    for s, G in enumerate(graph_list):
+        for p in range(P):
+            for q in G.neighbors(p):
+                L[s, p, q] -= 1.0
+                deg[s, p] += 1.0
+        L[s] += np.diag(deg[s])
+    y = np.asarray(y0, np.float64).reshape(B, P, n)
+    U = np.asarray(U0, np.float64).reshape(B, P, n)
+    d = np.asarray(d0, np.float64).reshape(B, P, n)
+    hyp = np.asarray(hyp, np.float64)
+    Y = []
+    for k in range(hyp.shape[0]):
+        al, ta, rh, et = (hyp[k][:, c][None, :, None] for c in range(4))
+        gclip = max(1.0, 30.0 - k) if variant == 0 else 10.0
+        vclip = max(10.0, 200.0 - 3 * k) if variant == 0 else 100.0
+        g = np.einsum("pij,bpj->bpi", AtA, y) - Atb + np.sign(y) * ta + U * deg[:, :, None] + d * rh
+        g = np.clip(g, -gclip, gclip)
+        yn = np.clip(y - al * g, -vclip, vclip)
+        d = 2.0 * np.einsum("bpq,bqi->bpi", L, yn)
+        if variant != 0:
+            d = np.clip(d, -20.0, 20.0)
+        U = np.clip(U + d * et, -vclip, vclip)
+        y = yn
+        Y.append(y)
+    return np.stack(Y), U
+
+
+def compute_loss(Y, label):
+    """gnn_dlasso_utils.compute_loss (:27-88) in float64: (mean_k loss_k + 1e-8, loss_{K-1} + 1e-8)
+    with loss_k = mean_p mean_{b,n} (Y[k,b,p,n] - label[b,n])^2, and (1, 1) on any NaN/Inf."""
+    Y = np.asarray(Y, np.float64)
+    K, B, P, n = Y.shape[:4]
+    Y = Y.reshape(K, B, P, n)
+    label = np.asarray(label, np.float64).reshape(B, n)
+    if not np.isfinite(Y).all() or not np.isfinite(label).all():
+        return 1.0, 1.0
+    losses = ((Y - label[None, :, None, :]) ** 2).mean(axis=(1, 3)).mean(axis=1)
+    if not np.isfinite(losses).all():
+        return 1.0, 1.0
+    return float(losses.mean() + 1e-8), float(losses[-1] + 1e-8)
+
+
+# --------------------------------------------------------------------------------------------
+def er_graph(P, prob, seed):
+    """nx.erdos_renyi_graph(P, prob, seed) (unfolded_train_new.py:56)."""
+    import networkx as nx
+    return nx.erdos_renyi_graph(P, prob, seed=seed)
+
+
+def connected_er_graph(P, prob, seed):
+    """The per-sample graph of gnn_dlasso_progressive.py:181-191 (ER with max(prob, 0.3), then
+    components chained by one edge each)."""
+    import networkx as nx
+    G = nx.erdos_renyi_graph(P, max(prob, 0.3), seed=seed)
+    if not nx.is_connected(G):
+        comps = list(nx.connected_components(G))
+        for i in range(len(comps) - 1):
+            G.add_edge(list(comps[i])[0], list(comps[i + 1])[0])
+    return G
+
+
+def make_problem(P, m, n, B, seed=1234):
+    """Synthetic inputs with the reference's distribution (gnn_dlasso_utils.py:4-16,
+    gnn_data.py:6-15): per-agent A_p = U clamp(S, 0.1, 10) V^T of a Gaussian, x* = 2 N(0,1) *
+    Bernoulli(0.25), b_p = A_p x* (noise-free: the noisy b is overwritten, gnn_data.py:13-14).
+    Returns float32 arrays A [P,m,n], b [B,P,m], x [B,n]."""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    A = torch.zeros(P, m, n)
+    for p in range(P):
+        T = torch.randn(m, n, generator=g)
+        Us, S, V = torch.svd(T)
+        A[p] = Us @ torch.diag(S.clamp(0.1, 10.0)) @ V.T
+    x = 2 * torch.randn(B, n, generator=g) * (torch.rand(B, n, generator=g) <= 0.25)
+    b = torch.einsum("pmn,bn->bpm", A, x)
+    return A.numpy(), b.numpy(), x.numpy()
+
+
+def load_fixture_tensor(path):
+    """Read the single fp32 storage of a shipped reference ``.pt`` (A.pt / model.pt) as a flat
+    float32 array, by reading the zip member ``*/data/0`` — nothing is unpickled."""
+    with zipfile.ZipFile(path) as z:
+        names = [x for x in z.namelist() if x.endswith("/data/0")]
+        if len(names) != 1:
+            raise ValueError(f"{path}: expected one storage, found {names}")
+        return np.frombuffer(z.read(names[0]), dtype="<f4").copy()
