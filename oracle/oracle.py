@@ -97,7 +97,12 @@ def _run(fn, out_dt, A, b, graph_list, hyp, y0, U0, d0, variant, hyp_mode):
     B = y0.shape[0]
     K = hyp.shape[0]
     H = hyp.shape[-1] if hyp_mode == 1 else hyp.shape[1]
-    nbr_ptr, nbr_idx, deg = graph_arrays(graph_list, P)
+    if isinstance(graph_list, tuple) and len(graph_list) == 3:   # precomputed CSR (goldens)
+        nbr_ptr, nbr_idx, deg = (np.ascontiguousarray(v) for v in graph_list)
+        nbr_ptr, nbr_idx = nbr_ptr.astype(np.int32), nbr_idx.astype(np.int32)
+        deg = deg.astype(np.float32)
+    else:
+        nbr_ptr, nbr_idx, deg = graph_arrays(graph_list, P)
     b = _c(b, np.float32).reshape(B, P, m)
     y0, U0, d0 = (_c(x, np.float32).reshape(B, P, n) for x in (y0, U0, d0))
     hyp = _c(hyp, np.float32)
@@ -113,6 +118,8 @@ def _run(fn, out_dt, A, b, graph_list, hyp, y0, U0, d0, variant, hyp_mode):
 
 def forward_f32(A, b, graph_list, hyp, y0, U0, d0, variant=0, hyp_mode=0):
     """Order-matched fp32 restatement (bit-exact target of the HIP kernel).
+
+    ``graph_list``: B networkx graphs, or a (nbr_ptr, nbr_idx, deg) CSR tuple (graph_arrays).
 
     Returns (Y [K,B,P,n] float32, U_K [B,P,n] float32, guard status bits)."""
     return _run(lib().oracle_forward_f32, np.float32, A, b, graph_list, hyp, y0, U0, d0, variant,

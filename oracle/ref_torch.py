@@ -1,0 +1,87 @@
+"""Literal torch restatement of the reference forward (TEST INFRASTRUCTURE ONLY).
+
+Replays the reference's exact op sequence with torch eager ops on the CPU — compute_Atx via
+per-agent ``torch.matmul(A[0,p].T, x[:,p])`` (unfolded_DLASSO.py:120-124), the Gram matrix AtA
+(:16), the per-agent ``AtA[0,p] @ y[:,p]`` GEMVs (:69-71), the gradient/clamp/update expressions
+(:73-99), the Python edge loop of compute_delta (:127-140) and the guards (:55-61, :84-86,
+:102-104) — so, with the same torch build, it computes what the reference's own fp32 CPU forward
+computes. It is the "reference-form fp32" control for the tolerance tests and the CPU-baseline
+leg that reproduces the reference's cost profile. It never imports the reference.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+
+def _atx(A, x):
+    # compute_Atx: [B,P,n,c] = A_p^T x_p, one matmul per agent
+    P, n = A.shape[1], A.shape[3]
+    out = torch.zeros((x.shape[0], P, n, x.shape[3]), dtype=x.dtype)
+    for p in range(P):
+        out[:, p] = torch.matmul(A[0, p].T, x[:, p])
+    return out
+
+
+def _delta(graph_list, y, P):
+    d = torch.zeros_like(y)
+    for s in range(len(graph_list)):
+        G = graph_list[s]
+        for p in range(P):
+            yp = y[s, p]
+            for q in G.neighbors(p):
+                diff = yp - y[s, q]
+                d[s, p] += diff
+                d[s, q] -= diff
+    return d
+
+
+def forward(A, b, graph_list, hyp, y0, U0, d0, variant=0, dtype=torch.float32):
+    """A [P,m,n] or [1,P,m,n]; b [B,P,m]; hyp [K,H,4] (rows of seq_hyp); y0/U0/d0 [B,P,n].
+
+    Returns Y [K,B,P,n] as numpy (dtype of the computation)."""
+    A = torch.as_tensor(np.asarray(A), dtype=dtype)
+    if A.dim() == 3:
+        A = A[None]
+    _, P, m, n = A.shape
+    B = y0.shape[0]
+    b = torch.as_tensor(np.asarray(b), dtype=dtype).reshape(B, P, m, 1)
+    hyp = torch.as_tensor(np.asarray(hyp), dtype=dtype)
+    AtA = torch.zeros((1, P, n, n), dtype=dtype)
+    for p in range(P):
+        AtA[0, p] = torch.matmul(A[0, p].T, A[0, p])
+    Atb = _atx(A, b)
+    deg = torch.zeros((B, P, 1, 1), dtype=dtype)
+    for s in range(B):
+        for p in range(P):
+            deg[s, p] = len(list(graph_list[s].neighbors(p)))
+    y = torch.as_tensor(np.asarray(y0), dtype=dtype).reshape(B, P, n, 1).clone()
+    U = torch.as_tensor(np.asarray(U0), dtype=dtype).reshape(B, P, n, 1).clone()
+    d = torch.as_tensor(np.asarray(d0), dtype=dtype).reshape(B, P, n, 1).clone()
+    Y = []
+    for k in range(hyp.shape[0]):
+        if torch.isnan(y).any() or torch.isinf(y).any():
+            y = torch.zeros_like(y)
+        if torch.isnan(U).any() or torch.isinf(U).any():
+            U = torch.zeros_like(U)
+        h = hyp[k]
+        al, ta, rh, et = (h[:, c].reshape(1, -1, 1, 1) for c in range(4))
+        AtAy = torch.zeros((B, P, n, 1), dtype=dtype)
+        for p in range(P):
+            AtAy[:, p] = torch.matmul(AtA[0, p], y[:, p])
+        grad = AtAy - Atb + y.sign() * ta + U * deg + d * rh
+        gclip = max(1.0, 30.0 - k) if variant == 0 else 10.0
+        vclip = max(10.0, 200.0 - k * 3) if variant == 0 else 100.0
+        grad = torch.clamp(grad, -gclip, gclip)
+        if torch.isnan(grad).any() or torch.isinf(grad).any():
+            grad = torch.zeros_like(grad)
+        yn = torch.clamp(y - al * grad, -vclip, vclip)
+        d = _delta(graph_list, yn, P)
+        if variant != 0:
+            d = torch.clamp(d, -20.0, 20.0)
+        U = torch.clamp(U + d * et, -vclip, vclip)
+        if torch.isnan(yn).any() or torch.isinf(yn).any():
+            yn = y
+        y = yn
+        Y.append(y)
+    return torch.stack(Y)[..., 0].numpy()

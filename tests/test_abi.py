@@ -1,0 +1,98 @@
+"""CPU: the C-ABI library loads, exports every symbol include/dadmm.h declares, and validates its
+arguments before touching the GPU (no kernel is launched by these tests)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dadmm.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dadmm_[a-z_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    from dadmm_hip import _lib
+    return _lib.load()
+
+
+def test_header_and_binding_agree():
+    from dadmm_hip import _lib
+    assert _declared() == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_every_declared_symbol_is_exported(L):
+    for name in _declared():
+        assert hasattr(L, name), name
+
+
+def test_abi_version(L):
+    from dadmm_hip import _lib
+    assert L.dadmm_abi_version() == _lib.ABI_VERSION
+
+
+def _dims(**kw):
+    from dadmm_hip import _lib
+    d = dict(B=8, P=5, m=64, n=256, K=25, variant=0, hyp_rows=5, graph_shared=1)
+    d.update(kw)
+    return _lib.Dims(**d)
+
+
+def test_operator_bytes(L):
+    d = _dims()
+    assert L.dadmm_operator_bytes(ctypes.byref(d)) == 2 * 4 * 5 * 64 * 256
+    d = _dims(n=200)
+    assert L.dadmm_operator_bytes(ctypes.byref(d)) == 2 * 4 * 5 * 64 * 256   # n padded to 256
+    d = _dims(P=0)
+    assert L.dadmm_operator_bytes(ctypes.byref(d)) == 0
+
+
+FAKE = [ctypes.c_void_p(0x10000 * (i + 1)) for i in range(12)]   # 16-B aligned, never touched
+
+
+def _fwd(L, d):
+    return L.dadmm_forward(ctypes.byref(d), *FAKE, None)
+
+
+@pytest.mark.parametrize("kw,code", [
+    (dict(P=0), -1), (dict(P=65), -1), (dict(m=0), -1), (dict(n=-3), -1), (dict(K=-1), -1),
+    (dict(variant=2), -1), (dict(hyp_rows=3), -1), (dict(graph_shared=2), -1),
+    (dict(m=65), -2), (dict(n=258), -2), (dict(P=7, n=64, hyp_rows=1), -2),
+    (dict(P=6, n=256, hyp_rows=6), -2),
+    (dict(n=512), -2), (dict(B=1 << 20, n=256), -2),
+])
+def test_forward_rejects_before_launch(L, kw, code):
+    d = _dims(**kw)
+    assert _fwd(L, d) == code
+    assert L.dadmm_last_error().decode()
+
+
+def test_forward_empty_work_is_ok(L):
+    assert _fwd(L, _dims(B=0)) == 0
+    assert _fwd(L, _dims(K=0)) == 0
+    assert L.dadmm_last_error().decode() == ""
+
+
+def test_forward_null_and_misaligned_pointers(L):
+    d = _dims()
+    args = list(FAKE)
+    args[1] = None        # b
+    assert L.dadmm_forward(ctypes.byref(d), *args, None) == -1
+    args = list(FAKE)
+    args[9] = ctypes.c_void_p(0x10004)   # Y misaligned
+    assert L.dadmm_forward(ctypes.byref(d), *args, None) == -1
+    assert "aligned" in L.dadmm_last_error().decode()
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    from dadmm_hip import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(ImportError):
+        _lib.load()

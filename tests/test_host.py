@@ -1,0 +1,184 @@
+"""CPU: host-side logic of the drop-in modules (no kernel launches): graph ingestion, the
+hyper-parameter table, module construction / state_dict, argument parsing, data and loss."""
+import argparse
+
+import networkx as nx
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+
+def _args(**kw):
+    d = dict(GHN_iter_num=25, DADMM_mode="diff", alpha_max=0.1, tau_max=0.99, rho_max=0.99,
+             eta_max=0.99, max_penalty_threshold=0.8, penalty_reduction_factor=0.95)
+    d.update(kw)
+    return argparse.Namespace(**d)
+
+
+# ---- graph ingestion ----------------------------------------------------------------------------
+def test_ingest_shared_graph_masks_and_degrees():
+    from dadmm_hip.graph import ingest
+    P = 6
+    G = nx.erdos_renyi_graph(P, 0.5, seed=3)
+    gb = ingest([G] * 10, P, 10, "cpu")
+    assert gb.shared
+    masks = gb.nbr.numpy().view(np.uint64)
+    for p in range(P):
+        assert sorted(G.neighbors(p)) == [q for q in range(P) if (int(masks[p]) >> q) & 1]
+        assert gb.deg[p] == G.degree(p)
+
+
+def test_ingest_per_sample_graphs():
+    from dadmm_hip.graph import ingest
+    P, B = 5, 7
+    graphs = [O.connected_er_graph(P, 0.3, seed=s) for s in range(B)]
+    gb = ingest(graphs, P, B, "cpu")
+    assert not gb.shared and gb.nbr.shape == (B, P) and gb.deg.shape == (B, P)
+    _, _, deg = O.graph_arrays(graphs, P)
+    np.testing.assert_array_equal(gb.deg.numpy(), deg)
+
+
+def test_ingest_single_graph_for_batch_keeps_reference_quirk():
+    """compute_sum_neighbors broadcasts one graph's degrees; compute_delta walks only sample 0."""
+    from dadmm_hip.graph import ingest
+    P, B = 4, 3
+    G = nx.complete_graph(P)
+    gb = ingest([G], P, B, "cpu")
+    assert not gb.shared
+    assert (gb.deg.numpy() == 3).all()
+    m = gb.nbr.numpy()
+    assert m[0].any() and not m[1:].any()
+
+
+def test_ingest_errors():
+    from dadmm_hip.graph import ingest
+    G = nx.path_graph(4)
+    with pytest.raises(RuntimeError):
+        ingest([G, G], 4, 3, "cpu")
+    with pytest.raises(ValueError):
+        ingest([nx.path_graph(5)], 4, 1, "cpu")      # node 4 is not an agent
+    with pytest.raises(ValueError):
+        ingest([G], 65, 1, "cpu")
+
+
+# ---- hyper-parameter table --------------------------------------------------------------------
+@pytest.mark.parametrize("mode", ["diff", "same"])
+def test_seq_hyp_table_matches_forward_k_and_oracle(mode):
+    import unfolded_DLASSO
+    K, P = 25, 5
+    H = 1 if mode == "same" else P
+    max_param = torch.tensor([0.1, 0.99, 0.99, 0.99])
+    sh = unfolded_DLASSO.seq_hyperparam([K, H, 4], max_param, _args())
+    with torch.no_grad():
+        sh.param.copy_(torch.from_numpy(np.random.default_rng(0).standard_normal((K, H, 4))
+                                        .astype(np.float32)))
+    sh.eval()
+    tab = sh.table(K).detach().numpy()
+    for k in range(K):
+        np.testing.assert_allclose(sh(k)[..., 0].detach().numpy(), tab[k], rtol=2e-6, atol=1e-7)
+    np.testing.assert_allclose(tab, O.hyp_table(sh.param.detach().numpy(), [0.1, 0.99, 0.99, 0.99]),
+                               rtol=2e-6, atol=1e-7)
+    assert sh(3).shape == (H, 4, 1)
+
+
+def test_seq_hyp_training_penalty():
+    import unfolded_DLASSO
+    K, P = 4, 5
+    sh = unfolded_DLASSO.seq_hyperparam([K, P, 4], torch.tensor([0.99] * 4),
+                                        _args(alpha_max=0.99))
+    with torch.no_grad():
+        sh.param.fill_(50.0)
+    sh.train()
+    np.testing.assert_allclose(sh.table(K).detach().numpy(), 0.99 * 0.95, rtol=1e-6)
+    np.testing.assert_allclose(sh(2)[..., 0].detach().numpy(), 0.99 * 0.95, rtol=1e-6)
+    sh.eval()
+    np.testing.assert_allclose(sh.table(K).detach().numpy(), 0.99, rtol=1e-6)
+
+
+def test_seq_hyp_table_is_differentiable():
+    import unfolded_DLASSO
+    sh = unfolded_DLASSO.seq_hyperparam([5, 3, 4], torch.tensor([0.1, 0.99, 0.99, 0.99]), _args())
+    sh.table(5).sum().backward()
+    assert sh.param.grad is not None and torch.isfinite(sh.param.grad).all()
+
+
+# ---- module construction ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mode,H", [("diff", 5), ("same", 1)])
+def test_module_state_dict_matches_reference_keys(mode, H):
+    import unfolded_DLASSO
+    A = torch.randn(1, 5, 16, 32)
+    model = unfolded_DLASSO.DLASSO_unfolded(A, _args(DADMM_mode=mode))
+    sd = model.state_dict()
+    assert list(sd) == ["seq_hyp.param"] and sd["seq_hyp.param"].shape == (25, H, 4)
+    assert (model.P, model.m, model.n, model.K) == (5, 16, 32, 25)
+    torch.testing.assert_close(model.AtA, torch.matmul(A.transpose(-1, -2), A))
+
+
+def test_module_refuses_cpu_tensors():
+    """No CPU fallback: the product path needs a ROCm device."""
+    import unfolded_DLASSO
+    A = torch.randn(1, 3, 8, 16)
+    model = unfolded_DLASSO.DLASSO_unfolded(A, _args(GHN_iter_num=3))
+    with pytest.raises((RuntimeError, ImportError)):
+        model(torch.randn(4, 3, 8, 1), [nx.path_graph(3)] * 4)
+
+
+def test_module_k_zero_raises():
+    import unfolded_DLASSO
+    model = unfolded_DLASSO.DLASSO_unfolded(torch.randn(1, 3, 8, 16), _args(GHN_iter_num=3))
+    with pytest.raises(RuntimeError):
+        model(torch.randn(4, 3, 8, 1), [nx.path_graph(3)] * 4, K=0)
+
+
+# ---- configurations, data, loss ------------------------------------------------------------------
+def test_args_parser_defaults_and_quirks():
+    import configurations
+    a = configurations.args_parser([])
+    assert (a.m, a.n, a.P, a.GHN_iter_num, a.DADMM_mode, a.batch_size) == (100, 500, 5, 15, "diff", 16)
+    assert (a.alpha_max, a.tau_max, a.max_penalty_threshold) == (0.1, 0.99, 0.8)
+    # the reference parses --GHyp_hidden/--seed as float, but argparse leaves defaults unconverted
+    assert a.GHyp_hidden == 100 and isinstance(a.GHyp_hidden, int) and a.seed == 42
+    assert isinstance(configurations.args_parser(["--GHyp_hidden", "64"]).GHyp_hidden, float)
+    assert a.eval is False and a.lr_scheduler is False
+    b = configurations.args_parser(["--P", "16", "--n", "512", "--DADMM_mode", "same", "--eval"])
+    assert (b.P, b.n, b.DADMM_mode, b.eval) == (16, 512, "same", True)
+    with pytest.raises(SystemExit):
+        configurations.args_parser(["--DADMM_mode", "other"])
+
+
+def test_set_A_clamps_singular_values():
+    import gnn_dlasso_utils
+    torch.manual_seed(0)
+    A = gnn_dlasso_utils.set_A(argparse.Namespace(P=3, m=20, n=60))
+    assert A.shape == (1, 3, 20, 60)
+    s = torch.linalg.svdvals(A[0].double())
+    assert (s <= 10.0 + 1e-4).all() and (s >= 0.1 - 1e-6).all()
+
+
+def test_set_Data_is_noise_free_and_sparse():
+    import gnn_data
+    torch.manual_seed(1)
+    A = torch.randn(1, 4, 8, 30)
+    loader = gnn_data.set_Data(A, 64, argparse.Namespace(snr=4, batch_size=16))
+    b, x = next(iter(loader))
+    assert b.shape == (16, 4, 8, 1) and x.shape == (16, 30, 1)
+    torch.testing.assert_close(b, torch.einsum("pmn,snc->spmc", A[0], x), rtol=1e-5, atol=1e-5)
+    assert 0.1 < (x != 0).float().mean() < 0.4
+    assert len(loader) == 4
+
+
+def test_compute_loss_matches_oracle_and_nan_fallback():
+    import gnn_dlasso_utils
+    rng = np.random.default_rng(3)
+    Y = rng.standard_normal((6, 4, 3, 10)).astype(np.float32)
+    x = rng.standard_normal((4, 10)).astype(np.float32)
+    mean, final = gnn_dlasso_utils.compute_loss(torch.from_numpy(Y)[..., None],
+                                                torch.from_numpy(x)[..., None])
+    om, of = O.compute_loss(Y, x)
+    assert mean.item() == pytest.approx(om, rel=1e-5) and final.item() == pytest.approx(of, rel=1e-5)
+    Y[2, 1, 0, 3] = np.inf
+    mean, final = gnn_dlasso_utils.compute_loss(torch.from_numpy(Y)[..., None],
+                                                torch.from_numpy(x)[..., None])
+    assert mean.item() == 1.0 and final.item() == 1.0
