@@ -79,8 +79,9 @@ int dadmm_prepare_operator(const dadmm_dims* d, const float* A, void* op, void* 
 }
 
 int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
-                  const float* deg, const float* hyp, const float* y0, const float* U0,
-                  const float* d0, float* Y, float* U_out, int32_t* status, void* stream) {
+                  const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
+                  const float* U0, const float* d0, float* Y, float* U_out, int32_t* status,
+                  void* stream) {
     int rc = check_dims(d);
     if (rc) return rc;
     if (d->B == 0 || d->K == 0) return ok();
@@ -98,7 +99,13 @@ int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uin
     if ((size_t)d->B * d->P * d->n * 4 >= ((size_t)1 << 31))
         return fail(DADMM_EUNSUPPORTED, "B*P*n*4 >= 2^31 bytes per iterate (split the batch)");
     const int nt = dadmm::fused_nt(d->n);
-    dadmm::fused_fn_ptr fn = dadmm::find_fused(d->P, nt, d->graph_shared != 0);
+    if (nbr_order != nullptr && d->graph_shared)
+        return fail(DADMM_EINVAL, "nbr_order needs per-sample graphs (graph_shared = 0)");
+    if (nbr_order != nullptr && d->P > 8)
+        return fail(DADMM_EINVAL, "nbr_order packs 4-bit agent ids: P <= 8");
+    const int graph = d->graph_shared ? dadmm::GRAPH_SHARED
+                                      : (nbr_order ? dadmm::GRAPH_ORDERED : dadmm::GRAPH_LANE);
+    dadmm::fused_fn_ptr fn = dadmm::find_fused(d->P, nt, graph);
     if (fn == nullptr)
         return fail(DADMM_EUNSUPPORTED, "no fused kernel for P=%d n=%d (n_pad=%d)", d->P, d->n,
                     64 * nt);
@@ -108,6 +115,7 @@ int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uin
     a.At = a.A + (size_t)d->P * dadmm::M_PAD * np;
     a.b = b;
     a.nbr = nbr;
+    a.nbr_order = nbr_order;
     a.deg = deg;
     a.hyp = hyp;
     a.y0 = y0;

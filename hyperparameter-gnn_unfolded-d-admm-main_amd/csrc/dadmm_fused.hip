@@ -145,8 +145,71 @@ __device__ __forceinline__ void consensus_lane(const float (&yy)[P][E], float (&
     }
 }
 
-template <int P, int NT, bool SHARED_GRAPH>
+// Per-lane graphs whose adjacency lists are not ascending: p's own loop follows the packed
+// adjacency order ord[p] (4 bits per neighbour, cnt[p] entries) exactly as graph.neighbors(p).
+template <int P, int E>
+__device__ __forceinline__ void consensus_ordered(const float (&yy)[P][E], float (&dl)[P][E],
+                                                  const uint32_t (&msk)[P],
+                                                  const uint32_t (&ord)[P]) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        float acc[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = 0.0f;
+#pragma unroll
+        for (int q = 0; q < p; ++q) {
+            const bool on = (msk[q] >> p) & 1u;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float t = acc[e] - (yy[q][e] - yy[p][e]);
+                acc[e] = on ? t : acc[e];
+            }
+        }
+        const int cnt = __builtin_popcount(msk[p]);
+#pragma unroll
+        for (int t = 0; t < P; ++t) {
+            const bool on = t < cnt;
+            const int q = (ord[p] >> (4 * t)) & 15;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                float yq = yy[0][e];
+#pragma unroll
+                for (int qq = 1; qq < P; ++qq) yq = (q == qq) ? yy[qq][e] : yq;
+                float v = acc[e] + (yy[p][e] - yq);
+                if (q == p) v = v - (yy[p][e] - yy[p][e]);
+                acc[e] = on ? v : acc[e];
+            }
+        }
+#pragma unroll
+        for (int q = p + 1; q < P; ++q) {
+            const bool on = (msk[q] >> p) & 1u;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float t = acc[e] - (yy[q][e] - yy[p][e]);
+                acc[e] = on ? t : acc[e];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) dl[p][e] = acc[e];
+    }
+}
+
+template <int P, int GRAPH>
+__device__ __forceinline__ void consensus_any(const float (&yy)[P][4], float (&dl)[P][4],
+                                              const uint32_t (&msk)[P], const uint32_t (&ord)[P]) {
+    if constexpr (GRAPH == GRAPH_SHARED)
+        consensus<P, 4>(yy, dl, [&](int q, int p) { return ((msk[q] >> p) & 1u) != 0; });
+    else if constexpr (GRAPH == GRAPH_LANE)
+        consensus_lane<P, 4>(yy, dl, msk);
+    else
+        consensus_ordered<P, 4>(yy, dl, msk, ord);
+}
+
+// GRAPH: GRAPH_SHARED (one graph, ascending adjacency), GRAPH_LANE (per-sample, ascending),
+//        GRAPH_ORDERED (per-sample, explicit adjacency order)
+template <int P, int NT, int GRAPH>
 __global__ __launch_bounds__(WAVES * 64) void fused_forward_kernel(FusedArgs a) {
+    constexpr bool SHARED_GRAPH = GRAPH == GRAPH_SHARED;
     constexpr int MP = M_PAD;                        // padded m: 4 m-blocks of 16
     constexpr int NP = NT * 64;                      // padded n
     constexpr int NB = NP / 16;                      // 16-row n-tiles
@@ -174,7 +237,7 @@ __global__ __launch_bounds__(WAVES * 64) void fused_forward_kernel(FusedArgs a) 
     const rsrc_t rAt = make_rsrc(a.At, (uint32_t)(P * MP * NP * 4));
 
     // ---- graph data --------------------------------------------------------------------------
-    uint32_t msk[P];
+    uint32_t msk[P], ord[P];
     float dg[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -185,6 +248,7 @@ __global__ __launch_bounds__(WAVES * 64) void fused_forward_kernel(FusedArgs a) 
             msk[p] = sv ? (uint32_t)a.nbr[(size_t)s * P + p] : 0u;
             dg[p] = sv ? a.deg[(size_t)s * P + p] : 0.0f;
         }
+        ord[p] = (GRAPH == GRAPH_ORDERED && sv) ? a.nbr_order[(size_t)s * P + p] : 0u;
     }
 
     // ---- state: this wave owns n-tiles nb = w*T2 + tt; element e = 4*tt + r is row
@@ -379,10 +443,7 @@ __global__ __launch_bounds__(WAVES * 64) void fused_forward_kernel(FusedArgs a) 
                     for (int r = 0; r < 4; ++r) dr[p][r] = v[r];
                 }
             } else {
-                if (SHARED_GRAPH)
-                    consensus<P, 4>(yr, dr, [&](int q, int p) { return ((msk[q] >> p) & 1u) != 0; });
-                else
-                    consensus_lane<P, 4>(yr, dr, msk);
+                consensus_any<P, GRAPH>(yr, dr, msk, ord);
                 if (a.variant != 0) {
 #pragma unroll
                     for (int p = 0; p < P; ++p)
@@ -419,10 +480,7 @@ __global__ __launch_bounds__(WAVES * 64) void fused_forward_kernel(FusedArgs a) 
             status |= bad_g ? 4u : 0u;
 
             // delta_{k+1} = 2 L y_{k+1} (:95) and the dual update (:98-99)
-            if (SHARED_GRAPH)
-                consensus<P, 4>(yr, dr, [&](int q, int p) { return ((msk[q] >> p) & 1u) != 0; });
-            else
-                consensus_lane<P, 4>(yr, dr, msk);
+            consensus_any<P, GRAPH>(yr, dr, msk, ord);
 #pragma unroll
             for (int p = 0; p < P; ++p)
 #pragma unroll
@@ -460,38 +518,43 @@ __global__ __launch_bounds__(WAVES * 64) void fused_forward_kernel(FusedArgs a) 
 }
 
 // ----------------------------------------------------------------------------------------------
-template <int P, int NT, bool SG>
+template <int P, int NT, int GRAPH>
 static hipError_t launch_fused(const FusedArgs& a, hipStream_t stream) {
     const int grid = (a.B + BT - 1) / BT;
-    hipLaunchKernelGGL((fused_forward_kernel<P, NT, SG>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+    hipLaunchKernelGGL((fused_forward_kernel<P, NT, GRAPH>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
     return hipGetLastError();
 }
 
 template <int P, int NT>
-static fused_fn_ptr pick_sg(bool sg) {
-    return sg ? &launch_fused<P, NT, true> : &launch_fused<P, NT, false>;
+static fused_fn_ptr pick_graph(int graph) {
+    switch (graph) {
+        case GRAPH_SHARED: return &launch_fused<P, NT, GRAPH_SHARED>;
+        case GRAPH_LANE: return &launch_fused<P, NT, GRAPH_LANE>;
+        case GRAPH_ORDERED: return &launch_fused<P, NT, GRAPH_ORDERED>;
+        default: return nullptr;
+    }
 }
 
 // Instantiated shapes: P = 1..6, n_pad = 64 * NT with NT in {1, 2, 4} (NT = 4 only for P <= 5:
 // the register budget of 2 waves per SIMD), m_pad = 64.
 template <int P>
-static fused_fn_ptr pick_nt(int nt, bool sg) {
-    if (nt == 1) return pick_sg<P, 1>(sg);
-    if (nt == 2) return pick_sg<P, 2>(sg);
+static fused_fn_ptr pick_nt(int nt, int graph) {
+    if (nt == 1) return pick_graph<P, 1>(graph);
+    if (nt == 2) return pick_graph<P, 2>(graph);
     if constexpr (P <= 5) {
-        if (nt == 4) return pick_sg<P, 4>(sg);
+        if (nt == 4) return pick_graph<P, 4>(graph);
     }
     return nullptr;
 }
 
-fused_fn_ptr find_fused(int P, int nt, bool shared_graph) {
+fused_fn_ptr find_fused(int P, int nt, int graph) {
     switch (P) {
-        case 1: return pick_nt<1>(nt, shared_graph);
-        case 2: return pick_nt<2>(nt, shared_graph);
-        case 3: return pick_nt<3>(nt, shared_graph);
-        case 4: return pick_nt<4>(nt, shared_graph);
-        case 5: return pick_nt<5>(nt, shared_graph);
-        case 6: return pick_nt<6>(nt, shared_graph);
+        case 1: return pick_nt<1>(nt, graph);
+        case 2: return pick_nt<2>(nt, graph);
+        case 3: return pick_nt<3>(nt, graph);
+        case 4: return pick_nt<4>(nt, graph);
+        case 5: return pick_nt<5>(nt, graph);
+        case 6: return pick_nt<6>(nt, graph);
         default: return nullptr;
     }
 }

@@ -15,7 +15,8 @@ struct FusedArgs {
     const float* A;      // prepared operator: [P][M_PAD][n_pad]
     const float* At;     // prepared operator: [P][n_pad][M_PAD]
     const float* b;      // [B][P][m]
-    const uint64_t* nbr; // [B][P]
+    const uint64_t* nbr; // [B][P] (or [P] for GRAPH_SHARED)
+    const uint32_t* nbr_order;  // [B][P] packed adjacency order (GRAPH_ORDERED) or nullptr
     const float* deg;    // [B][P]
     const float* hyp;    // [K][hyp_rows][4]
     const float* y0;     // [B][P][n]
@@ -30,7 +31,8 @@ struct FusedArgs {
 typedef hipError_t (*fused_fn_ptr)(const FusedArgs&, hipStream_t);
 
 // Returns the launcher for (P, n_pad = 64*nt) or nullptr when that shape is not instantiated.
-fused_fn_ptr find_fused(int P, int nt, bool shared_graph);
+enum { GRAPH_SHARED = 0, GRAPH_LANE = 1, GRAPH_ORDERED = 2 };
+fused_fn_ptr find_fused(int P, int nt, int graph);
 
 // Operator preparation kernel launcher (dadmm_prepare.hip).
 hipError_t launch_prepare(const float* A, float* Apad, float* Atpad, int P, int m, int n,

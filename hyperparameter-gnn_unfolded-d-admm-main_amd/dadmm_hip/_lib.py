@@ -67,7 +67,7 @@ def load() -> ctypes.CDLL:
     L.dadmm_prepare_operator.restype = ctypes.c_int
     L.dadmm_prepare_operator.argtypes = [ctypes.POINTER(Dims), vp, vp, vp]
     L.dadmm_forward.restype = ctypes.c_int
-    L.dadmm_forward.argtypes = [ctypes.POINTER(Dims)] + [vp] * 12
+    L.dadmm_forward.argtypes = [ctypes.POINTER(Dims)] + [vp] * 13
     v = L.dadmm_abi_version()
     if v != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {v}, expected {ABI_VERSION}")

@@ -4,10 +4,12 @@ Replaces the Python loops of ``compute_sum_neighbors`` (unfolded_DLASSO.py:111-1
 walk of ``compute_delta`` (:127-140) with the device layout the kernel reads (include/dadmm.h):
 ``nbr[s][p]`` bit q set <=> q in graph_list[s].neighbors(p), ``deg[s][p] = len(neighbors(p))``.
 
-The kernel visits neighbours in ascending order, which is networkx's adjacency order for the
-graphs the reference builds (``erdos_renyi_graph`` adds edges in lexicographic order). A graph
-whose adjacency lists are not ascending is still handled; its delta is then summed in a different
-order than the reference's loop (an fp32 rounding difference only).
+compute_delta sums each agent's own neighbour terms in ``graph.neighbors(p)`` order. For the
+graphs the reference builds with ``erdos_renyi_graph`` that order is ascending (edges are added in
+lexicographic order) and the masks alone describe it. Graphs whose adjacency lists are not
+ascending (e.g. the connectivity patch of gnn_dlasso_progressive.py:184-191 appends edges) also
+get ``order``: the adjacency order packed 4 bits per neighbour, so the kernel accumulates in
+exactly the reference's order (P <= 8).
 
 Quirks of the reference kept on purpose (it never checks ``len(graph_list) == len(b)``):
   * ``compute_sum_neighbors`` sizes its output by ``len(graph_list)`` and the result broadcasts
@@ -23,33 +25,34 @@ _MASK_CACHE: dict = {}
 
 
 def _graph_masks(G, P: int):
-    """(mask uint64 [P], deg float32 [P]) for one graph."""
-    key = id(G)
-    nodes_ok = True
+    """(mask uint64 [P], deg float32 [P], order uint32 [P] or None) for one graph."""
     masks = np.zeros(P, np.uint64)
     deg = np.zeros(P, np.float32)
+    order = np.zeros(P, np.uint32)
+    ascending = True
     for p in range(P):
         nb = list(G.neighbors(p))
         deg[p] = len(nb)
-        for q in nb:
+        for t, q in enumerate(nb):
             if not (0 <= q < P):
-                nodes_ok = False
-                break
+                raise ValueError(f"neighbour id {q} of agent {p}: must be an agent 0..{P - 1}")
             masks[p] |= np.uint64(1) << np.uint64(q)
-    if not nodes_ok:
-        raise ValueError(f"graph {key}: neighbour ids must be agents 0..{P - 1}")
-    return masks, deg
+            if t < 8:
+                order[p] |= np.uint32(q & 15) << np.uint32(4 * t)
+        ascending &= all(nb[i] < nb[i + 1] for i in range(len(nb) - 1))
+    return masks, deg, (None if ascending else order)
 
 
 class GraphBatch:
     """Device-resident neighbour masks and degrees for one forward call."""
 
-    __slots__ = ("nbr", "deg", "shared")
+    __slots__ = ("nbr", "deg", "shared", "order")
 
-    def __init__(self, nbr: torch.Tensor, deg: torch.Tensor, shared: bool):
+    def __init__(self, nbr: torch.Tensor, deg: torch.Tensor, shared: bool, order=None):
         self.nbr = nbr      # int64 (uint64 bit patterns) [P] if shared else [B, P]
         self.deg = deg      # float32 [P] if shared else [B, P]
         self.shared = shared
+        self.order = order  # int32 [B, P] packed adjacency order, or None (ascending)
 
 
 def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
@@ -67,8 +70,11 @@ def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
     for g in graph_list:
         if id(g) not in per:
             per[id(g)] = _graph_masks(g, P)
-    if len(per) == 1 and G == batch_size:
-        masks, deg = next(iter(per.values()))
+    ordered = any(v[2] is not None for v in per.values())
+    if ordered and P > 8:
+        raise ValueError("graphs with non-ascending adjacency lists need P <= 8 agents")
+    if len(per) == 1 and G == batch_size and not ordered:
+        masks, deg, _ = next(iter(per.values()))
         key = (str(device), masks.tobytes(), deg.tobytes())
         hit = _MASK_CACHE.get(key)
         if hit is None:
@@ -80,16 +86,69 @@ def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
         return hit
     nbr = np.zeros((batch_size, P), np.uint64)
     degs = np.zeros((batch_size, P), np.float32)
+    order = np.zeros((batch_size, P), np.uint32) if ordered else None
+
+    def _fill(s, v):
+        nbr[s], degs[s] = v[0], v[1]
+        if ordered:
+            order[s] = v[2] if v[2] is not None else _ascending_order(v[0], P)
+
     if G == 1:   # broadcast degrees, delta only for sample 0 (see module docstring)
-        masks, deg = per[id(graph_list[0])]
-        nbr[0] = masks
-        degs[:] = deg
+        v = per[id(graph_list[0])]
+        _fill(0, v)
+        degs[:] = v[1]
     else:
         for s, g in enumerate(graph_list):
-            nbr[s], degs[s] = per[id(g)]
-    nbr_t = torch.from_numpy(nbr.view(np.int64))
-    deg_t = torch.from_numpy(degs)
+            _fill(s, per[id(g)])
+    tensors = [torch.from_numpy(nbr.view(np.int64)), torch.from_numpy(degs)]
+    if ordered:
+        tensors.append(torch.from_numpy(order.view(np.int32)))
     if torch.device(device).type == "cuda":
-        nbr_t, deg_t = nbr_t.pin_memory(), deg_t.pin_memory()
-    return GraphBatch(nbr_t.to(device, non_blocking=True), deg_t.to(device, non_blocking=True),
-                      False)
+        tensors = [t.pin_memory() for t in tensors]
+    tensors = [t.to(device, non_blocking=True) for t in tensors]
+    return GraphBatch(tensors[0], tensors[1], False, tensors[2] if ordered else None)
+
+
+def _ascending_order(masks, P):
+    """Packed ascending adjacency order for every agent of one graph -> uint32 [P]."""
+    out = np.zeros(P, np.uint32)
+    for p in range(P):
+        o, t = 0, 0
+        for q in range(P):
+            if (int(masks[p]) >> q) & 1:
+                o |= q << (4 * t)
+                t += 1
+        out[p] = o
+    return out
+
+
+def from_csr(nbr_ptr, nbr_idx, deg, P: int, device) -> GraphBatch:
+    """GraphBatch from neighbour lists already in CSR form (no networkx): ``nbr_ptr`` [B*P+1],
+    ``nbr_idx`` (adjacency order), ``deg`` [B, P]. The tensor fast path for callers that keep
+    graphs as arrays; per-sample layout."""
+    nbr_ptr = np.asarray(nbr_ptr, np.int64)
+    nbr_idx = np.asarray(nbr_idx, np.int64)
+    deg = np.asarray(deg, np.float32)
+    B = deg.shape[0]
+    if nbr_ptr.shape[0] != B * P + 1:
+        raise ValueError("nbr_ptr must have B*P+1 entries")
+    nbr = np.zeros((B, P), np.uint64)
+    order = np.zeros((B, P), np.uint32)
+    ordered = False
+    for s in range(B):
+        for p in range(P):
+            nb = nbr_idx[nbr_ptr[s * P + p]:nbr_ptr[s * P + p + 1]]
+            if ((nb < 0) | (nb >= P)).any():
+                raise ValueError(f"neighbour ids must be agents 0..{P - 1}")
+            for t, q in enumerate(nb):
+                nbr[s, p] |= np.uint64(1) << np.uint64(q)
+                if t < 8:
+                    order[s, p] |= np.uint32(q) << np.uint32(4 * t)
+            ordered |= bool((np.diff(nb) <= 0).any())
+    if ordered and P > 8:
+        raise ValueError("graphs with non-ascending adjacency lists need P <= 8 agents")
+    out = [torch.from_numpy(nbr.view(np.int64)), torch.from_numpy(deg.copy())]
+    if ordered:
+        out.append(torch.from_numpy(order.view(np.int32)))
+    out = [t.to(device) for t in out]
+    return GraphBatch(out[0], out[1], False, out[2] if ordered else None)

@@ -95,8 +95,8 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     L = _lib.load()
     with torch.cuda.device(b.device):
         rc = L.dadmm_forward(ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.nbr),
-                             _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y),
-                             _ptr(U), _ptr(status), _stream(b.device))
+                             _ptr(graphs.order), _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0),
+                             _ptr(d0), _ptr(Y), _ptr(U), _ptr(status), _stream(b.device))
     _lib.check("dadmm_forward", rc)
     if ns != op.n:
         Y = Y[..., : op.n]

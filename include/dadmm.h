@@ -22,6 +22,9 @@
  *   nbr    [B][P] uint64    bit q of nbr[s][p] set <=> q in graph_list[s].neighbors(p)  (P <= 64);
  *                           neighbours are visited in ascending order (networkx order for
  *                           erdos_renyi_graph); [P] when dims.graph_shared
+ *   nbr_order [B][P] uint32 (nullable) graph.neighbors(p) in adjacency order, 4 bits per id,
+ *                           first neighbour in the low nibble (P <= 8, per-sample graphs only);
+ *                           NULL means ascending order
  *   deg    [B][P]           compute_sum_neighbors output (reference [B,P,1,1]); [P] when shared
  *   hyp    [K][H][4]        per-iteration (alpha, tau, rho, eta), H = P ('diff') or 1 ('same')
  *   y0,U0,d0 [B][P][n]      initial primal / dual / consensus states (reference draws them)
@@ -102,8 +105,9 @@ int dadmm_prepare_operator(const dadmm_dims* d, const float* A, void* op, void* 
  * `U_out` ([B][P][n], nullable) receives U_K. `status` (one int32, nullable) is OR-ed with
  * DADMM_STATUS_* bits; the caller zeroes it. */
 int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
-                  const float* deg, const float* hyp, const float* y0, const float* U0,
-                  const float* d0, float* Y, float* U_out, int32_t* status, void* stream);
+                  const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
+                  const float* U0, const float* d0, float* Y, float* U_out, int32_t* status,
+                  void* stream);
 
 #ifdef __cplusplus
 }

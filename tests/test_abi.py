@@ -54,6 +54,7 @@ def test_operator_bytes(L):
 
 
 FAKE = [ctypes.c_void_p(0x10000 * (i + 1)) for i in range(12)]   # 16-B aligned, never touched
+FAKE.insert(3, None)                                                 # nbr_order: ascending
 
 
 def _fwd(L, d):
@@ -73,6 +74,13 @@ def test_forward_rejects_before_launch(L, kw, code):
     assert L.dadmm_last_error().decode()
 
 
+def test_forward_order_needs_per_sample_graphs(L):
+    args = list(FAKE)
+    args[3] = ctypes.c_void_p(0x90000)
+    assert L.dadmm_forward(ctypes.byref(_dims(graph_shared=1)), *args, None) == -1
+    assert L.dadmm_forward(ctypes.byref(_dims(graph_shared=0, P=9, hyp_rows=1)), *args, None) == -1
+
+
 def test_forward_empty_work_is_ok(L):
     assert _fwd(L, _dims(B=0)) == 0
     assert _fwd(L, _dims(K=0)) == 0
@@ -85,7 +93,7 @@ def test_forward_null_and_misaligned_pointers(L):
     args[1] = None        # b
     assert L.dadmm_forward(ctypes.byref(d), *args, None) == -1
     args = list(FAKE)
-    args[9] = ctypes.c_void_p(0x10004)   # Y misaligned
+    args[10] = ctypes.c_void_p(0x10004)  # Y misaligned
     assert L.dadmm_forward(ctypes.byref(d), *args, None) == -1
     assert "aligned" in L.dadmm_last_error().decode()
 

@@ -236,3 +236,44 @@ def test_repeat_runs_identical(cuda):
     Y1 = _run_hip(cuda, A, b, [G] * B, hyp, y0, U0, d0)[0]
     Y2 = _run_hip(cuda, A, b, [G] * B, hyp, y0, U0, d0)[0]
     assert np.array_equal(Y1, Y2)
+
+
+@pytest.mark.parametrize("path", sorted(__import__("glob").glob(os.path.join(GOLD, "golden_*.npz"))),
+                         ids=lambda p: os.path.basename(p))
+def test_goldens_bit_exact(cuda, path):
+    """The kernel against the committed golden vectors (graphs given as CSR in adjacency
+    order, so non-ascending adjacency lists take the ordered-consensus kernel)."""
+    from dadmm_hip import PreparedOperator, forward_raw, from_csr
+    g = np.load(path)
+    P = g["A"].shape[0]
+    op = PreparedOperator(_t(g["A"], cuda))
+    gb = from_csr(g["nbr_ptr"], g["nbr_idx"], g["deg"], P, cuda)
+    Y, U, st = forward_raw(op, _t(g["b"], cuda), gb, _t(g["hyp"], cuda), _t(g["y0"], cuda),
+                           _t(g["U0"], cuda), _t(g["d0"], cuda), variant=int(g["variant"]),
+                           want_U=True)
+    assert int(st.item()) == 0
+    np.testing.assert_array_equal(Y.cpu().numpy(), g["Y32"])
+    np.testing.assert_array_equal(U.cpu().numpy(), g["U32"])
+
+
+def test_non_ascending_adjacency_bit_exact(cuda):
+    """Graphs whose neighbours(p) are not ascending (edges added out of order, like the
+    connectivity patch of the GNN driver): the reference's accumulation order is followed."""
+    import networkx as nx
+    P, m, n, B, K = 6, 32, 128, 21, 9
+    A, b, _ = O.make_problem(P, m, n, B, seed=77)
+    rng = np.random.default_rng(3)
+    graphs = []
+    for s in range(B):
+        G = nx.Graph()
+        G.add_nodes_from(range(P))
+        edges = [(i, j) for i in range(P) for j in range(i + 1, P) if rng.random() < 0.6]
+        rng.shuffle(edges)
+        for (i, j) in edges:
+            G.add_edge(*((i, j) if rng.random() < 0.5 else (j, i)))
+        graphs.append(G)
+    y0, U0, d0 = _inits(B, P, n, seed=5)
+    hyp = O.hyp_table((rng.standard_normal((K, P, 4))).astype(np.float32), MAXP)
+    Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0)
+    Yo, Uo, _ = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
+    assert np.array_equal(Y, Yo) and np.array_equal(U, Uo)

@@ -52,6 +52,24 @@ def test_ingest_single_graph_for_batch_keeps_reference_quirk():
     assert m[0].any() and not m[1:].any()
 
 
+def test_ingest_non_ascending_adjacency_gets_order():
+    from dadmm_hip.graph import ingest
+    P = 5
+    G = nx.Graph()
+    G.add_nodes_from(range(P))
+    for e in [(0, 3), (0, 1), (2, 4), (1, 2), (3, 4), (4, 0)]:
+        G.add_edge(*e)
+    gb = ingest([G] * 3, P, 3, "cpu")
+    assert not gb.shared and gb.order is not None
+    o = gb.order.numpy().view(np.uint32)
+    for p in range(P):
+        nb = list(G.neighbors(p))
+        assert [(int(o[1, p]) >> (4 * t)) & 15 for t in range(len(nb))] == nb
+    H = nx.erdos_renyi_graph(P, 0.6, seed=1)            # ascending: no order needed
+    assert ingest([H, H, G], P, 3, "cpu").order is not None
+    assert ingest([H] * 3, P, 3, "cpu").order is None
+
+
 def test_ingest_errors():
     from dadmm_hip.graph import ingest
     G = nx.path_graph(4)
