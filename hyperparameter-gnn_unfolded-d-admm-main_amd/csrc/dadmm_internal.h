@@ -8,7 +8,10 @@ namespace dadmm {
 
 constexpr int BT = 16;       // samples per workgroup of the fused kernel (MFMA N dimension)
 constexpr int M_PAD = 64;    // padded rows per agent (4 m-blocks of 16 rows)
-constexpr int WAVES = 8;     // waves per workgroup of the fused kernel (2 per SIMD)
+#ifndef DADMM_FUSED_WAVES
+#define DADMM_FUSED_WAVES 8
+#endif
+constexpr int FUSED_WAVES = DADMM_FUSED_WAVES;  // waves per workgroup of the fused kernel
 
 // Arguments of the fused kernel (device pointers; see include/dadmm.h for the layouts).
 struct FusedArgs {
