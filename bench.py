@@ -13,7 +13,8 @@ table and the fused K-iteration HIP kernel. Unit of work = one ADMM iteration of
 rank runs its own 4096-problem batch; no collective inside the step).
 
 Extra fields: "roofline" (dominant kernel: fused_forward_kernel, timed with HIP events on its
-stream; FP32 MFMA roofline), "cpu_baseline" (the C oracle — a port of the reference forward —
+stream; HBM roofline with SURVEY.md §8(d)'s algorithmic bytes/unit 4P(4n+m), plus the FP32 MFMA view;
+"traffic" = PMC-measured HBM bytes per launch from profiles/traffic.json), "cpu_baseline" (the C oracle — a port of the reference forward —
 on the host cores, bounded sample), "parity" (bit-exactness vs the order-matched fp32 oracle and
 final-iterate MSE vs the fp64 restatement, on a slice of the batch; outside the timed region).
 """
@@ -156,13 +157,18 @@ def main():
     ms_per_step = 1e3 * elapsed / a.steps
 
     if rank == 0:
-        # roofline of the dominant kernel (algorithmic flops: SURVEY.md §8(d))
+        # Roofline of the dominant kernel (fused_forward_kernel), SURVEY.md §8(d): HBM-bound
+        # with ALGORITHMIC bytes/unit = 4 P (4n + m) (read y_k, U_k, b_p; write y_{k+1}, U_{k+1}
+        # per sample-iteration, the operator amortised), units/launch = B K.
+        bytes_unit = 4 * P * (4 * n + m)
+        alg_bytes = bytes_unit * units_per_step
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        # MFMA view of the same launch (algorithmic flops/unit)
         deg_avg = float(sum(d for _, d in G.degree())) / P
         flop_unit = P * (4 * m * n + 14 * n) + 2 * P * n * deg_avg
-        flops = flop_unit * units_per_step
-        achieved = flops / (kern_ms * 1e-3) / 1e12
-        # HBM view: bytes the fused launch must move (inputs once, every iterate once)
-        hbm_bytes = 4 * (K * B * P * n + 3 * B * P * n + B * P * m) + 2 * 4 * P * 64 * n
+        tflops = flop_unit * units_per_step / (kern_ms * 1e-3) / 1e12
+        # bytes the fused launch cannot avoid: inputs once, every iterate once (state on-chip)
+        min_bytes = 4 * (K * B * P * n + 3 * B * P * n + B * P * m) + 2 * 4 * P * 64 * n
         traffic = None
         if os.path.exists(a.traffic_file):
             try:
@@ -195,13 +201,14 @@ def main():
                        "parallelism": f"batch-sharded dp{world}"},
             "agent_iters_per_s": value * P,
             "kernel_ms": kern_ms,
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS,
-                         "traffic": traffic,
-                         "flop_per_unit": flop_unit, "units_per_launch": units_per_step,
-                         "hbm_algorithmic_bytes": hbm_bytes,
-                         "hbm_achieved_GBs": hbm_bytes / (kern_ms * 1e-3) / 1e9,
-                         "hbm_frac": hbm_bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "kernel": "fused_forward_kernel", "kernel_ms": kern_ms,
+                         "bytes_per_unit": bytes_unit, "units_per_launch": units_per_step,
+                         "min_hbm_bytes_per_launch": min_bytes,
+                         "mfma_view": {"flop_per_unit": flop_unit, "achieved_TFLOPs": tflops,
+                                       "peak_TFLOPs": PEAK_FP32_TFLOPS,
+                                       "frac": tflops / PEAK_FP32_TFLOPS}},
             "cpu_baseline": cpu,
             "parity": parity,
         }
