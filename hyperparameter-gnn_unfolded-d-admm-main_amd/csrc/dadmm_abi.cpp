@@ -135,4 +135,67 @@ int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uin
     return ok();
 }
 
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d) {
+    if (check_dims(d) != DADMM_OK) return 0;
+    const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);
+    return align256(dadmm::stepwise_flag_bytes(d->K)) + 3 * state;
+}
+
+int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
+                           const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
+                           const float* hyp, const float* y0, const float* U0, const float* d0,
+                           float* Y, float* U_out, int32_t* status, int32_t gate, void* scratch,
+                           void* stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (gate != 0 && gate != 1) return fail(DADMM_EINVAL, "gate must be 0 or 1");
+    if (gate && status == nullptr) return fail(DADMM_EINVAL, "gate = 1 needs the status word");
+    if (d->B == 0 || d->K == 0) return ok();
+    if (!op || !b || !visit_ptr || !visit_q || !deg || !hyp || !y0 || !U0 || !d0 || !Y || !scratch)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(op) || !aligned16(Y) || !aligned16(y0) || !aligned16(U0) || !aligned16(d0) ||
+        (U_out != nullptr && !aligned16(U_out)))
+        return fail(DADMM_EINVAL, "op, Y, y0, U0, d0 and U_out must be 16-byte aligned");
+    if (((uintptr_t)scratch & 255u) != 0) return fail(DADMM_EINVAL, "scratch must be 256-byte aligned");
+    if (d->m > dadmm::M_PAD)
+        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
+                    dadmm::M_PAD);
+    if ((d->n & 3) != 0)
+        return fail(DADMM_EUNSUPPORTED, "n=%d: needs n %% 4 == 0 (zero-pad n)", d->n);
+    const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);
+    char* base = (char*)scratch + align256(dadmm::stepwise_flag_bytes(d->K));
+    const int np = n_pad_of(d);
+    dadmm::StepArgs a;
+    a.A = (const float*)op;
+    a.At = a.A + (size_t)d->P * dadmm::M_PAD * np;
+    a.b = b;
+    a.vptr = visit_ptr;
+    a.vq = visit_q;
+    a.deg = deg;
+    a.hyp = hyp;
+    a.y0 = y0;
+    a.U0 = U0;
+    a.d0 = d0;
+    a.Y = Y;
+    a.D = (float*)base;
+    a.G = (float*)(base + state);
+    a.U = U_out != nullptr ? U_out : (float*)(base + 2 * state);
+    a.flags = (int32_t*)scratch;
+    a.status = status;
+    a.B = d->B;
+    a.P = d->P;
+    a.m = d->m;
+    a.n = d->n;
+    a.n_pad = np;
+    a.K = d->K;
+    a.hyp_rows = d->hyp_rows;
+    a.variant = d->variant;
+    a.graph_shared = d->graph_shared;
+    hipError_t e = dadmm::launch_stepwise(a, gate, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "stepwise launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 }  // extern "C"

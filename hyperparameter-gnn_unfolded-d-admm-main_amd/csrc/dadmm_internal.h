@@ -41,6 +41,41 @@ fused_fn_ptr find_fused(int P, int nt, int graph);
 hipError_t launch_prepare(const float* A, float* Apad, float* Atpad, int P, int m, int n,
                           int n_pad, hipStream_t stream);
 
+// ---- stepwise path (dadmm_stepwise.hip) --------------------------------------------------------
+// flag words (int32, zeroed before every forward): barrier counter, barrier timeout, y0 guard,
+// then per iteration k: U_k non-finite, gradient NaN, y_next non-finite (U_K is index K).
+#define SW_F_BARRIER 0
+#define SW_F_TIMEOUT 1
+#define SW_F_Y0 2
+#define SW_F_UBAD(k) (4 + 4 * (k))
+#define SW_F_GBAD(k) (5 + 4 * (k))
+#define SW_F_YNB(k) (6 + 4 * (k))
+#define SW_FLAG_WORDS(K) (4 + 4 * ((K) + 1))
+
+struct StepArgs {
+    const float* A;         // prepared operator [P][M_PAD][n_pad]
+    const float* At;        // [P][n_pad][M_PAD]
+    const float* b;         // [B][P][m]
+    const int32_t* vptr;    // visit lists: [G*P + 1] offsets into vq (G = 1 shared, B otherwise)
+    const uint8_t* vq;      // neighbour ids in the reference's accumulation order
+    const float* deg;       // [G][P]
+    const float* hyp;       // [K][hyp_rows][4]
+    const float* y0;        // [B][P][n]
+    const float* U0;
+    const float* d0;
+    float* Y;               // [K][B][P][n]
+    float* U;               // [B][P][n]: U_k (caller's U_out or scratch)
+    float* D;               // [B][P][n]: delta_k (scratch)
+    float* G;               // [B][P][n]: gradient of the current iteration (scratch)
+    int32_t* flags;         // [SW_FLAG_WORDS(K)] (scratch)
+    int32_t* status;        // [1]
+    int B, P, m, n, n_pad, K, hyp_rows, variant, graph_shared;
+};
+
+size_t stepwise_flag_bytes(int K);
+// gate = 1: one persistent launch that runs only if *status != 0 when it starts
+hipError_t launch_stepwise(const StepArgs& a, int gate, hipStream_t stream);
+
 inline int fused_nt(int n) {
     const int nt = (n + 63) / 64;
     return nt <= 1 ? 1 : (nt <= 2 ? 2 : (nt <= 4 ? 4 : nt));

@@ -11,10 +11,11 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
+STATUS_BARRIER_TIMEOUT = 0x100
 
 # every symbol include/dadmm.h declares
 EXPORTED_SYMBOLS = (
@@ -23,6 +24,8 @@ EXPORTED_SYMBOLS = (
     "dadmm_operator_bytes",
     "dadmm_prepare_operator",
     "dadmm_forward",
+    "dadmm_stepwise_scratch_bytes",
+    "dadmm_forward_stepwise",
 )
 
 
@@ -68,6 +71,10 @@ def load() -> ctypes.CDLL:
     L.dadmm_prepare_operator.argtypes = [ctypes.POINTER(Dims), vp, vp, vp]
     L.dadmm_forward.restype = ctypes.c_int
     L.dadmm_forward.argtypes = [ctypes.POINTER(Dims)] + [vp] * 13
+    L.dadmm_stepwise_scratch_bytes.restype = ctypes.c_size_t
+    L.dadmm_stepwise_scratch_bytes.argtypes = [ctypes.POINTER(Dims)]
+    L.dadmm_forward_stepwise.restype = ctypes.c_int
+    L.dadmm_forward_stepwise.argtypes = [ctypes.POINTER(Dims)] + [vp] * 12 + [i32, vp, vp]
     v = L.dadmm_abi_version()
     if v != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {v}, expected {ABI_VERSION}")

@@ -1,15 +1,21 @@
-"""Graph ingestion: ``graph_list`` (networkx graphs) -> neighbour bitmasks + degrees.
+"""Graph ingestion: ``graph_list`` (networkx graphs) -> the device layouts the kernels read.
 
 Replaces the Python loops of ``compute_sum_neighbors`` (unfolded_DLASSO.py:111-118) and the graph
-walk of ``compute_delta`` (:127-140) with the device layout the kernel reads (include/dadmm.h):
-``nbr[s][p]`` bit q set <=> q in graph_list[s].neighbors(p), ``deg[s][p] = len(neighbors(p))``.
+walk of ``compute_delta`` (:127-140) with (include/dadmm.h):
+  * fused kernel: ``nbr[s][p]`` bit q set <=> q in graph_list[s].neighbors(p) and, for adjacency
+    lists that are not ascending, ``order`` (the adjacency order packed 4 bits per neighbour,
+    P <= 8);
+  * stepwise kernel: visit lists ``vptr``/``vq`` — for each agent p the neighbour ids in the
+    order compute_delta accumulates delta[p] (its own ``neighbors(p)`` loop between the visits
+    of lower and higher agents), any P <= 64;
+  * both: ``deg[s][p] = len(neighbors(p))``.
 
 compute_delta sums each agent's own neighbour terms in ``graph.neighbors(p)`` order. For the
 graphs the reference builds with ``erdos_renyi_graph`` that order is ascending (edges are added in
 lexicographic order) and the masks alone describe it. Graphs whose adjacency lists are not
-ascending (e.g. the connectivity patch of gnn_dlasso_progressive.py:184-191 appends edges) also
-get ``order``: the adjacency order packed 4 bits per neighbour, so the kernel accumulates in
-exactly the reference's order (P <= 8).
+ascending (e.g. the connectivity patch of gnn_dlasso_progressive.py:184-191 appends edges) carry
+``order`` (P <= 8) / their visit lists (any P), so the kernels accumulate in exactly the
+reference's order.
 
 Quirks of the reference kept on purpose (it never checks ``len(graph_list) == len(b)``):
   * ``compute_sum_neighbors`` sizes its output by ``len(graph_list)`` and the result broadcasts
@@ -21,38 +27,107 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-_MASK_CACHE: dict = {}
+_SHARED_CACHE: dict = {}
 
 
-def _graph_masks(G, P: int):
-    """(mask uint64 [P], deg float32 [P], order uint32 [P] or None) for one graph."""
-    masks = np.zeros(P, np.uint64)
-    deg = np.zeros(P, np.float32)
-    order = np.zeros(P, np.uint32)
-    ascending = True
+class _GraphInfo:
+    """Host arrays of one graph on agents 0..P-1."""
+
+    __slots__ = ("mask", "deg", "order", "ascending", "vcnt", "vq")
+
+    def __init__(self, adj, P: int):
+        self.mask = np.zeros(P, np.uint64)
+        self.deg = np.zeros(P, np.float32)
+        self.order = np.zeros(P, np.uint32)
+        self.ascending = True
+        for p, nb in enumerate(adj):
+            self.deg[p] = len(nb)
+            for t, q in enumerate(nb):
+                if not (0 <= q < P):
+                    raise ValueError(f"neighbour id {q} of agent {p}: must be an agent 0..{P - 1}")
+                self.mask[p] |= np.uint64(1) << np.uint64(q)
+                if t < 8:
+                    self.order[p] |= np.uint32(q & 15) << np.uint32(4 * t)
+            self.ascending &= all(nb[i] < nb[i + 1] for i in range(len(nb) - 1))
+        self.vcnt, self.vq = _visit_lists(adj, P)
+
+
+def _visit_lists(adj, P: int):
+    """Per agent p, the ids q whose term (y_p - y_q) compute_delta (unfolded_DLASSO.py:127-140)
+    adds to delta[p], in order: the outer loop over p' visits p' < p (p in neighbors(p'): -=),
+    then p itself (its neighbours in adjacency order: +=), then p' > p. A -= of fl(y_p' - y_p)
+    equals a += of fl(y_p - y_p') exactly, so every entry is one ``acc + (y_p - y_q)``; a
+    self-loop contributes its += and -= as two entries q = p."""
+    into = [[] for _ in range(P)]          # into[p] = [p' ...] with p in neighbors(p'), by p'
+    for pp, nb in enumerate(adj):
+        for q in nb:
+            if q != pp:
+                into[q].append(pp)
+    cnt = np.zeros(P, np.int32)
+    flat = []
     for p in range(P):
-        nb = list(G.neighbors(p))
-        deg[p] = len(nb)
-        for t, q in enumerate(nb):
-            if not (0 <= q < P):
-                raise ValueError(f"neighbour id {q} of agent {p}: must be an agent 0..{P - 1}")
-            masks[p] |= np.uint64(1) << np.uint64(q)
-            if t < 8:
-                order[p] |= np.uint32(q & 15) << np.uint32(4 * t)
-        ascending &= all(nb[i] < nb[i + 1] for i in range(len(nb) - 1))
-    return masks, deg, (None if ascending else order)
+        lst = [pp for pp in into[p] if pp < p]
+        for q in adj[p]:
+            lst.extend((q, q) if q == p else (q,))
+        lst.extend(pp for pp in into[p] if pp > p)
+        cnt[p] = len(lst)
+        flat.extend(lst)
+    return cnt, np.asarray(flat, np.uint8)
 
 
 class GraphBatch:
-    """Device-resident neighbour masks and degrees for one forward call."""
+    """Device-resident graph layouts for one forward call."""
 
-    __slots__ = ("nbr", "deg", "shared", "order")
+    __slots__ = ("nbr", "deg", "shared", "order", "vptr", "vq", "fused_ok")
 
-    def __init__(self, nbr: torch.Tensor, deg: torch.Tensor, shared: bool, order=None):
+    def __init__(self, nbr, deg, shared, order, vptr, vq, fused_ok=True):
         self.nbr = nbr      # int64 (uint64 bit patterns) [P] if shared else [B, P]
         self.deg = deg      # float32 [P] if shared else [B, P]
         self.shared = shared
-        self.order = order  # int32 [B, P] packed adjacency order, or None (ascending)
+        self.order = order  # int32 [B, P] packed adjacency order, or None (ascending / shared)
+        self.vptr = vptr    # int32 [P+1] if shared else [B*P+1]
+        self.vq = vq        # uint8 visit lists
+        # False when the fused kernel cannot follow the adjacency order (non-ascending lists with
+        # P > 8): such batches take the stepwise path, which follows any order
+        self.fused_ok = fused_ok
+
+
+def _to_device(arrays, device):
+    ts = [torch.from_numpy(np.ascontiguousarray(a)) for a in arrays]
+    if torch.device(device).type == "cuda":
+        ts = [t.pin_memory() for t in ts]
+    return [t.to(device, non_blocking=True) for t in ts]
+
+
+def _vq_nonempty(vq):
+    return vq if vq.size else np.zeros(1, np.uint8)   # the ABI wants a valid pointer
+
+
+def _batch(infos, P: int, device) -> GraphBatch:
+    """Per-sample layouts from one _GraphInfo (or None: no edges) per sample."""
+    B = len(infos)
+    nbr = np.zeros((B, P), np.uint64)
+    deg = np.zeros((B, P), np.float32)
+    ordered = any(i is not None and not i.ascending for i in infos)
+    fused_ok = not (ordered and P > 8)
+    ordered &= fused_ok
+    order = np.zeros((B, P), np.uint32) if ordered else None
+    vcnt = np.zeros((B, P), np.int32)
+    vqs = []
+    for s, i in enumerate(infos):
+        if i is None:
+            continue
+        nbr[s], deg[s] = i.mask, i.deg
+        if ordered:
+            order[s] = i.order
+        vcnt[s] = i.vcnt
+        vqs.append(i.vq)
+    vptr = np.zeros(B * P + 1, np.int32)
+    np.cumsum(vcnt.reshape(-1), out=vptr[1:])
+    vq = _vq_nonempty(np.concatenate(vqs) if vqs else np.zeros(0, np.uint8))
+    arrays = [nbr.view(np.int64), deg, vptr, vq] + ([order.view(np.int32)] if ordered else [])
+    t = _to_device(arrays, device)
+    return GraphBatch(t[0], t[1], False, t[4] if ordered else None, t[2], t[3], fused_ok)
 
 
 def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
@@ -69,57 +144,27 @@ def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
     per = {}
     for g in graph_list:
         if id(g) not in per:
-            per[id(g)] = _graph_masks(g, P)
-    ordered = any(v[2] is not None for v in per.values())
-    if ordered and P > 8:
-        raise ValueError("graphs with non-ascending adjacency lists need P <= 8 agents")
-    if len(per) == 1 and G == batch_size and not ordered:
-        masks, deg, _ = next(iter(per.values()))
-        key = (str(device), masks.tobytes(), deg.tobytes())
-        hit = _MASK_CACHE.get(key)
-        if hit is None:
-            hit = GraphBatch(torch.from_numpy(masks.view(np.int64).copy()).to(device),
-                             torch.from_numpy(deg.copy()).to(device), True)
-            if len(_MASK_CACHE) > 256:
-                _MASK_CACHE.clear()
-            _MASK_CACHE[key] = hit
-        return hit
-    nbr = np.zeros((batch_size, P), np.uint64)
-    degs = np.zeros((batch_size, P), np.float32)
-    order = np.zeros((batch_size, P), np.uint32) if ordered else None
-
-    def _fill(s, v):
-        nbr[s], degs[s] = v[0], v[1]
-        if ordered:
-            order[s] = v[2] if v[2] is not None else _ascending_order(v[0], P)
-
+            per[id(g)] = _GraphInfo([list(g.neighbors(p)) for p in range(P)], P)
+    if len(per) == 1 and G == batch_size:
+        i = next(iter(per.values()))
+        if i.ascending:
+            key = (str(device), P, i.mask.tobytes(), i.deg.tobytes(), i.vq.tobytes())
+            hit = _SHARED_CACHE.get(key)
+            if hit is None:
+                vptr = np.zeros(P + 1, np.int32)
+                np.cumsum(i.vcnt, out=vptr[1:])
+                t = _to_device([i.mask.view(np.int64), i.deg, vptr, _vq_nonempty(i.vq)], device)
+                hit = GraphBatch(t[0], t[1], True, None, t[2], t[3])
+                if len(_SHARED_CACHE) > 256:
+                    _SHARED_CACHE.clear()
+                _SHARED_CACHE[key] = hit
+            return hit
     if G == 1:   # broadcast degrees, delta only for sample 0 (see module docstring)
-        v = per[id(graph_list[0])]
-        _fill(0, v)
-        degs[:] = v[1]
-    else:
-        for s, g in enumerate(graph_list):
-            _fill(s, per[id(g)])
-    tensors = [torch.from_numpy(nbr.view(np.int64)), torch.from_numpy(degs)]
-    if ordered:
-        tensors.append(torch.from_numpy(order.view(np.int32)))
-    if torch.device(device).type == "cuda":
-        tensors = [t.pin_memory() for t in tensors]
-    tensors = [t.to(device, non_blocking=True) for t in tensors]
-    return GraphBatch(tensors[0], tensors[1], False, tensors[2] if ordered else None)
-
-
-def _ascending_order(masks, P):
-    """Packed ascending adjacency order for every agent of one graph -> uint32 [P]."""
-    out = np.zeros(P, np.uint32)
-    for p in range(P):
-        o, t = 0, 0
-        for q in range(P):
-            if (int(masks[p]) >> q) & 1:
-                o |= q << (4 * t)
-                t += 1
-        out[p] = o
-    return out
+        i = per[id(graph_list[0])]
+        gb = _batch([i] + [None] * (batch_size - 1), P, device)
+        gb.deg = gb.deg.new_tensor(np.broadcast_to(i.deg, (batch_size, P)).copy())
+        return gb
+    return _batch([per[id(g)] for g in graph_list], P, device)
 
 
 def from_csr(nbr_ptr, nbr_idx, deg, P: int, device) -> GraphBatch:
@@ -132,23 +177,12 @@ def from_csr(nbr_ptr, nbr_idx, deg, P: int, device) -> GraphBatch:
     B = deg.shape[0]
     if nbr_ptr.shape[0] != B * P + 1:
         raise ValueError("nbr_ptr must have B*P+1 entries")
-    nbr = np.zeros((B, P), np.uint64)
-    order = np.zeros((B, P), np.uint32)
-    ordered = False
+    infos = []
     for s in range(B):
-        for p in range(P):
-            nb = nbr_idx[nbr_ptr[s * P + p]:nbr_ptr[s * P + p + 1]]
-            if ((nb < 0) | (nb >= P)).any():
-                raise ValueError(f"neighbour ids must be agents 0..{P - 1}")
-            for t, q in enumerate(nb):
-                nbr[s, p] |= np.uint64(1) << np.uint64(q)
-                if t < 8:
-                    order[s, p] |= np.uint32(q) << np.uint32(4 * t)
-            ordered |= bool((np.diff(nb) <= 0).any())
-    if ordered and P > 8:
-        raise ValueError("graphs with non-ascending adjacency lists need P <= 8 agents")
-    out = [torch.from_numpy(nbr.view(np.int64)), torch.from_numpy(deg.copy())]
-    if ordered:
-        out.append(torch.from_numpy(order.view(np.int32)))
-    out = [t.to(device) for t in out]
-    return GraphBatch(out[0], out[1], False, out[2] if ordered else None)
+        adj = [nbr_idx[nbr_ptr[s * P + p]:nbr_ptr[s * P + p + 1]].tolist() for p in range(P)]
+        if any(q < 0 or q >= P for nb in adj for q in nb):
+            raise ValueError(f"neighbour ids must be agents 0..{P - 1}")
+        infos.append(_GraphInfo(adj, P))
+    gb = _batch(infos, P, device)
+    gb.deg = torch.from_numpy(deg.copy()).to(device)
+    return gb

@@ -75,11 +75,19 @@ def _pad_n(t, n_store):
 
 def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: torch.Tensor,
                 y0: torch.Tensor, U0: torch.Tensor, d0: torch.Tensor, *,
-                variant: int = _lib.VARIANT_UNFOLDED, want_U: bool = False):
-    """One fused launch. Shapes: b [B,P,m], hyp [K,H,4], y0/U0/d0 [B,P,n].
+                variant: int = _lib.VARIANT_UNFOLDED, want_U: bool = False, path: str = "auto"):
+    """The K-step forward with the reference's NaN/Inf guards, enqueued on the current stream
+    (no host synchronisation). Shapes: b [B,P,m], hyp [K,H,4], y0/U0/d0 [B,P,n].
+
+    path "auto": the fused kernel when the shape is compiled, followed by the device-gated
+    stepwise recomputation (runs only if the fused kernel flagged a guard event); otherwise the
+    stepwise kernels. "fused" / "stepwise" force one path ("fused" alone does NOT apply the
+    guards: its status only flags them).
 
     Returns (Y [K,B,P,n], U_K [B,P,n] or None, status int32 device tensor [1])."""
     _dev_check(b, hyp, y0, U0, d0, graphs.nbr, graphs.deg)
+    if path not in ("auto", "fused", "stepwise"):
+        raise ValueError(f"unknown path {path!r}")
     B, P, m = b.shape
     if P != op.P or m != op.m:
         raise ValueError(f"b is [B,{P},{m}], operator is P={op.P}, m={op.m}")
@@ -94,11 +102,43 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     d = op.dims(B=B, K=K, variant=variant, hyp_rows=H, graph_shared=graphs.shared)
     L = _lib.load()
     with torch.cuda.device(b.device):
-        rc = L.dadmm_forward(ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.nbr),
-                             _ptr(graphs.order), _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0),
-                             _ptr(d0), _ptr(Y), _ptr(U), _ptr(status), _stream(b.device))
-    _lib.check("dadmm_forward", rc)
+        stream = _stream(b.device)
+        if path == "fused" and not graphs.fused_ok:
+            raise ValueError("the fused kernel follows non-ascending adjacency orders only for "
+                             "P <= 8; use path='auto' or 'stepwise'")
+        fused = path != "stepwise" and graphs.fused_ok
+        if fused:
+            rc = L.dadmm_forward(ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.nbr),
+                                 _ptr(graphs.order), _ptr(graphs.deg), _ptr(hyp), _ptr(y0),
+                                 _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U), _ptr(status), stream)
+            if rc == _lib.DADMM_EUNSUPPORTED and path == "auto":
+                fused = False
+            else:
+                _lib.check("dadmm_forward", rc)
+        if path != "fused":
+            nbytes = L.dadmm_stepwise_scratch_bytes(ctypes.byref(d))
+            scratch = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=b.device)
+            _lib.check("dadmm_forward_stepwise", L.dadmm_forward_stepwise(
+                ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.vptr), _ptr(graphs.vq),
+                _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U),
+                _ptr(status), 1 if fused else 0, _ptr(scratch), stream))
     if ns != op.n:
         Y = Y[..., : op.n]
         U = U[..., : op.n] if U is not None else None
     return Y, U, status
+
+
+def describe_status(st: int) -> list:
+    """The reference's warnings (unfolded_DLASSO.py:56-104) for the guard bits in ``st``."""
+    out = []
+    if st & _lib.STATUS_Y_NONFINITE:
+        out.append("NaN/Inf detected in y_k, reset to zeros")
+    if st & _lib.STATUS_U_NONFINITE:
+        out.append("NaN/Inf detected in U_k, reset to zeros")
+    if st & _lib.STATUS_GRAD_NAN:
+        out.append("NaN/Inf in gradient, update skipped")
+    if st & _lib.STATUS_YNEXT_NAN:
+        out.append("NaN/Inf in y_next, previous value kept")
+    if st & _lib.STATUS_BARRIER_TIMEOUT:
+        out.append("stepwise grid barrier timed out: Y is invalid (device shared with other work)")
+    return out

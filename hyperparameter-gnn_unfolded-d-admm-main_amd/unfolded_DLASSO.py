@@ -11,7 +11,8 @@ import torch
 import torch.nn as nn
 
 from dadmm_hip import _lib
-from dadmm_hip.autograd import dadmm_unfolded_apply
+from dadmm_hip.autograd import check_status, dadmm_unfolded_apply
+from dadmm_hip.ops import describe_status
 from dadmm_hip.graph import ingest
 from dadmm_hip.ops import PreparedOperator
 
@@ -37,6 +38,9 @@ class DLASSO_unfolded(nn.Module):
         self.args = args
         self._op = None
         self._op_key = None
+        # device int32 [1]: DADMM_STATUS_* bits of the guards the last forward applied
+        # (include/dadmm.h); read it with guard_warnings() (synchronises)
+        self.last_status = None
 
     # The reference precomputes AtA eagerly (:16). The HIP path never forms it; it is kept as a
     # lazily computed attribute for callers that read it.
@@ -93,10 +97,17 @@ class DLASSO_unfolded(nn.Module):
         y0, U0, d0 = (x.reshape(batch_size, self.P, self.n) for x in (y0, U0, d0))
 
         table = self.hyp_table(K)                       # [K, H, 4]
-        Y = dadmm_unfolded_apply(self.operator(), bb, graphs, table, y0, U0, d0,
-                                 _lib.VARIANT_UNFOLDED)
+        Y, self.last_status = dadmm_unfolded_apply(self.operator(), bb, graphs, table, y0, U0,
+                                                   d0, _lib.VARIANT_UNFOLDED)
         hyp = table[K - 1].unsqueeze(-1)                # seq_hyp(K-1): [H, 4, 1]
         return Y.unsqueeze(-1), hyp
+
+    def guard_warnings(self):
+        """The reference's NaN/Inf warnings (unfolded_DLASSO.py:56-104) for the last forward
+        (synchronises with the device)."""
+        if self.last_status is None:
+            return []
+        return describe_status(check_status(self.last_status))
 
     # kept for API parity with the reference (:111-146); not used by the HIP forward
     def compute_sum_neighbors(self, graph_list, device):

@@ -30,9 +30,17 @@
  *   y0,U0,d0 [B][P][n]      initial primal / dual / consensus states (reference draws them)
  *   Y      [K][B][P][n]     every iterate y_1..y_K     (reference Y, shape [K,B,P,n,1])
  *
- * Compiled configurations of dadmm_forward: P <= 6 (P <= 5 at n > 128), m <= 64, n <= 256,
- * n % 4 == 0 (callers zero-pad n otherwise: zero columns of A are inert), B*P*n*4 < 2^31.
- * Anything else returns DADMM_EUNSUPPORTED.
+ *   visit_ptr [G*P+1] int32, visit_q [visit_ptr[G*P]] uint8 (stepwise path): for agent p of
+ *                           graph g, the neighbour ids q in the order compute_delta
+ *                           (unfolded_DLASSO.py:127-140) accumulates delta[p]: every p' < p
+ *                           with p in neighbors(p'), then neighbors(p) in adjacency order, then
+ *                           every p' > p with p in neighbors(p'); G = 1 when dims.graph_shared,
+ *                           else B
+ *
+ * Compiled configurations of dadmm_forward (fused): P <= 6 (P <= 5 at n > 128), m <= 64,
+ * n <= 256, n % 4 == 0 (callers zero-pad n otherwise: zero columns of A are inert),
+ * B*P*n*4 < 2^31. Anything else returns DADMM_EUNSUPPORTED; dadmm_forward_stepwise covers every
+ * P <= 64, m <= 64, n % 4 == 0.
  */
 #ifndef DADMM_H_
 #define DADMM_H_
@@ -44,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 1
+#define DADMM_ABI_VERSION 2
 
 enum {
     DADMM_OK = 0,
@@ -58,15 +66,21 @@ enum {
     DADMM_VARIANT_GNN = 1       /* gnn_dlasso_models_progressive.py:211-232: fixed clamps       */
 };
 
-/* Bits of the `status` word written by dadmm_forward (nullable). A set bit means a non-finite
- * value reached one of the reference's NaN/Inf guards (unfolded_DLASSO.py:55-61, 84-86,
- * 102-104). The fused kernel does not apply those batch-global resets; a caller that sees a
- * non-zero status re-runs the batch through dadmm_forward_guarded. */
+/* Bits of the `status` word. A set bit means a non-finite value reached one of the reference's
+ * batch-global NaN/Inf guards (unfolded_DLASSO.py:55-61, 84-86, 102-104).
+ *   dadmm_forward (fused) does NOT apply the guards: it ORs in the bits of every case where the
+ *   reference would have fired one (bit 8 also for a non-finite hyper-parameter), and its Y is
+ *   then not the reference's. dadmm_forward_stepwise with gate = 1, enqueued right after it on
+ *   the same stream, recomputes exactly such batches on the device (no host round trip).
+ *   dadmm_forward_stepwise applies the guards exactly and stores the bits of the guards that
+ *   fired (the reference prints one warning per fired guard). */
 enum {
     DADMM_STATUS_Y_NONFINITE = 1,    /* y_k had NaN/Inf at the top of an iteration   (:55)   */
     DADMM_STATUS_U_NONFINITE = 2,    /* U_k had NaN/Inf at the top of an iteration   (:59)   */
     DADMM_STATUS_GRAD_NAN = 4,       /* clamped gradient had NaN                     (:84)   */
-    DADMM_STATUS_YNEXT_NAN = 8       /* clamped y_next had NaN                       (:102)  */
+    DADMM_STATUS_YNEXT_NAN = 8,      /* y_next had NaN/Inf                           (:102)  */
+    DADMM_STATUS_BARRIER_TIMEOUT = 0x100 /* gated stepwise run could not synchronise its grid
+                                          * (device shared with other work): Y is invalid    */
 };
 
 typedef struct dadmm_dims {
@@ -108,6 +122,27 @@ int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uin
                   const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
                   const float* U0, const float* d0, float* Y, float* U_out, int32_t* status,
                   void* stream);
+
+/* Bytes of device scratch dadmm_forward_stepwise needs for `d` (256-byte aligned pointer). */
+size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d);
+
+/* The K-step forward one iteration at a time, with the reference's batch-global NaN/Inf guards
+ * applied exactly (unfolded_DLASSO.py:55-61, 84-86, 102-104) — same operation order as the fused
+ * kernel, so on guard-free inputs its Y is bit-identical to dadmm_forward's.
+ * Replaces: the same loop as dadmm_forward (unfolded_DLASSO.py:45, 53-109), for every shape.
+ * Graph: visit_ptr / visit_q (layout above) and deg ([P] when graph_shared, else [B][P]).
+ * gate = 0: always runs (2K + 2 launches).
+ * gate = 1: ONE persistent launch that returns at once unless *status != 0 when it starts: the
+ *           exact recomputation of a batch the fused dadmm_forward flagged, enqueued right after it
+ *           on the same stream. One workgroup per CU synchronised by an in-launch grid barrier;
+ *           the device must not be shared with other work (DADMM_STATUS_BARRIER_TIMEOUT).
+ * `status` (required for gate = 1) is overwritten with the DADMM_STATUS_* bits of the guards that
+ * fired. `scratch`: dadmm_stepwise_scratch_bytes(d) bytes. */
+int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
+                           const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
+                           const float* hyp, const float* y0, const float* U0, const float* d0,
+                           float* Y, float* U_out, int32_t* status, int32_t gate, void* scratch,
+                           void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,4 +1,5 @@
-"""GPU parity: the HIP fused forward (through the C ABI) against the CPU oracle.
+"""GPU parity: the HIP forward paths (fused, stepwise, fused + gated stepwise; through the C ABI)
+against the CPU oracle.
 
 Bar (BASELINE.json north_star: "final-iterate x matching the CPU reference ... within a stated
 fp32 tolerance"):
@@ -34,13 +35,13 @@ def _t(x, dev):
     return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
 
 
-def _run_hip(dev, A, b, graphs_list, hyp, y0, U0, d0, variant=0):
+def _run_hip(dev, A, b, graphs_list, hyp, y0, U0, d0, variant=0, path="auto"):
     from dadmm_hip import PreparedOperator, forward_raw, ingest
     B = y0.shape[0]
     op = PreparedOperator(_t(A, dev))
     g = ingest(graphs_list, A.shape[0], B, dev)
     Y, U, st = forward_raw(op, _t(b, dev), g, _t(hyp, dev), _t(y0, dev), _t(U0, dev),
-                           _t(d0, dev), variant=variant, want_U=True)
+                           _t(d0, dev), variant=variant, want_U=True, path=path)
     torch.cuda.synchronize()
     return Y.cpu().numpy(), U.cpu().numpy(), int(st.item()), g.shared
 
@@ -119,7 +120,7 @@ def test_headline_shape_vs_fp64(cuda):
     assert np.mean(mses) <= 1e-5 and np.median(mses) <= 1e-5, mses
 
 
-@pytest.mark.parametrize("P,m,n,B,K,prob,per_sample", [
+SHAPES = [
     (5, 50, 200, 32, 15, 0.5, False),   # BASELINE configs[0] shape (CPU config of the reference)
     (5, 64, 256, 17, 25, 0.5, True),    # per-sample connected graphs (progressive driver style)
     (3, 16, 64, 5, 7, 0.9, True),
@@ -127,8 +128,19 @@ def test_headline_shape_vs_fp64(cuda):
     (4, 64, 192, 16, 12, 0.3, False),
     (1, 8, 16, 3, 4, 0.5, False),       # a single agent: no consensus at all
     (2, 20, 124, 31, 9, 1.0, False),
-])
-def test_shapes_bit_exact(cuda, P, m, n, B, K, prob, per_sample):
+]
+# shapes only the stepwise path covers (BASELINE configs[2] / configs[4] agent counts and sizes)
+BIG_SHAPES = [
+    (16, 64, 512, 20, 6, 0.3, True),    # configs[2]: P=16, n=512, m=64, graph_prob 0.3
+    (50, 32, 1024, 3, 3, 0.5, True),    # configs[4]: P=50, n=1024, m=32, graph_prob 0.5
+    (9, 40, 320, 18, 5, 0.4, False),
+    (64, 16, 64, 2, 3, 0.2, True),      # the uint64-mask / uint8-id limit
+]
+
+
+@pytest.mark.parametrize("path", ["auto", "stepwise"])
+@pytest.mark.parametrize("P,m,n,B,K,prob,per_sample", SHAPES + BIG_SHAPES)
+def test_shapes_bit_exact(cuda, P, m, n, B, K, prob, per_sample, path):
     A, b, _ = O.make_problem(P, m, n, B, seed=P * 100 + n)
     if per_sample:
         graphs = [O.connected_er_graph(P, prob, seed=1000 + s) for s in range(B)]
@@ -137,14 +149,15 @@ def test_shapes_bit_exact(cuda, P, m, n, B, K, prob, per_sample):
     y0, U0, d0 = _inits(B, P, n, seed=B)
     rng = np.random.default_rng(K)
     hyp = O.hyp_table((0.5 * rng.standard_normal((K, P, 4))).astype(np.float32), MAXP)
-    Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0)
+    Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0, path=path)
     Yo, Uo, _ = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
     assert st == 0
     assert np.array_equal(Y, Yo), f"max |diff| {np.abs(Y - Yo).max()}"
     assert np.array_equal(U, Uo)
 
 
-def test_same_mode_and_gnn_variant(cuda):
+@pytest.mark.parametrize("path", ["auto", "stepwise"])
+def test_same_mode_and_gnn_variant(cuda, path):
     """'same' hyper-parameters (H = 1) and the GNN variant's fixed clamps / delta clamp."""
     P, m, n, B, K = 5, 32, 128, 24, 12
     A, b, _ = O.make_problem(P, m, n, B, seed=8)
@@ -153,27 +166,83 @@ def test_same_mode_and_gnn_variant(cuda):
     rng = np.random.default_rng(2)
     hyp = O.hyp_table((rng.standard_normal((K, 1, 4))).astype(np.float32), [0.3, 0.99, 0.99, 0.99])
     for variant in (0, 1):
-        Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0, variant=variant)
+        Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0, variant=variant, path=path)
         Yo, Uo, _ = O.forward_f32(A, b, graphs, hyp, y0, U0, d0, variant=variant)
         assert np.array_equal(Y, Yo), (variant, np.abs(Y - Yo).max())
         assert np.array_equal(U, Uo)
 
 
-def test_nonfinite_inputs_are_flagged(cuda):
+def test_nonfinite_inputs_are_flagged_by_the_fused_kernel(cuda):
     P, m, n, B, K = 3, 16, 64, 8, 3
     A, b, _ = O.make_problem(P, m, n, B, seed=1)
     G = O.er_graph(P, 0.5, seed=1)
     y0, U0, d0 = _inits(B, P, n)
     hyp = O.hyp_table(np.zeros((K, P, 4), np.float32), MAXP)
+    run = lambda *a: _run_hip(cuda, A, *a, path="fused")[2]   # noqa: E731
     b2 = b.copy(); b2[3, 1, 2] = np.nan
-    assert _run_hip(cuda, A, b2, [G] * B, hyp, y0, U0, d0)[2] & 4
+    assert run(b2, [G] * B, hyp, y0, U0, d0) & 4
     y2 = y0.copy(); y2[0, 0, 0] = np.inf
-    assert _run_hip(cuda, A, b, [G] * B, hyp, y2, U0, d0)[2] & 1
+    assert run(b, [G] * B, hyp, y2, U0, d0) & 1
     U2 = U0.copy(); U2[7, 2, 63] = -np.inf
-    assert _run_hip(cuda, A, b, [G] * B, hyp, y0, U2, d0)[2] & 2
+    assert run(b, [G] * B, hyp, y0, U2, d0) & 2
     h2 = hyp.copy(); h2[1, 0, 0] = np.nan
-    assert _run_hip(cuda, A, b, [G] * B, h2, y0, U0, d0)[2] & 8
-    assert _run_hip(cuda, A, b, [G] * B, hyp, y0, U0, d0)[2] == 0
+    assert run(b, [G] * B, h2, y0, U0, d0) & 8
+    assert run(b, [G] * B, hyp, y0, U0, d0) == 0
+
+
+def _guard_cases(P, m, n, B, K, seed):
+    """(name, A, b, hyp, y0, U0, d0) with non-finite values placed so that each of the
+    reference's batch-global guards fires (unfolded_DLASSO.py:55-61, 84-86, 102-104)."""
+    A, b, _ = O.make_problem(P, m, n, B, seed=seed)
+    y0, U0, d0 = _inits(B, P, n, seed=seed)
+    rng = np.random.default_rng(seed)
+    hyp = O.hyp_table((0.5 * rng.standard_normal((K, P, 4))).astype(np.float32), MAXP)
+    cases = []
+    y2 = y0.copy(); y2[B - 1, P - 1, n - 1] = np.inf
+    cases.append(("y0_inf", A, b, hyp, y2, U0, d0))
+    U2 = U0.copy(); U2[0, 1 % P, 5] = np.nan
+    cases.append(("U0_nan", A, b, hyp, y0, U2, d0))
+    b2 = b.copy(); b2[B // 2, 0, 3] = np.nan
+    cases.append(("b_nan_grad", A, b2, hyp, y0, U0, d0))
+    d2 = d0.copy(); d2[1, 0, 7] = np.nan
+    cases.append(("d0_nan_grad_once", A, b, hyp, y0, U0, d2))
+    d3 = d0.copy(); d3[1, 0, 7] = np.inf
+    cases.append(("d0_inf_clamped", A, b, hyp, y0, U0, d3))
+    h2 = hyp.copy(); h2[min(2, K - 1), P - 1, 0] = np.nan
+    cases.append(("alpha_nan_ynext", A, b, h2, y0, U0, d0))
+    h3 = hyp.copy(); h3[min(1, K - 1), 0, 3] = np.inf
+    cases.append(("eta_inf_U", A, b, h3, y0, U0, d0))
+    h4 = hyp.copy(); h4[K - 1, 0, 0] = np.nan
+    cases.append(("alpha_nan_last_iter", A, b, h4, y0, U0, d0))
+    return cases
+
+
+@pytest.mark.parametrize("path", ["auto", "stepwise"])
+def test_guards_bit_exact(cuda, path):
+    """Every NaN/Inf guard of the reference, batch-global, against the oracle (which restates
+    them literally): identical iterates, U_K and guard bits. "auto" runs the fused kernel and
+    then the device-gated persistent recomputation; "stepwise" the multi-launch kernels."""
+    P, m, n, B, K = 4, 24, 96, 37, 6
+    G = O.er_graph(P, 0.6, seed=2)
+    for name, A, b, hyp, y0, U0, d0 in _guard_cases(P, m, n, B, K, seed=11):
+        Y, U, st, _ = _run_hip(cuda, A, b, [G] * B, hyp, y0, U0, d0, path=path)
+        Yo, Uo, sto = O.forward_f32(A, b, [G] * B, hyp, y0, U0, d0)
+        assert st == sto, (name, st, sto)
+        np.testing.assert_array_equal(Y, Yo, err_msg=name)
+        np.testing.assert_array_equal(U, Uo, err_msg=name)
+
+
+def test_guards_bit_exact_per_sample_graphs_large_batch(cuda):
+    """The gated persistent recomputation at a batch of several hundred workgroup items
+    (grid-stride over a one-per-CU grid) with per-sample graphs."""
+    P, m, n, B, K = 5, 64, 256, 1000, 4
+    graphs = [O.connected_er_graph(P, 0.5, seed=300 + s) for s in range(B)]
+    for name, A, b, hyp, y0, U0, d0 in _guard_cases(P, m, n, B, K, seed=5)[:3]:
+        Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0)
+        Yo, Uo, sto = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
+        assert st == sto, (name, st, sto)
+        np.testing.assert_array_equal(Y, Yo, err_msg=name)
+        np.testing.assert_array_equal(U, Uo, err_msg=name)
 
 
 def test_module_forward_matches_oracle(cuda):
