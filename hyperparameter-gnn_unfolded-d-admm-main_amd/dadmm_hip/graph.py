@@ -28,6 +28,21 @@ import numpy as np
 import torch
 
 _SHARED_CACHE: dict = {}
+_INFO_CACHE: dict = {}
+
+
+def _info(g, P: int) -> "_GraphInfo":
+    """_GraphInfo of graph ``g``, memoised on its current adjacency (graphs are mutable: the key
+    is the adjacency itself, never the object's identity)."""
+    adj = tuple(tuple(g.neighbors(p)) for p in range(P))
+    key = (P, adj)
+    hit = _INFO_CACHE.get(key)
+    if hit is None:
+        hit = _GraphInfo(adj, P)
+        if len(_INFO_CACHE) > 65536:
+            _INFO_CACHE.clear()
+        _INFO_CACHE[key] = hit
+    return hit
 
 
 class _GraphInfo:
@@ -141,10 +156,16 @@ def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
         raise RuntimeError(
             f"The size of tensor a ({batch_size}) must match the size of tensor b ({G}) at "
             "non-singleton dimension 0")
-    per = {}
-    for g in graph_list:
-        if id(g) not in per:
-            per[id(g)] = _GraphInfo([list(g.neighbors(p)) for p in range(P)], P)
+    g0 = graph_list[0]
+    same = (graph_list.count(g0) if hasattr(graph_list, "count")      # C-speed identity scan
+            else sum(1 for g in graph_list if g is g0))
+    if same == G:                   # one object repeated
+        per = {id(g0): _info(g0, P)}
+    else:
+        per = {}
+        for g in graph_list:
+            if id(g) not in per:
+                per[id(g)] = _info(g, P)
     if len(per) == 1 and G == batch_size:
         i = next(iter(per.values()))
         if i.ascending:

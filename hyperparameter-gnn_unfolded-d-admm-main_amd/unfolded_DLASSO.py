@@ -41,6 +41,8 @@ class DLASSO_unfolded(nn.Module):
         # device int32 [1]: DADMM_STATUS_* bits of the guards the last forward applied
         # (include/dadmm.h); read it with guard_warnings() (synchronises)
         self.last_status = None
+        self._table = None
+        self._table_key = None
 
     # The reference precomputes AtA eagerly (:16). The HIP path never forms it; it is kept as a
     # lazily computed attribute for callers that read it.
@@ -59,8 +61,17 @@ class DLASSO_unfolded(nn.Module):
         return self._op
 
     def hyp_table(self, K: int) -> torch.Tensor:
-        """[K, H, 4] rows seq_hyp(0..K-1), differentiable w.r.t. seq_hyp.param."""
-        return self.seq_hyp.table(K)
+        """[K, H, 4] rows seq_hyp(0..K-1), differentiable w.r.t. seq_hyp.param. Outside autograd
+        the table is memoised on (param version, K, train/eval mode)."""
+        param = self.seq_hyp.param
+        if torch.is_grad_enabled() and param.requires_grad:
+            return self.seq_hyp.table(K)
+        key = (param.data_ptr(), param._version, param.device, K, self.seq_hyp.training)
+        if self._table_key != key:
+            with torch.no_grad():
+                self._table = self.seq_hyp.table(K)
+            self._table_key = key
+        return self._table
 
     def forward(self, b, graph_list, K=None, *, inits=None):
         """b [B,P,m,1]; graph_list: B networkx graphs on agents 0..P-1 (may repeat one object).
@@ -89,9 +100,13 @@ class DLASSO_unfolded(nn.Module):
         graphs = ingest(graph_list, self.P, batch_size, device)
 
         if inits is None:
-            y0 = torch.randn((batch_size, self.P, self.n, 1), device=device) * 1e-2
-            U0 = torch.randn((batch_size, self.P, self.n, 1), device=device) * 1e-2
-            d0 = torch.randn((batch_size, self.P, self.n, 1), device=device) * 1e-2
+            # == torch.randn(shape) * 1e-2 value for value (same generator stream, same
+            # product rounding; tests/test_gpu_parity.py::test_init_draws_match_randn), one
+            # kernel per tensor instead of two
+            shape = (batch_size, self.P, self.n, 1)
+            y0 = torch.empty(shape, device=device).normal_(0.0, 1e-2)
+            U0 = torch.empty(shape, device=device).normal_(0.0, 1e-2)
+            d0 = torch.empty(shape, device=device).normal_(0.0, 1e-2)
         else:
             y0, U0, d0 = inits
         y0, U0, d0 = (x.reshape(batch_size, self.P, self.n) for x in (y0, U0, d0))

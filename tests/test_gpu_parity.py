@@ -346,3 +346,40 @@ def test_non_ascending_adjacency_bit_exact(cuda):
     Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0)
     Yo, Uo, _ = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
     assert np.array_equal(Y, Yo) and np.array_equal(U, Uo)
+
+
+@pytest.mark.parametrize("shape", [(4096, 5, 256, 1), (7, 3, 62, 1), (1, 1, 4, 1)])
+def test_init_draws_match_randn(cuda, shape):
+    """The module draws y0, U0, d0 with normal_(0, 1e-2): value for value the reference's
+    torch.randn(shape) * 1e-2 (unfolded_DLASSO.py:49-51), in the same generator order."""
+    torch.manual_seed(1234)
+    ref = [torch.randn(shape, device=cuda) * 1e-2 for _ in range(3)]
+    torch.manual_seed(1234)
+    got = [torch.empty(shape, device=cuda).normal_(0.0, 1e-2) for _ in range(3)]
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g)
+
+
+def test_module_default_inits_follow_the_seed(cuda):
+    """forward() without inits == forward() with the reference's randn draws under the same
+    seed (the module's draw order y, U, delta)."""
+    import argparse
+
+    import unfolded_DLASSO
+    P, m, n, B, K = 4, 16, 64, 12, 5
+    A, b, _ = O.make_problem(P, m, n, B, seed=3)
+    args = argparse.Namespace(GHN_iter_num=K, DADMM_mode="diff", alpha_max=0.1, tau_max=0.99,
+                              rho_max=0.99, eta_max=0.99, max_penalty_threshold=0.8,
+                              penalty_reduction_factor=0.95)
+    model = unfolded_DLASSO.DLASSO_unfolded(torch.from_numpy(A).to(cuda)[None], args).to(cuda)
+    model.eval()
+    G = O.er_graph(P, 0.5, seed=1)
+    bt = torch.from_numpy(b).to(cuda)[..., None]
+    with torch.no_grad():
+        torch.manual_seed(77)
+        Y1, _ = model(bt, [G] * B)
+        torch.manual_seed(77)
+        inits = tuple(torch.randn((B, P, n, 1), device=cuda) * 1e-2 for _ in range(3))
+        Y2, _ = model(bt, [G] * B, inits=inits)
+    assert torch.equal(Y1, Y2)
+    assert model.guard_warnings() == []
