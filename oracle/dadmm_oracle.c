@@ -70,11 +70,13 @@ static float signf_t(float x) { return (float)((0.0f < x) - (x < 0.0f)); }
 static double signd_t(double x) { return (double)((0.0 < x) - (x < 0.0)); }
 
 /* ------------------------------------------------------------------------------------------ */
-int oracle_forward_f32(int B, int P, int m, int n, int K, int variant, int hyp_mode, int H,
-                       const float* A, const float* b, const int32_t* nbr_ptr,
-                       const int32_t* nbr_idx, const float* deg, const float* hyp,
-                       const float* y0, const float* U0, const float* d0, float* Y, float* U_out,
-                       int32_t* status) {
+/* Grec / Urec (nullable, [K][B][P][n]): the trajectory the adjoint needs — the gradient of iteration
+ * k BEFORE its clamp (unfolded_DLASSO.py:73-77) and U_k entering iteration k (after the :59 guard). */
+static int forward_f32_impl(int B, int P, int m, int n, int K, int variant, int hyp_mode, int H,
+                            const float* A, const float* b, const int32_t* nbr_ptr,
+                            const int32_t* nbr_idx, const float* deg, const float* hyp,
+                            const float* y0, const float* U0, const float* d0, float* Y,
+                            float* U_out, int32_t* status, float* Grec, float* Urec) {
     if (B < 0 || P < 1 || m < 1 || n < 1 || K < 0 || (H != 1 && H != P)) return -1;
     const size_t S = (size_t)B * P * n;
     float* y = (float*)malloc(S * sizeof(float));
@@ -103,6 +105,7 @@ int oracle_forward_f32(int B, int P, int m, int n, int K, int variant, int hyp_m
         }
         if (bad_y) { memset(y, 0, S * sizeof(float)); st |= 1; }
         if (bad_u) { memset(U, 0, S * sizeof(float)); st |= 2; }
+        if (Urec) memcpy(Urec + (size_t)k * S, U, S * sizeof(float));
 
         int bad_g = 0;
 #pragma omp parallel for schedule(static) reduction(| : bad_g)
@@ -136,6 +139,7 @@ int oracle_forward_f32(int B, int P, int m, int n, int K, int variant, int hyp_m
                     float t = g + signf_t(y[e]) * h4[1];
                     t = t + U[e] * dg;
                     t = t + dl[e] * h4[2];
+                    if (Grec) Grec[(size_t)k * S + e] = t;
                     t = clampf_t(t, -gclip, gclip); /* :80-81 */
                     bad_g |= (t != t);
                     gr[e] = t;
@@ -196,6 +200,25 @@ int oracle_forward_f32(int B, int P, int m, int n, int K, int variant, int hyp_m
     if (status) *status = st;
     free(y); free(U); free(dl); free(yn); free(gr);
     return 0;
+}
+
+int oracle_forward_f32(int B, int P, int m, int n, int K, int variant, int hyp_mode, int H,
+                       const float* A, const float* b, const int32_t* nbr_ptr,
+                       const int32_t* nbr_idx, const float* deg, const float* hyp,
+                       const float* y0, const float* U0, const float* d0, float* Y, float* U_out,
+                       int32_t* status) {
+    return forward_f32_impl(B, P, m, n, K, variant, hyp_mode, H, A, b, nbr_ptr, nbr_idx, deg, hyp,
+                            y0, U0, d0, Y, U_out, status, NULL, NULL);
+}
+
+/* oracle_forward_f32 that also records the adjoint's trajectory (Grec, Urec: [K][B][P][n]). */
+int oracle_forward_f32_rec(int B, int P, int m, int n, int K, int variant, int hyp_mode, int H,
+                           const float* A, const float* b, const int32_t* nbr_ptr,
+                           const int32_t* nbr_idx, const float* deg, const float* hyp,
+                           const float* y0, const float* U0, const float* d0, float* Y,
+                           float* U_out, int32_t* status, float* Grec, float* Urec) {
+    return forward_f32_impl(B, P, m, n, K, variant, hyp_mode, H, A, b, nbr_ptr, nbr_idx, deg, hyp,
+                            y0, U0, d0, Y, U_out, status, Grec, Urec);
 }
 
 /* ------------------------------------------------------------------------------------------ */

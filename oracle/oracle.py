@@ -6,6 +6,8 @@ Restates, from the reference source text:
   * ``DLASSO_unfolded.forward`` + ``compute_delta``  unfolded_DLASSO.py:34-140    -> forward_f32/_f64
     (C: oracle/dadmm_oracle.c), and a vectorised numpy fp64 form (forward_np64) used as an
     independent second restatement
+  * the reverse-mode derivative of that forward w.r.t. the hyper-parameter table, as torch autograd
+    takes it through the reference's eager ops (clamp/sign/matmul backward rules)   -> backward_np64
   * ``gnn_dlasso_utils.compute_loss``                gnn_dlasso_utils.py:27-88    -> compute_loss()
   * ``gnn_dlasso_utils.set_A`` / ``gnn_data.set_Data`` (input distribution)       -> make_problem()
   * reading the reference's shipped fixtures (A.pt, model.pt) without unpickling  -> load_fixture()
@@ -20,6 +22,7 @@ import numpy as np
 
 __all__ = [
     "lib", "hyp_table", "graph_arrays", "forward_f32", "forward_f64", "forward_np64",
+    "forward_f32_rec", "laplacians", "backward_np64",
     "compute_loss", "make_problem", "load_fixture_tensor", "er_graph", "connected_er_graph",
 ]
 
@@ -42,6 +45,8 @@ def lib() -> ctypes.CDLL:
             f = getattr(L, name)
             f.restype = ctypes.c_int
             f.argtypes = [i, i, i, i, i, i, i, i] + [fp] * 12
+        L.oracle_forward_f32_rec.restype = ctypes.c_int
+        L.oracle_forward_f32_rec.argtypes = [i, i, i, i, i, i, i, i] + [fp] * 14
         L.oracle_abi_version.restype = ctypes.c_int
         _LIB = L
     return _LIB
@@ -91,7 +96,7 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
-def _run(fn, out_dt, A, b, graph_list, hyp, y0, U0, d0, variant, hyp_mode):
+def _run(fn, out_dt, A, b, graph_list, hyp, y0, U0, d0, variant, hyp_mode, rec=None):
     A = _c(A, np.float32).reshape(A.shape[-3:]) if A.ndim == 4 else _c(A, np.float32)
     P, m, n = A.shape
     B = y0.shape[0]
@@ -109,8 +114,13 @@ def _run(fn, out_dt, A, b, graph_list, hyp, y0, U0, d0, variant, hyp_mode):
     Y = np.empty((K, B, P, n), out_dt)
     U = np.empty((B, P, n), out_dt)
     st = np.zeros(1, np.int32)
+    extra = ()
+    if rec is not None:
+        rec[0] = np.empty((K, B, P, n), out_dt)
+        rec[1] = np.empty((K, B, P, n), out_dt)
+        extra = (_ptr(rec[0]), _ptr(rec[1]))
     rc = fn(B, P, m, n, K, variant, hyp_mode, H, _ptr(A), _ptr(b), _ptr(nbr_ptr), _ptr(nbr_idx),
-            _ptr(deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U), _ptr(st))
+            _ptr(deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U), _ptr(st), *extra)
     if rc != 0:
         raise RuntimeError(f"oracle returned {rc}")
     return Y, U, int(st[0])
@@ -124,6 +134,17 @@ def forward_f32(A, b, graph_list, hyp, y0, U0, d0, variant=0, hyp_mode=0):
     Returns (Y [K,B,P,n] float32, U_K [B,P,n] float32, guard status bits)."""
     return _run(lib().oracle_forward_f32, np.float32, A, b, graph_list, hyp, y0, U0, d0, variant,
                 hyp_mode)
+
+
+def forward_f32_rec(A, b, graph_list, hyp, y0, U0, d0, variant=0, hyp_mode=0):
+    """forward_f32 that also records the adjoint's trajectory.
+
+    Returns (Y, U_K, status, Grec, Urec): Grec[k] = the gradient of iteration k before its clamp
+    (unfolded_DLASSO.py:73-77), Urec[k] = U_k entering iteration k; both [K,B,P,n] float32."""
+    rec = [None, None]
+    Y, U, st = _run(lib().oracle_forward_f32_rec, np.float32, A, b, graph_list, hyp, y0, U0, d0,
+                    variant, hyp_mode, rec)
+    return Y, U, st, rec[0], rec[1]
 
 
 def forward_f64(A, b, graph_list, hyp, y0, U0, d0, variant=0, hyp_mode=0):
@@ -169,6 +190,102 @@ def forward_np64(A, b, graph_list, hyp, y0, U0, d0, variant=0):
         y = yn
         Y.append(y)
     return np.stack(Y), U
+
+
+def laplacians(graph_list, P):
+    """(D - Adj) per sample [B,P,P] float64 and degrees [B,P] (compute_delta = 2 (D - Adj) y)."""
+    B = len(graph_list)
+    L = np.zeros((B, P, P))
+    deg = np.zeros((B, P))
+    for s, G in enumerate(graph_list):
+        for p in range(P):
+            for q in G.neighbors(p):
+                L[s, p, q] -= 1.0
+                deg[s, p] += 1.0
+        L[s] += np.diag(deg[s])
+    return L, deg
+
+
+def backward_np64(A, graph_list, hyp, y0, d0, Y, Grec, Urec, gY, variant=0):
+    """d(sum_k <gY[k], Y[k]>) / d hyp  ->  [K, H, 4] float64, in reverse mode along a recorded
+    trajectory (Y, Grec, Urec as forward_f32_rec / the HIP recording path return them).
+
+    Follows the derivative torch autograd takes through the reference's forward
+    (unfolded_DLASSO.py:53-107): sign() has zero derivative; clamp(x, lo, hi) passes the
+    gradient where lo <= x <= hi; delta_{k+1} = compute_delta(y_{k+1}) = 2 (D - Adj) y_{k+1} is
+    differentiated (its transpose is itself), delta_0 is a random leaf; b, y0, U0 carry no
+    gradient. Per iteration k (a = alpha_k, ...; g = clamp(gr_k); z = y_k - a g; w = U_k + d_{k+1} e):
+        dEta_k   += sum(w_bar d_{k+1})            w_bar = U_bar [|w| <= vclip]
+        d_bar    += w_bar e ;  y_bar += 2 L d_bar  (GNN variant: d_bar masked by |2Ly| <= 20)
+        z_bar     = y_bar [|z| <= vclip] ;  dAlpha_k += sum(-z_bar g)
+        gr_bar    = -a z_bar [|gr| <= gclip]
+        dTau_k   += sum(gr_bar sign(y_k)) ;  dRho_k += sum(gr_bar d_k)
+        U_bar     = w_bar + deg gr_bar ;  d_bar = rho gr_bar ;  y_bar = z_bar + AtA gr_bar
+    z is re-evaluated in the trajectory's dtype (two roundings, as the kernels do); w and the
+    consensus in float64, so a float32 trajectory can differ from the kernels' masks only where
+    |w| or |2Ly| lies within rounding of its clip bound. Sums run over the batch and n; for
+    H = 1 ('same' mode) also over the agents. No guard handling: finite trajectories only.
+    """
+    A = np.asarray(A, np.float64).reshape(np.shape(A)[-3:])
+    P, m, n = A.shape
+    K, B = Y.shape[0], Y.shape[1]
+    tdt = np.asarray(Y).dtype
+    AtA = np.einsum("pri,prj->pij", A, A)
+    L, deg = laplacians(graph_list, P)
+    hyp = np.asarray(hyp)
+    H = hyp.shape[1]
+    Yd = np.asarray(Y, np.float64).reshape(K, B, P, n)
+    y0d = np.asarray(y0, np.float64).reshape(B, P, n)
+    d0d = np.asarray(d0, np.float64).reshape(B, P, n)
+    gY = np.asarray(gY, np.float64).reshape(K, B, P, n)
+    dh = np.zeros((K, P, 4))
+    yb = np.zeros((B, P, n))
+    Ub = np.zeros((B, P, n))
+    db = np.zeros((B, P, n))
+
+    def cons(x):
+        return 2.0 * np.einsum("bpq,bqi->bpi", L, x)
+
+    for k in reversed(range(K)):
+        hk = np.broadcast_to(hyp[k], (P, 4))
+        al, ta, rh, et = (hk[:, c].astype(np.float64)[None, :, None] for c in range(4))
+        gclip = max(1.0, 30.0 - k) if variant == 0 else 10.0
+        vclip = max(10.0, 200.0 - 3 * k) if variant == 0 else 100.0
+        y1 = Yd[k]
+        yk = Yd[k - 1] if k > 0 else y0d
+        d1 = cons(y1)
+        md1 = None
+        if variant != 0:
+            md1 = np.abs(d1) <= 20.0
+            d1 = np.clip(d1, -20.0, 20.0)
+        if k > 0:
+            dk = cons(yk)
+            if variant != 0:
+                dk = np.clip(dk, -20.0, 20.0)
+        else:
+            dk = d0d
+        yb = yb + gY[k]
+        w = np.asarray(Urec[k], np.float64) + d1 * et
+        wb = Ub * (np.abs(w) <= vclip)
+        dh[k, :, 3] += (wb * d1).sum(axis=(0, 2))
+        d1b = db + wb * et
+        if md1 is not None:
+            d1b = d1b * md1
+        yb = yb + cons(d1b)
+        gr = np.asarray(Grec[k], np.float64)
+        g = np.clip(gr, -gclip, gclip)
+        z = (np.asarray(yk, tdt) - hk[:, 0].astype(tdt)[None, :, None] * g.astype(tdt)).astype(np.float64)
+        zb = yb * (np.abs(z) <= vclip)
+        dh[k, :, 0] += (-zb * g).sum(axis=(0, 2))
+        grb = -al * zb * (np.abs(gr) <= gclip)
+        dh[k, :, 1] += (grb * np.sign(yk)).sum(axis=(0, 2))
+        dh[k, :, 2] += (grb * dk).sum(axis=(0, 2))
+        Ub = wb + grb * deg[:, :, None]
+        db = grb * rh
+        yb = zb + np.einsum("pij,bpj->bpi", AtA, grb)
+    if H == 1:
+        dh = dh.sum(axis=1, keepdims=True)
+    return dh
 
 
 def compute_loss(Y, label):

@@ -85,3 +85,63 @@ def forward(A, b, graph_list, hyp, y0, U0, d0, variant=0, dtype=torch.float32):
         y = yn
         Y.append(y)
     return torch.stack(Y)[..., 0].numpy()
+
+
+def forward_autograd(A, b, graph_list, hyp, y0, U0, d0, variant=0, dtype=torch.float64):
+    """The same op sequence as ``forward`` (no guards: finite inputs only) on torch tensors that keep
+    the autograd graph, so ``torch.autograd.grad`` takes exactly the derivative the reference's
+    ``loss.backward()`` takes (unfolded_train_new.py:78). ``hyp`` [K,H,4] is a
+    tensor (may require grad). Returns (Y [K,B,P,n], Grec [K,B,P,n] pre-clamp gradients,
+    Urec [K,B,P,n] U_k entering iteration k, U_K); Grec/Urec/U_K are detached."""
+    A = torch.as_tensor(np.asarray(A), dtype=dtype)
+    if A.dim() == 3:
+        A = A[None]
+    _, P, m, n = A.shape
+    B = y0.shape[0]
+    b = torch.as_tensor(np.asarray(b), dtype=dtype).reshape(B, P, m, 1)
+    AtA = torch.stack([A[0, p].T @ A[0, p] for p in range(P)])[None]
+    Atb = _atx(A, b)
+    deg = torch.zeros((B, P, 1, 1), dtype=dtype)
+    for s in range(B):
+        for p in range(P):
+            deg[s, p] = len(list(graph_list[s].neighbors(p)))
+    y = torch.as_tensor(np.asarray(y0), dtype=dtype).reshape(B, P, n, 1)
+    U = torch.as_tensor(np.asarray(U0), dtype=dtype).reshape(B, P, n, 1)
+    d = torch.as_tensor(np.asarray(d0), dtype=dtype).reshape(B, P, n, 1)
+    Y, G, Ur = [], [], []
+    for k in range(hyp.shape[0]):
+        h = hyp[k]
+        al, ta, rh, et = (h[:, c].reshape(1, -1, 1, 1) for c in range(4))
+        AtAy = torch.stack([AtA[0, p] @ y[:, p] for p in range(P)], dim=1)
+        grad = AtAy - Atb + y.sign() * ta + U * deg + d * rh
+        G.append(grad.detach())
+        Ur.append(U.detach())
+        gclip = max(1.0, 30.0 - k) if variant == 0 else 10.0
+        vclip = max(10.0, 200.0 - k * 3) if variant == 0 else 100.0
+        grad = torch.clamp(grad, -gclip, gclip)
+        yn = torch.clamp(y - al * grad, -vclip, vclip)
+        d = _delta_autograd(graph_list, yn, P)
+        if variant != 0:
+            d = torch.clamp(d, -20.0, 20.0)
+        U = torch.clamp(U + d * et, -vclip, vclip)
+        y = yn
+        Y.append(y)
+    sq = lambda L: torch.stack(L)[..., 0]
+    return sq(Y), sq(G), sq(Ur), U.detach()[..., 0]
+
+
+def _delta_autograd(graph_list, y, P):
+    # compute_delta's edge loop (unfolded_DLASSO.py:127-140) without in-place writes, so autograd
+    # can run through it: same terms, same per-agent accumulation order
+    B = len(graph_list)
+    rows = []
+    for s in range(B):
+        G = graph_list[s]
+        acc = [torch.zeros_like(y[s, 0]) for _ in range(P)]
+        for p in range(P):
+            for q in G.neighbors(p):
+                diff = y[s, p] - y[s, q]
+                acc[p] = acc[p] + diff
+                acc[q] = acc[q] - diff
+        rows.append(torch.stack(acc))
+    return torch.stack(rows)

@@ -281,3 +281,76 @@ def test_fixture_trained_hyp_ranges():
     h = O.hyp_table(TRAINED, MAXP)
     assert 0.0175 <= h[..., 0].min() and h[..., 0].max() <= 0.0502
     assert 0.494 <= h[..., 1].min() and h[..., 1].max() <= 0.923
+
+
+# ---- the adjoint (§8(f) row 1): reverse mode of the forward w.r.t. the hyper-parameter table ---
+@pytest.mark.parametrize("variant,H,per_sample", [(0, 5, False), (0, 1, False), (1, 5, True),
+                                                  (1, 1, True)])
+def test_adjoint_matches_torch_autograd_of_the_reference_ops(variant, H, per_sample):
+    """backward_np64 == torch.autograd.grad through the reference's op sequence (fp64 replay,
+    unfolded_DLASSO.py:53-107 + compute_delta's edge loop), on the same trajectory."""
+    import torch
+    P, m, n, B, K = 5, 16, 48, 3, 12
+    A, b, _ = O.make_problem(P, m, n, B, seed=31)
+    if per_sample:
+        graphs = [O.connected_er_graph(P, 0.5, seed=60 + s) for s in range(B)]
+    else:
+        graphs = [O.er_graph(P, 0.5, seed=7)] * B
+    y0, U0, d0 = _inits(B, P, n, seed=5)
+    param = TRAINED[:K, :P] if H == P else TRAINED[:K, :1]
+    hyp = O.hyp_table(param, MAXP)
+    ht = torch.tensor(hyp, dtype=torch.float64, requires_grad=True)
+    Y, Gr, Ur, _ = ref_torch.forward_autograd(A, b, graphs, ht, y0, U0, d0, variant=variant)
+    gY = torch.randn(Y.shape, dtype=torch.float64, generator=torch.Generator().manual_seed(3))
+    want, = torch.autograd.grad((Y * gY).sum(), ht)
+    got = O.backward_np64(A, graphs, hyp, y0, d0, Y.detach().numpy(), Gr.numpy(), Ur.numpy(),
+                          gY.numpy(), variant=variant)
+    assert got.shape == (K, H, 4)
+    np.testing.assert_allclose(got, want.numpy(), rtol=1e-9, atol=1e-9 * np.abs(want.numpy()).max())
+    # the gradient clamp really is active in this regime (the Gram path is cut on most lanes)
+    gclip = np.array([max(1.0, 30.0 - k) if variant == 0 else 10.0 for k in range(K)])
+    assert (np.abs(Gr.numpy()) > gclip[:, None, None, None]).mean() > 0.1
+
+
+def test_forward_f32_rec_records_the_trajectory():
+    """Grec/Urec of the order-matched fp32 oracle: Y unchanged, and every y_{k+1} follows from the
+    recorded (y_k, Grec[k]) by the reference's clamp/update (:80-93) bit-for-bit."""
+    P, m, n, B, K = 5, 16, 64, 4, 10
+    A, b, _ = O.make_problem(P, m, n, B, seed=8)
+    graphs = [O.er_graph(P, 0.5, seed=7)] * B
+    y0, U0, d0 = _inits(B, P, n, seed=2)
+    hyp = O.hyp_table(TRAINED[:K, :P], MAXP)
+    Y, U, st = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
+    Yr, Ur_, st2, G, Urec = O.forward_f32_rec(A, b, graphs, hyp, y0, U0, d0)
+    assert st == st2 == 0
+    assert np.array_equal(Y, Yr) and np.array_equal(U, Ur_)
+    assert np.array_equal(Urec[0], U0)
+    for k in range(K):
+        yk = y0 if k == 0 else Y[k - 1]
+        gc, vc = np.float32(max(1.0, 30.0 - k)), np.float32(max(10.0, 200.0 - 3 * k))
+        g = np.clip(G[k], -gc, gc)
+        al = hyp[k][:, 0][None, :, None]
+        assert np.array_equal(np.clip(yk - al * g, -vc, vc), Y[k])
+
+
+def test_adjoint_sensitivity_fp32_vs_fp64_trajectory():
+    """The adjoint inherits the forward's sensitivity: an fp32 and an fp64 trajectory of the same
+    problem drift apart (clamp masks flip where a lane sits near a bound), and the
+    adjoints along them differ by up to a few percent of the largest entry. That is why the GPU
+    tests check the HIP adjoint along the kernel's OWN recorded trajectory (tight tolerance), and
+    only this loose band against the fp64 trajectory."""
+    import torch
+    P, m, n, B, K = 5, 32, 128, 4, 25
+    A, b, _ = O.make_problem(P, m, n, B, seed=9)
+    graphs = [O.er_graph(P, 0.5, seed=7)] * B
+    y0, U0, d0 = _inits(B, P, n, seed=4)
+    hyp = O.hyp_table(TRAINED[:K, :P], MAXP)
+    rng = np.random.default_rng(0)
+    gY = np.zeros((K, B, P, n))
+    gY[-1] = rng.standard_normal((B, P, n))
+    ht = torch.tensor(hyp, dtype=torch.float64)
+    Y64, G64, U64, _ = ref_torch.forward_autograd(A, b, graphs, ht, y0, U0, d0)
+    d64 = O.backward_np64(A, graphs, hyp, y0, d0, Y64.numpy(), G64.numpy(), U64.numpy(), gY)
+    Y32, _, _, G32, U32 = O.forward_f32_rec(A, b, graphs, hyp, y0, U0, d0)
+    d32 = O.backward_np64(A, graphs, hyp, y0, d0, Y32, G32, U32, gY)
+    assert np.abs(d32 - d64).max() <= 0.1 * np.abs(d64).max()
