@@ -78,19 +78,13 @@ int dadmm_prepare_operator(const dadmm_dims* d, const float* A, void* op, void* 
     return ok();
 }
 
-int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
-                  const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
-                  const float* U0, const float* d0, float* Y, float* U_out, int32_t* status,
-                  void* stream) {
-    int rc = check_dims(d);
-    if (rc) return rc;
-    if (d->B == 0 || d->K == 0) return ok();
-    if (!op || !b || !nbr || !deg || !hyp || !y0 || !U0 || !d0 || !Y)
-        return fail(DADMM_EINVAL, "a required pointer is NULL");
-    if (!aligned16(op)) return fail(DADMM_EINVAL, "op workspace must be 16-byte aligned");
-    if (!aligned16(Y) || !aligned16(y0) || !aligned16(U0) || !aligned16(d0) ||
-        (U_out != nullptr && !aligned16(U_out)))
-        return fail(DADMM_EINVAL, "Y, y0, U0, d0 and U_out must be 16-byte aligned");
+}  // extern "C"
+
+namespace {
+
+// shape checks shared by the fused forward (plain / recording) and the fused adjoint; on success
+// *graph and *nt select the compiled configuration
+int check_fused_shape(const dadmm_dims* d, const uint32_t* nbr_order, int* graph, int* nt) {
     if (d->m > dadmm::M_PAD)
         return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
                     dadmm::M_PAD);
@@ -98,14 +92,35 @@ int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uin
         return fail(DADMM_EUNSUPPORTED, "n=%d: the fused kernel needs n %% 4 == 0 (zero-pad n)", d->n);
     if ((size_t)d->B * d->P * d->n * 4 >= ((size_t)1 << 31))
         return fail(DADMM_EUNSUPPORTED, "B*P*n*4 >= 2^31 bytes per iterate (split the batch)");
-    const int nt = dadmm::fused_nt(d->n);
     if (nbr_order != nullptr && d->graph_shared)
         return fail(DADMM_EINVAL, "nbr_order needs per-sample graphs (graph_shared = 0)");
     if (nbr_order != nullptr && d->P > 8)
         return fail(DADMM_EINVAL, "nbr_order packs 4-bit agent ids: P <= 8");
-    const int graph = d->graph_shared ? dadmm::GRAPH_SHARED
-                                      : (nbr_order ? dadmm::GRAPH_ORDERED : dadmm::GRAPH_LANE);
-    dadmm::fused_fn_ptr fn = dadmm::find_fused(d->P, nt, graph);
+    *nt = dadmm::fused_nt(d->n);
+    *graph = d->graph_shared ? dadmm::GRAPH_SHARED
+                             : (nbr_order ? dadmm::GRAPH_ORDERED : dadmm::GRAPH_LANE);
+    return DADMM_OK;
+}
+
+int forward_impl(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
+                 const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
+                 const float* U0, const float* d0, float* Y, float* Grec, float* Urec,
+                 float* U_out, int32_t* status, void* stream, bool rec) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (d->B == 0 || d->K == 0) return ok();
+    if (rec && (Grec == nullptr || Urec == nullptr || !aligned16(Grec) || !aligned16(Urec)))
+        return fail(DADMM_EINVAL, "Grec and Urec must be non-NULL and 16-byte aligned");
+    if (!op || !b || !nbr || !deg || !hyp || !y0 || !U0 || !d0 || !Y)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(op)) return fail(DADMM_EINVAL, "op workspace must be 16-byte aligned");
+    if (!aligned16(Y) || !aligned16(y0) || !aligned16(U0) || !aligned16(d0) ||
+        (U_out != nullptr && !aligned16(U_out)))
+        return fail(DADMM_EINVAL, "Y, y0, U0, d0 and U_out must be 16-byte aligned");
+    int graph = 0, nt = 0;
+    if ((rc = check_fused_shape(d, nbr_order, &graph, &nt)) != DADMM_OK) return rc;
+    dadmm::fused_fn_ptr fn = rec ? dadmm::find_fused_rec(d->P, nt, graph)
+                                 : dadmm::find_fused(d->P, nt, graph);
     if (fn == nullptr)
         return fail(DADMM_EUNSUPPORTED, "no fused kernel for P=%d n=%d (n_pad=%d)", d->P, d->n,
                     64 * nt);
@@ -124,6 +139,8 @@ int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uin
     a.Y = Y;
     a.U_out = U_out;
     a.status = status;
+    a.Grec = Grec;
+    a.Urec = Urec;
     a.B = d->B;
     a.m = d->m;
     a.n = d->n;
@@ -132,6 +149,88 @@ int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uin
     a.variant = d->variant;
     hipError_t e = fn(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(DADMM_EHIP, "fused launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+}  // namespace
+
+extern "C" {
+
+int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
+                  const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
+                  const float* U0, const float* d0, float* Y, float* U_out, int32_t* status,
+                  void* stream) {
+    return forward_impl(d, op, b, nbr, nbr_order, deg, hyp, y0, U0, d0, Y, nullptr, nullptr, U_out,
+                        status, stream, false);
+}
+
+int dadmm_forward_record(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
+                         const uint32_t* nbr_order, const float* deg, const float* hyp,
+                         const float* y0, const float* U0, const float* d0, float* Y, float* Grec,
+                         float* Urec, float* U_out, int32_t* status, void* stream) {
+    return forward_impl(d, op, b, nbr, nbr_order, deg, hyp, y0, U0, d0, Y, Grec, Urec, U_out,
+                        status, stream, true);
+}
+
+size_t dadmm_backward_scratch_bytes(const dadmm_dims* d) {
+    if (check_dims(d) != DADMM_OK) return 0;
+    const size_t nwg = ((size_t)d->B + dadmm::BT - 1) / dadmm::BT;
+    const size_t bytes = sizeof(float) * nwg * (size_t)d->K * d->P * 4;
+    return bytes > 0 ? bytes : 16;
+}
+
+int dadmm_backward(const dadmm_dims* d, const void* op, const uint64_t* nbr,
+                   const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
+                   const float* d0, const float* Y, const float* Grec, const float* Urec,
+                   const float* gY, float* dhyp, void* scratch, void* stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (d->K == 0) return ok();
+    if (!dhyp) return fail(DADMM_EINVAL, "dhyp is NULL");
+    if (d->B == 0) {
+        hipError_t e = hipMemsetAsync(dhyp, 0, sizeof(float) * (size_t)d->K * d->hyp_rows * 4,
+                                      (hipStream_t)stream);
+        if (e != hipSuccess) return fail(DADMM_EHIP, "memset: %s", hipGetErrorString(e));
+        return ok();
+    }
+    if (!op || !nbr || !deg || !hyp || !y0 || !d0 || !Y || !Grec || !Urec || !gY || !scratch)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(op) || !aligned16(Y) || !aligned16(y0) || !aligned16(d0) || !aligned16(Grec) ||
+        !aligned16(Urec) || !aligned16(gY) || !aligned16(scratch))
+        return fail(DADMM_EINVAL, "op, Y, y0, d0, Grec, Urec, gY and scratch must be 16-byte aligned");
+    int graph = 0, nt = 0;
+    if ((rc = check_fused_shape(d, nbr_order, &graph, &nt)) != DADMM_OK) return rc;
+    dadmm::backward_fn_ptr fn = dadmm::find_backward(d->P, nt, graph);
+    if (fn == nullptr)
+        return fail(DADMM_EUNSUPPORTED, "no adjoint kernel for P=%d n=%d (n_pad=%d)", d->P, d->n,
+                    64 * nt);
+    const int np = 64 * nt;
+    dadmm::BackwardArgs a;
+    a.A = (const float*)op;
+    a.At = a.A + (size_t)d->P * dadmm::M_PAD * np;
+    a.nbr = nbr;
+    a.nbr_order = nbr_order;
+    a.deg = deg;
+    a.hyp = hyp;
+    a.y0 = y0;
+    a.d0 = d0;
+    a.Y = Y;
+    a.Grec = Grec;
+    a.Urec = Urec;
+    a.gY = gY;
+    a.partial = (float*)scratch;
+    a.B = d->B;
+    a.m = d->m;
+    a.n = d->n;
+    a.K = d->K;
+    a.hyp_rows = d->hyp_rows;
+    a.variant = d->variant;
+    hipError_t e = fn(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "adjoint launch: %s", hipGetErrorString(e));
+    const int nwg = (d->B + dadmm::BT - 1) / dadmm::BT;
+    e = dadmm::launch_backward_reduce(a.partial, dhyp, nwg, d->K, d->P, d->hyp_rows,
+                                      (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "adjoint reduce launch: %s", hipGetErrorString(e));
     return ok();
 }
 
@@ -146,8 +245,8 @@ size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d) {
 int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
                            const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
                            const float* hyp, const float* y0, const float* U0, const float* d0,
-                           float* Y, float* U_out, int32_t* status, int32_t gate, void* scratch,
-                           void* stream) {
+                           float* Y, float* U_out, float* Grec, float* Urec, int32_t* status,
+                           int32_t gate, void* scratch, void* stream) {
     int rc = check_dims(d);
     if (rc) return rc;
     if (gate != 0 && gate != 1) return fail(DADMM_EINVAL, "gate must be 0 or 1");
@@ -159,6 +258,10 @@ int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
         (U_out != nullptr && !aligned16(U_out)))
         return fail(DADMM_EINVAL, "op, Y, y0, U0, d0 and U_out must be 16-byte aligned");
     if (((uintptr_t)scratch & 255u) != 0) return fail(DADMM_EINVAL, "scratch must be 256-byte aligned");
+    if ((Grec == nullptr) != (Urec == nullptr))
+        return fail(DADMM_EINVAL, "Grec and Urec: both or neither");
+    if (Grec != nullptr && (!aligned16(Grec) || !aligned16(Urec)))
+        return fail(DADMM_EINVAL, "Grec and Urec must be 16-byte aligned");
     if (d->m > dadmm::M_PAD)
         return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
                     dadmm::M_PAD);
@@ -184,6 +287,8 @@ int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
     a.U = U_out != nullptr ? U_out : (float*)(base + 2 * state);
     a.flags = (int32_t*)scratch;
     a.status = status;
+    a.Grec = Grec;
+    a.Urec = Urec;
     a.B = d->B;
     a.P = d->P;
     a.m = d->m;

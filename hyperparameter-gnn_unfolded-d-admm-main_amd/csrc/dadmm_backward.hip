@@ -1,0 +1,408 @@
+// dadmm_backward.hip — the adjoint of the fused unfolded D-ADMM forward for gfx950 (MI355X).
+//
+// Computes dL/dhyp [K][H][4] (alpha, tau, rho, eta) for L = sum_k <gY[k], Y[k]>, i.e. what torch
+// autograd returns for the hyper-parameter rows when a driver calls loss.backward() through
+// DLASSO_unfolded.forward (unfolded_train_new.py:74-80; forward unfolded_DLASSO.py:53-107). The
+// derivative follows torch's rules for the reference's eager ops: sign() has zero derivative,
+// clamp(x, lo, hi) passes the gradient where lo <= x <= hi, delta_{k+1} = compute_delta(y_{k+1})
+// = 2 (D - Adj) y_{k+1} is differentiated (the map is its own transpose), delta_0 is a random leaf,
+// and b / y0 / U0 carry no gradient. The oracle is oracle.backward_np64 (pinned to torch autograd
+// through the reference's op sequence, tests/test_oracle.py).
+//
+// Reverse sweep along the trajectory the recording forward stored (Y, Grec = pre-clamp gradient,
+// Urec = U_k). Per iteration k, with g = clamp(gr_k), z = y_k - alpha g, w = U_k + delta_{k+1} eta:
+//   w_bar = U_bar [|w| <= vclip]            dEta   += w_bar delta_{k+1}
+//   d_bar = rho_{k+1} gr_bar_{k+1} + w_bar eta     (GNN variant: masked by |2 L y_{k+1}| <= 20)
+//   y_bar += gY[k] + 2 L d_bar
+//   z_bar = y_bar [|z| <= vclip]            dAlpha -= z_bar g
+//   gr_bar = -alpha z_bar [|gr| <= gclip]   dTau   += gr_bar sign(y_k);  dRho += gr_bar delta_k
+//   U_bar = w_bar + deg gr_bar ;  y_bar = z_bar + A^T (A gr_bar)
+// The masks are re-evaluated with the forward's own float operations (same consensus order, same
+// two-rounding update), so they are exactly the forward's.
+//
+// Layout mirrors the forward: one workgroup = 16 samples x all P agents x all K
+// iterations (reversed), 8 waves; a lane owns rows nb*16 + 4h + r of every agent of sample j, so
+// the consensus and its adjoint are lane-local. The Gram product of gr_bar is the forward's GEMM
+// pair with gr_bar as the B operand (LDS) and no -b seed. dhyp partial sums: per lane -> wave
+// (shuffles) -> workgroup (LDS, fixed order) -> partial[wg][k][P][4]; bwd_reduce_kernel sums the
+// workgroups in a fixed order (deterministic).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dadmm_consensus.h"
+#include "dadmm_internal.h"
+
+namespace dadmm {
+namespace bwd {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ float tclamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+__device__ __forceinline__ bool inside(float x, float lo, float hi) { return x >= lo && x <= hi; }
+
+constexpr int WAVES = 8;
+
+template <int P, int NT, int GRAPH, int HALF>
+__device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ lds, const int w) {
+    constexpr int AS = WAVES / 4;                   // GEMM1 agent stride
+    constexpr int MP = M_PAD;
+    constexpr int NP = NT * 64;
+    constexpr int NB = NP / 16;
+    constexpr int T2 = (NB + WAVES - 1) / WAVES;
+    constexpr int E = T2 * 4;
+    constexpr int TH = (P - HALF + AS - 1) / AS;
+    constexpr int THA = TH > 0 ? TH : 1;
+    constexpr int YS = NP + 4;
+    constexpr int RS = MP + 4;
+    float* __restrict__ Glds = lds;                 // [P][BT][YS]  gr_bar (GEMM B operand)
+    float* __restrict__ Rlds = lds + P * BT * YS;   // [P][BT][RS]  A gr_bar
+    float* __restrict__ red = Rlds + P * BT * RS;   // [WAVES][P][4] partial sums
+
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15;
+    const int h = lane >> 4;
+    const int s = blockIdx.x * BT + j;
+    const bool sv = s < a.B;
+    const int n = a.n, B = a.B, K = a.K;
+    const int mb = w & 3;
+    const bool has_tiles = w * T2 < NB;
+    const uint32_t state_bytes = (uint32_t)((size_t)B * P * n * 4);
+    const size_t S = (size_t)B * P * n;
+    const rsrc_t rA = make_rsrc(a.A, (uint32_t)(P * MP * NP * 4));
+    const rsrc_t rAt = make_rsrc(a.At, (uint32_t)(P * MP * NP * 4));
+
+    uint32_t msk[P], ord[P];
+    float dg[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        if (GRAPH == GRAPH_SHARED) {
+            msk[p] = __builtin_amdgcn_readfirstlane((uint32_t)a.nbr[p]);
+            dg[p] = a.deg[p];
+        } else {
+            msk[p] = sv ? (uint32_t)a.nbr[(size_t)s * P + p] : 0u;
+            dg[p] = sv ? a.deg[(size_t)s * P + p] : 0.0f;
+        }
+        ord[p] = (GRAPH == GRAPH_ORDERED && sv) ? a.nbr_order[(size_t)s * P + p] : 0u;
+    }
+
+    // carried state: y_bar, U_bar (adjoints w.r.t. y_{k+1}, U_{k+1}) and y_{k+1} itself;
+    // d_bar (w.r.t. delta_{k+1}) is rho_{k+1} * gr_bar_{k+1}, read back from this lane's Glds rows
+    float yb[P][E], Ub[P][E], y1[P][E];
+    {
+        const rsrc_t ry = make_rsrc(a.Y + (size_t)(K - 1) * S, state_bytes);
+#pragma unroll
+        for (int tt = 0; tt < T2; ++tt) {
+            const int n0 = (w * T2 + tt) * 16 + 4 * h;
+            const bool ok = has_tiles && n0 < n;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+                if (ok) v = bload4(ry, (uint32_t)(((s * P + p) * n + n0) * 4), 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    y1[p][4 * tt + r] = v[r];
+                    yb[p][4 * tt + r] = 0.0f;
+                    Ub[p][4 * tt + r] = 0.0f;
+                }
+                if (has_tiles) *(f32x4*)(Glds + (p * BT + j) * YS + n0) = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+            }
+        }
+    }
+    float rh_next[P];   // rho_{k+1} (0 at k = K-1: no later iteration reads delta_K)
+#pragma unroll
+    for (int p = 0; p < P; ++p) rh_next[p] = 0.0f;
+
+    const uint32_t voffA = (uint32_t)(((16 * mb + j) * NP + 4 * h) * 4);
+    const uint32_t voffAt = (uint32_t)((j * MP + 4 * h) * 4);
+    const float* brow = Glds + j * YS + 4 * h;
+    __syncthreads();
+
+    for (int k = K - 1; k >= 0; --k) {
+        float al[P], ta[P], rh[P], et[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const float* hp = a.hyp + ((size_t)k * a.hyp_rows + (a.hyp_rows == 1 ? 0 : p)) * 4;
+            al[p] = hp[0]; ta[p] = hp[1]; rh[p] = hp[2]; et[p] = hp[3];
+        }
+        float gclip, vclip;
+        if (a.variant == 0) {
+            gclip = fmaxf(1.0f, 30.0f - (float)k);          // unfolded_DLASSO.py:80
+            vclip = fmaxf(10.0f, 200.0f - (float)(k * 3));  // unfolded_DLASSO.py:92
+        } else {
+            gclip = 10.0f;                                   // gnn_dlasso_models_progressive.py:212
+            vclip = 100.0f;                                  // :224, :232
+        }
+        float part[P][4];
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) part[p][c] = 0.0f;
+
+        // ---- elementwise adjoint of iteration k on this lane's rows ---------------------------
+        if (has_tiles) {
+            const rsrc_t ryk = make_rsrc(k > 0 ? a.Y + (size_t)(k - 1) * S : a.y0, state_bytes);
+            const rsrc_t rgr = make_rsrc(a.Grec + (size_t)k * S, state_bytes);
+            const rsrc_t ruk = make_rsrc(a.Urec + (size_t)k * S, state_bytes);
+            const rsrc_t rgy = make_rsrc(a.gY + (size_t)k * S, state_bytes);
+            const rsrc_t rd0 = make_rsrc(a.d0, state_bytes);
+#pragma unroll
+            for (int tt = 0; tt < T2; ++tt) {
+                const int n0 = (w * T2 + tt) * 16 + 4 * h;
+                const bool ok = n0 < n;
+                float yk[P][4], y1t[P][4], d1[P][4], d1b[P][4], c1b[P][4], dk[P][4];
+                bool md1[P][4];
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const uint32_t off = (uint32_t)(((s * P + p) * n + n0) * 4);
+                    f32x4 vy = {0, 0, 0, 0}, vg = {0, 0, 0, 0};
+                    if (ok) {
+                        vy = bload4(ryk, off, 0);
+                        vg = bload4(rgy, off, 0);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        yk[p][r] = vy[r];
+                        y1t[p][r] = y1[p][4 * tt + r];
+                        yb[p][4 * tt + r] = yb[p][4 * tt + r] + vg[r];      // + gY[k]
+                    }
+                }
+                // delta_{k+1} exactly as the forward formed it
+                consensus_any<P, GRAPH>(y1t, d1, msk, ord);
+#pragma unroll
+                for (int p = 0; p < P; ++p)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        md1[p][r] = a.variant == 0 || inside(d1[p][r], -20.0f, 20.0f);
+                        if (a.variant != 0) d1[p][r] = tclamp(d1[p][r], -20.0f, 20.0f);   // :229
+                    }
+                // dual update adjoint (:98-99)
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const uint32_t off = (uint32_t)(((s * P + p) * n + n0) * 4);
+                    f32x4 vu = {0, 0, 0, 0};
+                    if (ok) vu = bload4(ruk, off, 0);
+                    const f32x4 gprev = *(const f32x4*)(Glds + (p * BT + j) * YS + n0);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int e = 4 * tt + r;
+                        const float wv = vu[r] + d1[p][r] * et[p];
+                        const float wb = inside(wv, -vclip, vclip) ? Ub[p][e] : 0.0f;
+                        part[p][3] += wb * d1[p][r];
+                        const float db = gprev[r] * rh_next[p] + wb * et[p];
+                        d1b[p][r] = md1[p][r] ? db : 0.0f;
+                        Ub[p][e] = wb;
+                    }
+                }
+                consensus_any<P, GRAPH>(d1b, c1b, msk, ord);   // 2 L d_bar
+                if (k > 0) {
+                    consensus_any<P, GRAPH>(yk, dk, msk, ord);  // delta_k
+                    if (a.variant != 0) {
+#pragma unroll
+                        for (int p = 0; p < P; ++p)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) dk[p][r] = tclamp(dk[p][r], -20.0f, 20.0f);
+                    }
+                } else {
+#pragma unroll
+                    for (int p = 0; p < P; ++p) {
+                        f32x4 v = {0, 0, 0, 0};
+                        if (ok) v = bload4(rd0, (uint32_t)(((s * P + p) * n + n0) * 4), 0);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) dk[p][r] = v[r];
+                    }
+                }
+                // primal update + gradient clamp adjoint (:73-93)
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const uint32_t off = (uint32_t)(((s * P + p) * n + n0) * 4);
+                    f32x4 vgr = {0, 0, 0, 0};
+                    if (ok) vgr = bload4(rgr, off, 0);
+                    f32x4 gbv;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int e = 4 * tt + r;
+                        const float gr = vgr[r];
+                        const float g = tclamp(gr, -gclip, gclip);
+                        const float z = yk[p][r] - al[p] * g;
+                        const float ybar = yb[p][e] + c1b[p][r];
+                        const float zb = inside(z, -vclip, vclip) ? ybar : 0.0f;
+                        part[p][0] -= zb * g;
+                        const float grb = inside(gr, -gclip, gclip) ? -al[p] * zb : 0.0f;
+                        const float sg = yk[p][r] > 0.0f ? 1.0f : (yk[p][r] < 0.0f ? -1.0f : 0.0f);
+                        part[p][1] += grb * sg;
+                        part[p][2] += grb * dk[p][r];
+                        Ub[p][e] = Ub[p][e] + grb * dg[p];
+                        yb[p][e] = zb;
+                        y1[p][e] = yk[p][r];
+                        gbv[r] = ok ? grb : 0.0f;
+                    }
+                    *(f32x4*)(Glds + (p * BT + j) * YS + n0) = gbv;
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- GEMM1: R_p = A_p gr_bar_p (this wave: m-block mb, agents HALF + AS*i) -----------
+        {
+            f32x4 acc[THA];
+#pragma unroll
+            for (int i = 0; i < TH; ++i) acc[i] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 4
+            for (int t = 0; t < NB; ++t) {
+#pragma unroll
+                for (int i = 0; i < TH; ++i) {
+                    const int p = HALF + AS * i;
+                    const f32x4 av = bload4(rA, voffA + 64 * t, (uint32_t)(p * MP * NP * 4));
+                    const f32x4 bv = *(const f32x4*)(brow + p * BT * YS + 16 * t);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[i] = mfma4(av[r], bv[r], acc[i]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < TH; ++i)
+                *(f32x4*)(Rlds + ((HALF + AS * i) * BT + j) * RS + 16 * mb + 4 * h) = acc[i];
+        }
+        __syncthreads();
+
+        // ---- GEMM2: y_bar_p += A_p^T R_p on this wave's n-tiles ---------------------------------
+        if (has_tiles) {
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                f32x4 rv[MP / 16];
+#pragma unroll
+                for (int t = 0; t < MP / 16; ++t)
+                    rv[t] = *(const f32x4*)(Rlds + (p * BT + j) * RS + 4 * h + 16 * t);
+#pragma unroll
+                for (int tt = 0; tt < T2; ++tt) {
+                    const int nb = w * T2 + tt;
+                    const uint32_t vAt = voffAt + (uint32_t)(16 * nb * MP * 4);
+                    f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                    for (int t = 0; t < MP / 16; ++t) {
+                        const f32x4 av = bload4(rAt, vAt + 64 * t, (uint32_t)(p * NP * MP * 4));
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) gc = mfma4(av[r], rv[t][r], gc);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) yb[p][4 * tt + r] += gc[r];
+                }
+            }
+        }
+
+        // ---- dhyp partial sums of iteration k: lane -> wave -> workgroup --------------------
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float v = part[p][c];
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+                if (lane == 0) red[(w * P + p) * 4 + c] = v;
+            }
+        __syncthreads();
+        if ((int)threadIdx.x < P * 4) {
+            float v = 0.0f;
+#pragma unroll
+            for (int ww = 0; ww < WAVES; ++ww) v += red[ww * P * 4 + threadIdx.x];
+            a.partial[((size_t)blockIdx.x * K + k) * P * 4 + threadIdx.x] = v;
+        }
+#pragma unroll
+        for (int p = 0; p < P; ++p) rh_next[p] = rh[p];
+    }
+}
+
+template <int P, int NT, int GRAPH>
+__global__ __launch_bounds__(WAVES * 64) void backward_kernel(BackwardArgs a) {
+    constexpr int NP = NT * 64;
+    __shared__ __attribute__((aligned(16))) float lds[P * BT * ((NP + 4) + (M_PAD + 4)) + WAVES * P * 4];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (w < 4)
+        body<P, NT, GRAPH, 0>(a, lds, w);
+    else
+        body<P, NT, GRAPH, 1>(a, lds, w);
+}
+
+// dhyp[k][hh][c] = sum over workgroups (and over agents for H = 1) of partial[wg][k][p][c]; one
+// wave per output, lanes stride the workgroups, fixed shuffle tree: deterministic.
+__global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ partial,
+                                                     float* __restrict__ dhyp, int nwg, int K, int P,
+                                                     int H) {
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= K * H * 4) return;
+    const int c = t & 3, hh = (t >> 2) % H, k = t / (4 * H);
+    float v = 0.0f;
+    for (int wg = lane; wg < nwg; wg += 64) {
+        const float* row = partial + ((size_t)wg * K + k) * P * 4;
+        if (H == P) {
+            v += row[hh * 4 + c];
+        } else {
+            for (int p = 0; p < P; ++p) v += row[p * 4 + c];
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) dhyp[t] = v;
+}
+
+template <int P, int NT, int GRAPH>
+hipError_t launch(const BackwardArgs& a, hipStream_t stream) {
+    const int grid = (a.B + BT - 1) / BT;
+    hipLaunchKernelGGL((backward_kernel<P, NT, GRAPH>), dim3(grid), dim3(WAVES * 64), 0, stream, a);
+    return hipGetLastError();
+}
+
+template <int P, int NT>
+backward_fn_ptr pick_graph(int graph) {
+    switch (graph) {
+        case GRAPH_SHARED: return &launch<P, NT, GRAPH_SHARED>;
+        case GRAPH_LANE: return &launch<P, NT, GRAPH_LANE>;
+        case GRAPH_ORDERED: return &launch<P, NT, GRAPH_ORDERED>;
+        default: return nullptr;
+    }
+}
+
+template <int P>
+backward_fn_ptr pick_nt(int nt, int graph) {
+    if (nt == 1) return pick_graph<P, 1>(graph);
+    if (nt == 2) return pick_graph<P, 2>(graph);
+    if constexpr (P <= 5) {
+        if (nt == 4) return pick_graph<P, 4>(graph);
+    }
+    return nullptr;
+}
+
+}  // namespace bwd
+
+backward_fn_ptr find_backward(int P, int nt, int graph) {
+    switch (P) {
+        case 1: return bwd::pick_nt<1>(nt, graph);
+        case 2: return bwd::pick_nt<2>(nt, graph);
+        case 3: return bwd::pick_nt<3>(nt, graph);
+        case 4: return bwd::pick_nt<4>(nt, graph);
+        case 5: return bwd::pick_nt<5>(nt, graph);
+        case 6: return bwd::pick_nt<6>(nt, graph);
+        default: return nullptr;
+    }
+}
+
+hipError_t launch_backward_reduce(const float* partial, float* dhyp, int nwg, int K, int P, int H,
+                                  hipStream_t stream) {
+    const int outs = K * H * 4;
+    hipLaunchKernelGGL(bwd::reduce_kernel, dim3((outs + 3) / 4), dim3(256), 0, stream, partial, dhyp,
+                       nwg, K, P, H);
+    return hipGetLastError();
+}
+
+}  // namespace dadmm

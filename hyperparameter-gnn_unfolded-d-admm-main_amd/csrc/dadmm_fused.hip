@@ -31,6 +31,11 @@
 #include <stdint.h>
 
 #include "dadmm_internal.h"
+#include "dadmm_consensus.h"
+
+#ifndef DADMM_FUSED_REC
+#define DADMM_FUSED_REC 0
+#endif
 
 namespace dadmm {
 
@@ -118,165 +123,6 @@ __device__ __forceinline__ unsigned long long stamp() {
 // Compiler-only memory barrier: bounds how far the scheduler hoists operand loads.
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
 
-// delta_p = 2 (L y)_p accumulated exactly as compute_delta (unfolded_DLASSO.py:127-140) does for
-// one sample: the agents' loops run p' = 0..P-1 over graph.neighbors(p') in ascending order,
-// each visit (p', q) doing delta[p'] += (y_p' - y_q); delta[q] -= (y_p' - y_q). Restricted to the
-// updates of delta[p], in order: every q < p with p in N(q) (-=), then p's own neighbours
-// (+=, a self-loop also takes its -= there), then every q > p with p in N(q) (-=).
-// Every such update of delta[p] adds +-fl(y_a - y_b) for the pair's ordered difference
-// d(a, b) = fl(y_a - y_b), a < b, and fl(y_b - y_a) == -d(a, b) exactly (round-to-nearest is
-// symmetric), so acc - fl(y_q - y_p) == acc + fl(y_p - y_q): one subtraction per pair serves all
-// four updates an undirected edge makes, bit-for-bit.
-// `bit(q, p)` = p in N(q); E positions (rows) at a time.
-template <int P, int E, typename BitFn>
-__device__ __forceinline__ void consensus(const float (&yy)[P][E], float (&dl)[P][E], BitFn bit) {
-    float acc[P][E];
-#pragma unroll
-    for (int p = 0; p < P; ++p)
-#pragma unroll
-        for (int e = 0; e < E; ++e) acc[p][e] = 0.0f;
-    // contribution of pair (a, b) to agent p, as the reference's sequence for p orders it:
-    //   q < p  (other's loop):  acc -= (y_q - y_p)  ==  acc - d(q, p)
-    //   own loop, q < p:        acc += (y_p - y_q)  ==  acc - d(q, p)
-    //   own loop, q > p:        acc += (y_p - y_q)  ==  acc + d(p, q)
-    //   q > p  (other's loop):  acc -= (y_q - y_p)  ==  acc + d(p, q)
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-#pragma unroll
-        for (int q = 0; q < p; ++q)
-            if (bit(q, p)) {
-#pragma unroll
-                for (int e = 0; e < E; ++e) acc[p][e] = acc[p][e] - (yy[q][e] - yy[p][e]);
-            }
-#pragma unroll
-        for (int q = 0; q < P; ++q)
-            if (bit(p, q)) {
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    if (q < p) acc[p][e] = acc[p][e] - (yy[q][e] - yy[p][e]);
-                    else if (q > p) acc[p][e] = acc[p][e] + (yy[p][e] - yy[q][e]);
-                    else acc[p][e] = (acc[p][e] + (yy[p][e] - yy[p][e])) - (yy[p][e] - yy[p][e]);
-                }
-            }
-#pragma unroll
-        for (int q = p + 1; q < P; ++q)
-            if (bit(q, p)) {
-#pragma unroll
-                for (int e = 0; e < E; ++e) acc[p][e] = acc[p][e] + (yy[p][e] - yy[q][e]);
-            }
-    }
-#pragma unroll
-    for (int p = 0; p < P; ++p)
-#pragma unroll
-        for (int e = 0; e < E; ++e) dl[p][e] = acc[p][e];
-}
-
-// Per-lane (per-sample graph) form: the conditional adds become selects; pair differences are
-// shared as above (the compiler CSEs yy[a] - yy[b] across the four uses).
-template <int P, int E>
-__device__ __forceinline__ void consensus_lane(const float (&yy)[P][E], float (&dl)[P][E],
-                                               const uint32_t (&msk)[P]) {
-    float d[P][P][E];   // d[a][b] = y_a - y_b for a < b
-#pragma unroll
-    for (int a = 0; a < P; ++a)
-#pragma unroll
-        for (int b2 = a + 1; b2 < P; ++b2)
-#pragma unroll
-            for (int e = 0; e < E; ++e) d[a][b2][e] = yy[a][e] - yy[b2][e];
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-        float acc[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) acc[e] = 0.0f;
-#pragma unroll
-        for (int q = 0; q < p; ++q) {
-            const bool on = (msk[q] >> p) & 1u;
-#pragma unroll
-            for (int e = 0; e < E; ++e) acc[e] = on ? acc[e] - d[q][p][e] : acc[e];
-        }
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const bool on = (msk[p] >> q) & 1u;
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                float t;
-                if (q < p) t = acc[e] - d[q][p][e];
-                else if (q > p) t = acc[e] + d[p][q][e];
-                else t = (acc[e] + (yy[p][e] - yy[p][e])) - (yy[p][e] - yy[p][e]);
-                acc[e] = on ? t : acc[e];
-            }
-        }
-#pragma unroll
-        for (int q = p + 1; q < P; ++q) {
-            const bool on = (msk[q] >> p) & 1u;
-#pragma unroll
-            for (int e = 0; e < E; ++e) acc[e] = on ? acc[e] + d[p][q][e] : acc[e];
-        }
-#pragma unroll
-        for (int e = 0; e < E; ++e) dl[p][e] = acc[e];
-    }
-}
-
-// Per-lane graphs whose adjacency lists are not ascending: p's own loop follows the packed
-// adjacency order ord[p] (4 bits per neighbour, cnt[p] entries) exactly as graph.neighbors(p).
-template <int P, int E>
-__device__ __forceinline__ void consensus_ordered(const float (&yy)[P][E], float (&dl)[P][E],
-                                                  const uint32_t (&msk)[P],
-                                                  const uint32_t (&ord)[P]) {
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-        float acc[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) acc[e] = 0.0f;
-#pragma unroll
-        for (int q = 0; q < p; ++q) {
-            const bool on = (msk[q] >> p) & 1u;
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const float t = acc[e] - (yy[q][e] - yy[p][e]);
-                acc[e] = on ? t : acc[e];
-            }
-        }
-        const int cnt = __builtin_popcount(msk[p]);
-#pragma unroll
-        for (int t = 0; t < P; ++t) {
-            const bool on = t < cnt;
-            const int q = (ord[p] >> (4 * t)) & 15;
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                float yq = yy[0][e];
-#pragma unroll
-                for (int qq = 1; qq < P; ++qq) yq = (q == qq) ? yy[qq][e] : yq;
-                float v = acc[e] + (yy[p][e] - yq);
-                if (q == p) v = v - (yy[p][e] - yy[p][e]);
-                acc[e] = on ? v : acc[e];
-            }
-        }
-#pragma unroll
-        for (int q = p + 1; q < P; ++q) {
-            const bool on = (msk[q] >> p) & 1u;
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const float t = acc[e] - (yy[q][e] - yy[p][e]);
-                acc[e] = on ? t : acc[e];
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < E; ++e) dl[p][e] = acc[e];
-    }
-}
-
-template <int P, int GRAPH>
-__device__ __forceinline__ void consensus_any(const float (&yy)[P][4], float (&dl)[P][4],
-                                              const uint32_t (&msk)[P], const uint32_t (&ord)[P]) {
-    if constexpr (GRAPH == GRAPH_SHARED)
-        consensus<P, 4>(yy, dl, [&](int q, int p) { return ((msk[q] >> p) & 1u) != 0; });
-    else if constexpr (GRAPH == GRAPH_LANE)
-        consensus_lane<P, 4>(yy, dl, msk);
-    else
-        consensus_ordered<P, 4>(yy, dl, msk, ord);
-}
-
 // GRAPH: GRAPH_SHARED (one graph, ascending adjacency), GRAPH_LANE (per-sample, ascending),
 //        GRAPH_ORDERED (per-sample, explicit adjacency order).
 //
@@ -285,7 +131,7 @@ __device__ __forceinline__ void consensus_any(const float (&yy)[P][4], float (&d
 // m-block w % 4 (waves w and w + 4 share a SIMD under the observed dispatch order, so each SIMD
 // carries P GEMM1 tiles). All operand rings are indexed at compile time (full unroll), so the
 // compiler never copies registers between pipeline stages and its vmcnt/lgkmcnt waits are counted.
-template <int P, int NT, int GRAPH, int WV, int HALF>
+template <int P, int NT, int GRAPH, int WV, int HALF, bool REC>
 __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict__ lds, const int w) {
     constexpr bool SHARED_GRAPH = GRAPH == GRAPH_SHARED;
     constexpr int WAVES = WV;                        // waves per workgroup (4 or 8)
@@ -532,6 +378,9 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
         //      assembly + primal update runs under the next chain's MFMAs -------------------------
         if (has_tiles) {
             const rsrc_t rY = make_rsrc(a.Y + (size_t)k * B * P * n, state_bytes);
+            // REC (training): the adjoint's trajectory, Grec[k] = pre-clamp gradient, Urec[k] = U_k
+            const rsrc_t rG = make_rsrc(REC ? a.Grec + (size_t)k * B * P * n : a.Y, REC ? state_bytes : 0u);
+            const rsrc_t rUr = make_rsrc(REC ? a.Urec + (size_t)k * B * P * n : a.Y, REC ? state_bytes : 0u);
             constexpr int NS = P * T2;                       // chains: s = p*T2 + tt
             f32x4 tring[2][MP / 16];
             f32x4 g[2];
@@ -548,7 +397,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 const int p = s2 / T2, tt = s2 % T2;
                 const int nb = w * T2 + tt;
                 const int n0 = nb * 16 + 4 * h;
-                f32x4 yn;
+                f32x4 yn, grv, urv;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int e = 4 * tt + r;
@@ -560,6 +409,8 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                     gr = gr + st;
                     gr = gr + U[p][e] * dg[p];
                     gr = gr + D[p][e] * rh[p];
+                    grv[r] = gr;
+                    urv[r] = U[p][e];
                     bad_g |= (gr != gr);                            // :84 guard (flag only)
                     gr = tclamp(gr, -gclip, gclip);                 // :80-81
                     float v = yv - al[p] * gr;                      // :89
@@ -572,6 +423,11 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 // Y[k][s][p][n0..n0+3]; rows past n go to an offset the range check drops
                 bstore4_stream(yn, rY, n0 < n ? voffY + (uint32_t)((p * n + nb * 16) * 4) : 0x80000000u);
 #endif
+                if constexpr (REC) {
+                    const uint32_t o = n0 < n ? voffY + (uint32_t)((p * n + nb * 16) * 4) : 0x80000000u;
+                    bstore4_stream(grv, rG, o);
+                    bstore4_stream(urv, rUr, o);
+                }
             };
             load_at(tring[0], 0);
 #pragma unroll
@@ -643,18 +499,18 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     }
 }
 
-template <int P, int NT, int GRAPH, int WV>
+template <int P, int NT, int GRAPH, int WV, bool REC>
 __global__ __launch_bounds__(WV * 64) void fused_forward_kernel(FusedArgs a) {
     constexpr int NP = NT * 64;
     __shared__ __attribute__((aligned(16))) float lds[P * BT * ((NP + 4) + 2 * (M_PAD + 4))];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave id, in an SGPR
     if constexpr (WV == 4) {
-        fused_body<P, NT, GRAPH, 4, 0>(a, lds, w);
+        fused_body<P, NT, GRAPH, 4, 0, REC>(a, lds, w);
     } else {
         if (w < 4)
-            fused_body<P, NT, GRAPH, 8, 0>(a, lds, w);
+            fused_body<P, NT, GRAPH, 8, 0, REC>(a, lds, w);
         else
-            fused_body<P, NT, GRAPH, 8, 1>(a, lds, w);
+            fused_body<P, NT, GRAPH, 8, 1, REC>(a, lds, w);
     }
 }
 
@@ -662,7 +518,7 @@ __global__ __launch_bounds__(WV * 64) void fused_forward_kernel(FusedArgs a) {
 template <int P, int NT, int GRAPH>
 static hipError_t launch_fused(const FusedArgs& a, hipStream_t stream) {
     const int grid = (a.B + BT - 1) / BT;
-    hipLaunchKernelGGL((fused_forward_kernel<P, NT, GRAPH, FUSED_WAVES>), dim3(grid),
+    hipLaunchKernelGGL((fused_forward_kernel<P, NT, GRAPH, FUSED_WAVES, DADMM_FUSED_REC != 0>), dim3(grid),
                        dim3(FUSED_WAVES * 64), 0, stream, a);
     return hipGetLastError();
 }
@@ -689,13 +545,19 @@ static fused_fn_ptr pick_nt(int nt, int graph) {
     return nullptr;
 }
 
-#ifdef DADMM_STAMPS
+#if defined(DADMM_STAMPS) && !DADMM_FUSED_REC
 extern "C" int dadmm_debug_set_stamps(void* buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -3;
 }
 #endif
 
+// This file is compiled twice (csrc/Makefile): DADMM_FUSED_REC = 0 defines find_fused (inference),
+// DADMM_FUSED_REC = 1 defines find_fused_rec (training: also records Grec / Urec).
+#if DADMM_FUSED_REC
+fused_fn_ptr find_fused_rec(int P, int nt, int graph) {
+#else
 fused_fn_ptr find_fused(int P, int nt, int graph) {
+#endif
 #ifdef DADMM_ONLY_H   // compile-time experiments: instantiate the headline shape only
     return (P == 5 && nt == 4 && graph == GRAPH_SHARED) ? &launch_fused<5, 4, GRAPH_SHARED> : nullptr;
 #else

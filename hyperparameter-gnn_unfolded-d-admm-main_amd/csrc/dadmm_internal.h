@@ -28,6 +28,8 @@ struct FusedArgs {
     float* Y;            // [K][B][P][n]
     float* U_out;        // [B][P][n] or nullptr
     int32_t* status;     // or nullptr
+    float* Grec;         // [K][B][P][n] pre-clamp gradients (recording launchers only)
+    float* Urec;         // [K][B][P][n] U_k entering iteration k (recording launchers only)
     int B, m, n, K, hyp_rows, variant;
 };
 
@@ -36,6 +38,30 @@ typedef hipError_t (*fused_fn_ptr)(const FusedArgs&, hipStream_t);
 // Returns the launcher for (P, n_pad = 64*nt) or nullptr when that shape is not instantiated.
 enum { GRAPH_SHARED = 0, GRAPH_LANE = 1, GRAPH_ORDERED = 2 };
 fused_fn_ptr find_fused(int P, int nt, int graph);
+// Same shapes, recording the adjoint's trajectory (a.Grec / a.Urec must be set).
+fused_fn_ptr find_fused_rec(int P, int nt, int graph);
+
+// ---- adjoint (dadmm_backward.hip) ---------------------------------------------------------------
+struct BackwardArgs {
+    const float* A;      // prepared operator [P][M_PAD][n_pad]
+    const float* At;     // [P][n_pad][M_PAD]
+    const uint64_t* nbr; // as FusedArgs
+    const uint32_t* nbr_order;
+    const float* deg;
+    const float* hyp;    // [K][hyp_rows][4]
+    const float* y0;     // [B][P][n]
+    const float* d0;     // [B][P][n]
+    const float* Y;      // [K][B][P][n] recorded trajectory
+    const float* Grec;   // [K][B][P][n]
+    const float* Urec;   // [K][B][P][n]
+    const float* gY;     // [K][B][P][n] dL/dY
+    float* partial;      // [ceil(B/BT)][K][P][4] per-workgroup sums
+    int B, m, n, K, hyp_rows, variant;
+};
+typedef hipError_t (*backward_fn_ptr)(const BackwardArgs&, hipStream_t);
+backward_fn_ptr find_backward(int P, int nt, int graph);
+hipError_t launch_backward_reduce(const float* partial, float* dhyp, int nwg, int K, int P, int H,
+                                  hipStream_t stream);
 
 // Operator preparation kernel launcher (dadmm_prepare.hip).
 hipError_t launch_prepare(const float* A, float* Apad, float* Atpad, int P, int m, int n,
@@ -69,6 +95,8 @@ struct StepArgs {
     float* G;               // [B][P][n]: gradient of the current iteration (scratch)
     int32_t* flags;         // [SW_FLAG_WORDS(K)] (scratch)
     int32_t* status;        // [1]
+    float* Grec;            // nullable [K][B][P][n]: pre-clamp gradient of iteration k
+    float* Urec;            // nullable [K][B][P][n]: U_k entering iteration k
     int B, P, m, n, n_pad, K, hyp_rows, variant, graph_shared;
 };
 

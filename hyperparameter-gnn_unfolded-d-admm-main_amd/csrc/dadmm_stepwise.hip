@@ -182,7 +182,7 @@ __device__ void phase_grad(const StepArgs& a, int k, int item, float* lds) {
             f32x4 uv = {0.0f, 0.0f, 0.0f, 0.0f};
             if (!uzero) uv = *(const f32x4*)(usrc + off);
             const f32x4 dv = *(const f32x4*)(dsrc + off);
-            f32x4 gv;
+            f32x4 gv, gpre;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float y = yv[r];
@@ -190,11 +190,16 @@ __device__ void phase_grad(const StepArgs& a, int k, int item, float* lds) {
                 float g = gc[r] + st;
                 g = g + uv[r] * dg;
                 g = g + dv[r] * rh;
+                gpre[r] = g;
                 g = clamp_t(g, -gclip, gclip);
                 bad |= g != g;                     // after the clamp only NaN remains (:84)
                 gv[r] = g;
             }
             *(f32x4*)(a.G + off) = gv;
+            if (a.Grec != nullptr) {   // the adjoint's trajectory (training)
+                *(f32x4*)(a.Grec + (size_t)k * S + off) = gpre;
+                *(f32x4*)(a.Urec + (size_t)k * S + off) = uv;
+            }
         }
     }
     flag_or(a.flags + SW_F_GBAD(k), bad);

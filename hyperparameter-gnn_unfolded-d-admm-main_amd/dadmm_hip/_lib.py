@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -24,8 +24,11 @@ EXPORTED_SYMBOLS = (
     "dadmm_operator_bytes",
     "dadmm_prepare_operator",
     "dadmm_forward",
+    "dadmm_forward_record",
     "dadmm_stepwise_scratch_bytes",
     "dadmm_forward_stepwise",
+    "dadmm_backward_scratch_bytes",
+    "dadmm_backward",
 )
 
 
@@ -74,7 +77,13 @@ def load() -> ctypes.CDLL:
     L.dadmm_stepwise_scratch_bytes.restype = ctypes.c_size_t
     L.dadmm_stepwise_scratch_bytes.argtypes = [ctypes.POINTER(Dims)]
     L.dadmm_forward_stepwise.restype = ctypes.c_int
-    L.dadmm_forward_stepwise.argtypes = [ctypes.POINTER(Dims)] + [vp] * 12 + [i32, vp, vp]
+    L.dadmm_forward_record.restype = ctypes.c_int
+    L.dadmm_forward_record.argtypes = [ctypes.POINTER(Dims)] + [vp] * 15
+    L.dadmm_forward_stepwise.argtypes = [ctypes.POINTER(Dims)] + [vp] * 14 + [i32, vp, vp]
+    L.dadmm_backward_scratch_bytes.restype = ctypes.c_size_t
+    L.dadmm_backward_scratch_bytes.argtypes = [ctypes.POINTER(Dims)]
+    L.dadmm_backward.restype = ctypes.c_int
+    L.dadmm_backward.argtypes = [ctypes.POINTER(Dims)] + [vp] * 14
     v = L.dadmm_abi_version()
     if v != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {v}, expected {ABI_VERSION}")

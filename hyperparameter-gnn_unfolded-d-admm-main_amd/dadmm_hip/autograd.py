@@ -1,4 +1,10 @@
-"""autograd plumbing for the fused forward (the drivers call ``loss.backward()`` through it)."""
+"""autograd plumbing for the HIP forward (the drivers call ``loss.backward()`` through it).
+
+Training-mode forwards (the hyper-parameter table requires grad) run the recording forward
+(``dadmm_forward_record``) and keep the trajectory; ``backward`` runs the adjoint kernel
+(``dadmm_backward``) and returns d loss / d table, from which torch autograd continues into
+``seq_hyp.param`` (cumsum / sigmoid / penalty / clamp of ``seq_hyperparam.table``).
+"""
 from __future__ import annotations
 
 import os
@@ -6,7 +12,7 @@ import os
 import torch
 
 from . import _lib
-from .ops import describe_status, forward_raw
+from .ops import backward_raw, describe_status, forward_raw
 
 # DADMM_GUARD_WARNINGS=1: synchronise after every forward and print the reference's guard
 # warnings (unfolded_DLASSO.py:56-104). Off by default: the guards themselves are applied on the
@@ -16,6 +22,10 @@ _WARN = os.environ.get("DADMM_GUARD_WARNINGS", "0") not in ("", "0")
 
 class GuardTimeoutError(RuntimeError):
     """The gated stepwise recomputation could not synchronise its grid (Y is invalid)."""
+
+
+class GuardAdjointError(NotImplementedError):
+    """backward through a forward in which one of the reference's NaN/Inf guards fired."""
 
 
 def check_status(status: torch.Tensor) -> int:
@@ -29,20 +39,31 @@ def check_status(status: torch.Tensor) -> int:
 class _UnfoldedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, table, op, b, graphs, y0, U0, d0, variant):
-        Y, _, status = forward_raw(op, b, graphs, table.detach(), y0, U0, d0, variant=variant)
+        record = ctx.needs_input_grad[0]
+        out = forward_raw(op, b, graphs, table.detach(), y0, U0, d0, variant=variant,
+                          record=record)
+        Y, _, status = out[:3]
         if _WARN:
             for msg in describe_status(check_status(status)):
                 print(f"Warning: {msg}")
         ctx.mark_non_differentiable(status)
+        if record:
+            ctx.op, ctx.graphs, ctx.traj, ctx.status = op, graphs, out[3], status
         return Y, status
 
     @staticmethod
     def backward(ctx, gY, gstatus):
-        raise NotImplementedError(
-            "the adjoint (backward) kernel of the fused D-ADMM forward is not built yet")
+        st = check_status(ctx.status)   # one host sync per backward
+        if st:
+            raise GuardAdjointError(
+                "backward through a forward in which the reference's NaN/Inf guards fired ("
+                + "; ".join(describe_status(st)) + ") is not supported by the adjoint kernel")
+        dtable = backward_raw(ctx.op, ctx.graphs, ctx.traj, gY)
+        ctx.traj = None
+        return dtable, None, None, None, None, None, None, None
 
 
 def dadmm_unfolded_apply(op, b, graphs, table, y0, U0, d0, variant=_lib.VARIANT_UNFOLDED):
     """(Y [K,B,P,n], status [1] int32 device tensor) = the K-step recurrence with the reference's
-    guards; Y is differentiable w.r.t. ``table`` once the adjoint kernel exists."""
+    guards; Y is differentiable w.r.t. ``table`` (adjoint kernel)."""
     return _UnfoldedFn.apply(table, op, b, graphs, y0, U0, d0, variant)

@@ -75,7 +75,8 @@ def _pad_n(t, n_store):
 
 def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: torch.Tensor,
                 y0: torch.Tensor, U0: torch.Tensor, d0: torch.Tensor, *,
-                variant: int = _lib.VARIANT_UNFOLDED, want_U: bool = False, path: str = "auto"):
+                variant: int = _lib.VARIANT_UNFOLDED, want_U: bool = False, path: str = "auto",
+                record: bool = False):
     """The K-step forward with the reference's NaN/Inf guards, enqueued on the current stream
     (no host synchronisation). Shapes: b [B,P,m], hyp [K,H,4], y0/U0/d0 [B,P,n].
 
@@ -84,7 +85,10 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     stepwise kernels. "fused" / "stepwise" force one path ("fused" alone does NOT apply the
     guards: its status only flags them).
 
-    Returns (Y [K,B,P,n], U_K [B,P,n] or None, status int32 device tensor [1])."""
+    record: also store the trajectory the adjoint consumes (training; dadmm_forward_record).
+
+    Returns (Y [K,B,P,n], U_K [B,P,n] or None, status int32 device tensor [1]), plus, with
+    ``record``, a ``Trajectory`` as a fourth element."""
     _dev_check(b, hyp, y0, U0, d0, graphs.nbr, graphs.deg)
     if path not in ("auto", "fused", "stepwise"):
         raise ValueError(f"unknown path {path!r}")
@@ -98,6 +102,10 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     y0, U0, d0 = (_pad_n(x, ns).contiguous().float() for x in (y0, U0, d0))
     Y = torch.empty((K, B, P, ns), dtype=torch.float32, device=b.device)
     U = torch.empty((B, P, ns), dtype=torch.float32, device=b.device) if want_U else None
+    Grec = Urec = None
+    if record:
+        Grec = torch.empty((K, B, P, ns), dtype=torch.float32, device=b.device)
+        Urec = torch.empty((K, B, P, ns), dtype=torch.float32, device=b.device)
     status = torch.zeros(1, dtype=torch.int32, device=b.device)
     d = op.dims(B=B, K=K, variant=variant, hyp_rows=H, graph_shared=graphs.shared)
     L = _lib.load()
@@ -108,24 +116,77 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
                              "P <= 8; use path='auto' or 'stepwise'")
         fused = path != "stepwise" and graphs.fused_ok
         if fused:
-            rc = L.dadmm_forward(ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.nbr),
-                                 _ptr(graphs.order), _ptr(graphs.deg), _ptr(hyp), _ptr(y0),
-                                 _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U), _ptr(status), stream)
+            if record:
+                rc = L.dadmm_forward_record(
+                    ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.nbr),
+                    _ptr(graphs.order), _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0),
+                    _ptr(Y), _ptr(Grec), _ptr(Urec), _ptr(U), _ptr(status), stream)
+            else:
+                rc = L.dadmm_forward(ctypes.byref(d), _ptr(op.workspace), _ptr(b),
+                                     _ptr(graphs.nbr), _ptr(graphs.order), _ptr(graphs.deg),
+                                     _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U),
+                                     _ptr(status), stream)
             if rc == _lib.DADMM_EUNSUPPORTED and path == "auto":
                 fused = False
             else:
-                _lib.check("dadmm_forward", rc)
+                _lib.check("dadmm_forward_record" if record else "dadmm_forward", rc)
         if path != "fused":
             nbytes = L.dadmm_stepwise_scratch_bytes(ctypes.byref(d))
             scratch = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=b.device)
             _lib.check("dadmm_forward_stepwise", L.dadmm_forward_stepwise(
                 ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.vptr), _ptr(graphs.vq),
                 _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U),
-                _ptr(status), 1 if fused else 0, _ptr(scratch), stream))
+                _ptr(Grec), _ptr(Urec), _ptr(status), 1 if fused else 0, _ptr(scratch), stream))
+    traj = Trajectory(Y, Grec, Urec, y0, d0, hyp, variant) if record else None
     if ns != op.n:
         Y = Y[..., : op.n]
         U = U[..., : op.n] if U is not None else None
+    if record:
+        return Y, U, status, traj
     return Y, U, status
+
+
+class Trajectory:
+    """What the adjoint consumes: the n-padded iterates Y, pre-clamp gradients Grec and dual
+    states Urec ([K,B,P,n_store] each), the inits y0 / d0 and the hyper-parameter table."""
+
+    __slots__ = ("Y", "Grec", "Urec", "y0", "d0", "hyp", "variant")
+
+    def __init__(self, Y, Grec, Urec, y0, d0, hyp, variant):
+        self.Y, self.Grec, self.Urec = Y, Grec, Urec
+        self.y0, self.d0, self.hyp, self.variant = y0, d0, hyp, variant
+
+
+def backward_raw(op: PreparedOperator, graphs: GraphBatch, traj: Trajectory,
+                 gY: torch.Tensor) -> torch.Tensor:
+    """dL/dhyp [K,H,4] for L = sum_k <gY[k], Y[k]> along ``traj`` (dadmm_backward), enqueued on
+    the current stream. gY: [K,B,P,n] (n or n_store columns)."""
+    _dev_check(gY)
+    K, B, P, ns = traj.Y.shape
+    H = int(traj.hyp.shape[1])
+    gY = _pad_n(gY.float(), ns).contiguous()
+    if tuple(gY.shape) != (K, B, P, ns):
+        raise ValueError(f"gY must be [{K},{B},{P},{op.n}], got {tuple(gY.shape)}")
+    d = op.dims(B=B, K=K, variant=traj.variant, hyp_rows=H, graph_shared=graphs.shared)
+    L = _lib.load()
+    dhyp = torch.empty((K, H, 4), dtype=torch.float32, device=gY.device)
+    nbytes = L.dadmm_backward_scratch_bytes(ctypes.byref(d))
+    scratch = torch.empty(max(nbytes, 16) // 4 + 4, dtype=torch.float32, device=gY.device)
+    order = graphs.order
+    if not graphs.fused_ok:
+        raise NotImplementedError(
+            "the adjoint kernel follows non-ascending adjacency orders only for P <= 8")
+    with torch.cuda.device(gY.device):
+        rc = L.dadmm_backward(ctypes.byref(d), _ptr(op.workspace), _ptr(graphs.nbr), _ptr(order),
+                              _ptr(graphs.deg), _ptr(traj.hyp), _ptr(traj.y0), _ptr(traj.d0),
+                              _ptr(traj.Y), _ptr(traj.Grec), _ptr(traj.Urec), _ptr(gY),
+                              _ptr(dhyp), _ptr(scratch), _stream(gY.device))
+        if rc == _lib.DADMM_EUNSUPPORTED:
+            raise NotImplementedError(
+                "the adjoint kernel covers the fused kernel's shapes (P <= 6, n <= 256, m <= 64); "
+                + _lib.load().dadmm_last_error().decode(errors="replace"))
+        _lib.check("dadmm_backward", rc)
+    return dhyp
 
 
 def describe_status(st: int) -> list:

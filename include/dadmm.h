@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 2
+#define DADMM_ABI_VERSION 3
 
 enum {
     DADMM_OK = 0,
@@ -123,6 +123,16 @@ int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uin
                   const float* U0, const float* d0, float* Y, float* U_out, int32_t* status,
                   void* stream);
 
+/* dadmm_forward that also records the trajectory the adjoint (dadmm_backward) consumes — the
+ * training-mode forward (the drivers call loss.backward() through it: unfolded_train_new.py:74-80).
+ *   Grec [K][B][P][n]: the gradient of iteration k BEFORE its clamp (unfolded_DLASSO.py:73-77)
+ *   Urec [K][B][P][n]: U_k entering iteration k
+ * Y is bit-identical to dadmm_forward's. Same shapes as dadmm_forward. */
+int dadmm_forward_record(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
+                         const uint32_t* nbr_order, const float* deg, const float* hyp,
+                         const float* y0, const float* U0, const float* d0, float* Y, float* Grec,
+                         float* Urec, float* U_out, int32_t* status, void* stream);
+
 /* Bytes of device scratch dadmm_forward_stepwise needs for `d` (256-byte aligned pointer). */
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d);
 
@@ -137,12 +147,29 @@ size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d);
  *           on the same stream. One workgroup per CU synchronised by an in-launch grid barrier;
  *           the device must not be shared with other work (DADMM_STATUS_BARRIER_TIMEOUT).
  * `status` (required for gate = 1) is overwritten with the DADMM_STATUS_* bits of the guards that
- * fired. `scratch`: dadmm_stepwise_scratch_bytes(d) bytes. */
+ * fired. `scratch`: dadmm_stepwise_scratch_bytes(d) bytes. Grec / Urec (nullable, both or neither):
+ * the trajectory recording of dadmm_forward_record. */
 int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
                            const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
                            const float* hyp, const float* y0, const float* U0, const float* d0,
-                           float* Y, float* U_out, int32_t* status, int32_t gate, void* scratch,
-                           void* stream);
+                           float* Y, float* U_out, float* Grec, float* Urec, int32_t* status,
+                           int32_t gate, void* scratch, void* stream);
+
+/* Bytes of device scratch dadmm_backward needs for `d` (16-byte aligned pointer). */
+size_t dadmm_backward_scratch_bytes(const dadmm_dims* d);
+
+/* The adjoint of the K-step forward w.r.t. the hyper-parameter table: dhyp [K][H][4] (overwritten)
+ * = d(sum_k <gY[k], Y[k]>)/d hyp along the trajectory (Y, Grec, Urec) that dadmm_forward_record
+ * (or dadmm_forward_stepwise with recording) produced from the same operands; the derivative torch
+ * autograd takes through the reference's forward (unfolded_DLASSO.py:53-107 with clamp / sign /
+ * compute_delta backward rules), i.e. what loss.backward() delivers to the seq_hyp rows
+ * (unfolded_train_new.py:78). Valid only when that forward's status was 0 (no guard fired).
+ * Replaces: the autograd backward of the reference's eager forward graph.
+ * Same shapes and graph operands as dadmm_forward; deterministic (fixed reduction order). */
+int dadmm_backward(const dadmm_dims* d, const void* op, const uint64_t* nbr,
+                   const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
+                   const float* d0, const float* Y, const float* Grec, const float* Urec,
+                   const float* gY, float* dhyp, void* scratch, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Per-instantiation register report of the fused kernel (VGPRs, VGPR/SGPR spills).
 
-    python scripts/spills.py [extra hipcc flags...]
+    python scripts/spills.py [--src FILE] [extra hipcc flags...]
 
-Compiles csrc/dadmm_fused.hip with the Makefile's flags and -Rpass-analysis=kernel-resource-usage
+Compiles csrc/dadmm_fused.hip (or csrc/FILE, e.g. --src dadmm_backward.hip; -DDADMM_FUSED_REC=1
+for the recording forward) with the Makefile's flags and -Rpass-analysis=kernel-resource-usage
 and prints one line per fused_forward_kernel<P, NT, GRAPH, WAVES> instantiation."""
 import os
 import re
@@ -18,7 +19,10 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=o
 
 
 def main():
-    r = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *sys.argv[1:], SRC],
+    args, src = sys.argv[1:], SRC
+    if args[:1] == ["--src"]:
+        src, args = os.path.join(os.path.dirname(SRC), args[1]), args[2:]
+    r = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *args, src],
                        capture_output=True, text=True)
     if r.returncode:
         sys.stderr.write(r.stderr)
@@ -27,8 +31,8 @@ def main():
     for line in r.stderr.splitlines():
         m = re.search(r"Function Name: (\S+)", line)
         if m:
-            k = re.search(r"kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", m.group(1))
-            cur = "P=%s NT=%s graph=%s waves=%s" % k.groups() if k else m.group(1)
+            k = re.search(r"kernelILi(\d+)ELi(\d+)ELi(\d+)E", m.group(1))
+            cur = "P=%s NT=%s graph=%s" % k.groups() if k else m.group(1)
             rows[cur] = {}
             continue
         m = re.search(r"remark:\s+(VGPRs|VGPRs Spill|SGPRs Spill|LDS Size \[bytes/block\]): (\d+)",

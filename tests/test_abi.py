@@ -104,3 +104,62 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(ImportError):
         _lib.load()
+
+
+# ---- training path: recording forward and the adjoint (argument validation only) -----------------
+REC = FAKE[:10] + [ctypes.c_void_p(0xA0000), ctypes.c_void_p(0xB0000)] + FAKE[10:]  # Y, Grec, Urec
+
+
+def test_forward_record_rejects_before_launch(L):
+    d = _dims()
+    args = list(REC)
+    args[11] = None        # Grec
+    assert L.dadmm_forward_record(ctypes.byref(d), *args, None) == -1
+    assert "Grec" in L.dadmm_last_error().decode()
+    args = list(REC)
+    args[12] = ctypes.c_void_p(0xB0008)   # Urec misaligned
+    assert L.dadmm_forward_record(ctypes.byref(d), *args, None) == -1
+    assert L.dadmm_forward_record(ctypes.byref(_dims(P=7, n=64, hyp_rows=1)), *REC, None) == -2
+    assert L.dadmm_forward_record(ctypes.byref(_dims(B=0)), *REC, None) == 0
+
+
+BWD = [ctypes.c_void_p(0x10000 * (i + 1)) for i in range(14)]
+BWD[2] = None   # nbr_order: ascending
+
+
+def test_backward_scratch_bytes(L):
+    d = _dims(B=40)
+    assert L.dadmm_backward_scratch_bytes(ctypes.byref(d)) == 4 * 3 * 25 * 5 * 4   # ceil(40/16) wgs
+    assert L.dadmm_backward_scratch_bytes(ctypes.byref(_dims(P=0))) == 0
+
+
+@pytest.mark.parametrize("kw,code", [
+    (dict(P=0), -1), (dict(hyp_rows=3), -1), (dict(m=65), -2), (dict(n=258), -2),
+    (dict(P=7, n=64, hyp_rows=1), -2), (dict(P=6, n=256, hyp_rows=6), -2), (dict(n=512), -2),
+])
+def test_backward_rejects_before_launch(L, kw, code):
+    assert L.dadmm_backward(ctypes.byref(_dims(**kw)), *BWD, None) == code
+    assert L.dadmm_last_error().decode()
+
+
+def test_backward_null_and_misaligned(L):
+    d = _dims()
+    args = list(BWD)
+    args[11] = None   # gY
+    assert L.dadmm_backward(ctypes.byref(d), *args, None) == -1
+    args = list(BWD)
+    args[12] = None   # dhyp
+    assert L.dadmm_backward(ctypes.byref(d), *args, None) == -1
+    args = list(BWD)
+    args[9] = ctypes.c_void_p(0x10004)   # Grec misaligned
+    assert L.dadmm_backward(ctypes.byref(d), *args, None) == -1
+    assert L.dadmm_backward(ctypes.byref(_dims(K=0)), *BWD, None) == 0
+
+
+def test_stepwise_record_pointers_both_or_neither(L):
+    d = _dims(graph_shared=1)
+    args = [ctypes.c_void_p(0x10000 * (i + 1)) for i in range(11)]   # op .. U_out
+    scratch = ctypes.c_void_p(0x100000)
+    assert L.dadmm_forward_stepwise(ctypes.byref(d), *args, ctypes.c_void_p(0xA0000), None,
+                                    ctypes.c_void_p(0xC0000), 0, scratch, None) == -1
+    assert "both" in L.dadmm_last_error().decode()
