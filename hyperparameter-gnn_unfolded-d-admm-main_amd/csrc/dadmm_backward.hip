@@ -10,7 +10,7 @@
 // through the reference's op sequence, tests/test_oracle.py).
 //
 // Reverse sweep along the trajectory the recording forward stored (Y, Grec = pre-clamp gradient,
-// Urec = U_k). Per iteration k, with g = clamp(gr_k), z = y_k - alpha g, w = U_k + delta_{k+1} eta:
+// Urec = U_k); each step reads Y[k], Y[k-1], Grec[k], Urec[k] and gY[k]. Per iteration k, with g = clamp(gr_k), z = y_k - alpha g, w = U_k + delta_{k+1} eta:
 //   w_bar = U_bar [|w| <= vclip]            dEta   += w_bar delta_{k+1}
 //   d_bar = rho_{k+1} gr_bar_{k+1} + w_bar eta     (GNN variant: masked by |2 L y_{k+1}| <= 20)
 //   y_bar += gY[k] + 2 L d_bar
@@ -50,8 +50,33 @@ __device__ __forceinline__ f32x4 bload4(rsrc_t r, uint32_t voff, uint32_t soff) 
 }
 __device__ __forceinline__ float tclamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 __device__ __forceinline__ bool inside(float x, float lo, float hi) { return x >= lo && x <= hi; }
+// compiler-only barrier: bounds how far the scheduler hoists loads (register budget)
+__device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
+// a per-iteration opaque copy of a wave-uniform value: keeps the shared graph's neighbour tests
+// inside the loop (s_bitcmp + branch) instead of P*P hoisted 64-bit condition registers
+__device__ __forceinline__ uint32_t fresh_s(uint32_t x) {
+    asm volatile("" : "=s"(x) : "0"(x));
+    return x;
+}
 
 constexpr int WAVES = 8;
+
+// GNN variant: delta = clamp(delta, -20, 20) (gnn_dlasso_models_progressive.py:229) in place;
+// returns bit 4p+r set where the pre-clamp value was inside (the clamp passes the gradient)
+template <int P>
+__device__ __forceinline__ uint32_t clamp_delta(float (&dd)[P][4], int variant) {
+    uint32_t bits = 0xffffffffu;
+    if (variant != 0) {
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (!inside(dd[p][r], -20.0f, 20.0f)) bits &= ~(1u << (4 * p + r));
+                dd[p][r] = tclamp(dd[p][r], -20.0f, 20.0f);
+            }
+    }
+    return bits;
+}
 
 template <int P, int NT, int GRAPH, int HALF>
 __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ lds, const int w) {
@@ -96,27 +121,21 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
         ord[p] = (GRAPH == GRAPH_ORDERED && sv) ? a.nbr_order[(size_t)s * P + p] : 0u;
     }
 
-    // carried state: y_bar, U_bar (adjoints w.r.t. y_{k+1}, U_{k+1}) and y_{k+1} itself;
-    // d_bar (w.r.t. delta_{k+1}) is rho_{k+1} * gr_bar_{k+1}, read back from this lane's Glds rows
-    float yb[P][E], Ub[P][E], y1[P][E];
-    {
-        const rsrc_t ry = make_rsrc(a.Y + (size_t)(K - 1) * S, state_bytes);
+    // carried state (registers): y_bar, U_bar, the adjoints w.r.t. y_{k+1}, U_{k+1}; d_bar (w.r.t.
+    // delta_{k+1}) is rho_{k+1} * gr_bar_{k+1}, read back from this lane's Glds rows; delta_{k+1}
+    // is re-formed from y_{k+1} = Y[k] (re-read: the register budget holds two [P][E] arrays)
+    float yb[P][E], Ub[P][E];
 #pragma unroll
-        for (int tt = 0; tt < T2; ++tt) {
-            const int n0 = (w * T2 + tt) * 16 + 4 * h;
-            const bool ok = has_tiles && n0 < n;
+    for (int tt = 0; tt < T2; ++tt) {
+        const int n0 = (w * T2 + tt) * 16 + 4 * h;
 #pragma unroll
-            for (int p = 0; p < P; ++p) {
-                f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-                if (ok) v = bload4(ry, (uint32_t)(((s * P + p) * n + n0) * 4), 0);
+        for (int p = 0; p < P; ++p) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    y1[p][4 * tt + r] = v[r];
-                    yb[p][4 * tt + r] = 0.0f;
-                    Ub[p][4 * tt + r] = 0.0f;
-                }
-                if (has_tiles) *(f32x4*)(Glds + (p * BT + j) * YS + n0) = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+            for (int r = 0; r < 4; ++r) {
+                yb[p][4 * tt + r] = 0.0f;
+                Ub[p][4 * tt + r] = 0.0f;
             }
+            if (has_tiles) *(f32x4*)(Glds + (p * BT + j) * YS + n0) = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
         }
     }
     float rh_next[P];   // rho_{k+1} (0 at k = K-1: no later iteration reads delta_K)
@@ -129,6 +148,12 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
     __syncthreads();
 
     for (int k = K - 1; k >= 0; --k) {
+        uint32_t mk[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            if constexpr (GRAPH == GRAPH_SHARED) mk[p] = fresh_s(msk[p]);
+            else mk[p] = msk[p];
+        }
         float al[P], ta[P], rh[P], et[P];
 #pragma unroll
         for (int p = 0; p < P; ++p) {
@@ -152,6 +177,7 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
         // ---- elementwise adjoint of iteration k on this lane's rows ---------------------------
         if (has_tiles) {
             const rsrc_t ryk = make_rsrc(k > 0 ? a.Y + (size_t)(k - 1) * S : a.y0, state_bytes);
+            const rsrc_t ry1 = make_rsrc(a.Y + (size_t)k * S, state_bytes);
             const rsrc_t rgr = make_rsrc(a.Grec + (size_t)k * S, state_bytes);
             const rsrc_t ruk = make_rsrc(a.Urec + (size_t)k * S, state_bytes);
             const rsrc_t rgy = make_rsrc(a.gY + (size_t)k * S, state_bytes);
@@ -160,91 +186,84 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
             for (int tt = 0; tt < T2; ++tt) {
                 const int n0 = (w * T2 + tt) * 16 + 4 * h;
                 const bool ok = n0 < n;
-                float yk[P][4], y1t[P][4], d1[P][4], d1b[P][4], c1b[P][4], dk[P][4];
-                bool md1[P][4];
+                // one VGPR offset per row group; the agent's (uniform) offset rides in soffset.
+                // Rows past n get an offset the buffer range check turns into zeros (no branches).
+                const uint32_t vrow = ok ? (uint32_t)((s * P * n + n0) * 4) : 0x80000000u;
+                // live ranges kept short (register budget): [P][4] temporaries t1, t2
+                float t1[P][4], t2[P][4];
+                // t2 = delta_{k+1} formed from y_{k+1} exactly as the forward did
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
-                    const uint32_t off = (uint32_t)(((s * P + p) * n + n0) * 4);
-                    f32x4 vy = {0, 0, 0, 0}, vg = {0, 0, 0, 0};
-                    if (ok) {
-                        vy = bload4(ryk, off, 0);
-                        vg = bload4(rgy, off, 0);
-                    }
+                    const f32x4 v = bload4(ry1, vrow, (uint32_t)(p * n * 4));
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        yk[p][r] = vy[r];
-                        y1t[p][r] = y1[p][4 * tt + r];
-                        yb[p][4 * tt + r] = yb[p][4 * tt + r] + vg[r];      // + gY[k]
-                    }
+                    for (int r = 0; r < 4; ++r) t1[p][r] = v[r];
                 }
-                // delta_{k+1} exactly as the forward formed it
-                consensus_any<P, GRAPH>(y1t, d1, msk, ord);
-#pragma unroll
-                for (int p = 0; p < P; ++p)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        md1[p][r] = a.variant == 0 || inside(d1[p][r], -20.0f, 20.0f);
-                        if (a.variant != 0) d1[p][r] = tclamp(d1[p][r], -20.0f, 20.0f);   // :229
-                    }
-                // dual update adjoint (:98-99)
+                consensus_any<P, GRAPH>(t1, t2, mk, ord);
+                const uint32_t md1 = clamp_delta(t2, a.variant);
+                fence();
+                // dual update adjoint (:98-99); t1 = d_bar
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
-                    const uint32_t off = (uint32_t)(((s * P + p) * n + n0) * 4);
-                    f32x4 vu = {0, 0, 0, 0};
-                    if (ok) vu = bload4(ruk, off, 0);
+                    const f32x4 vu = bload4(ruk, vrow, (uint32_t)(p * n * 4));
+                    const f32x4 vg = bload4(rgy, vrow, (uint32_t)(p * n * 4));
                     const f32x4 gprev = *(const f32x4*)(Glds + (p * BT + j) * YS + n0);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int e = 4 * tt + r;
-                        const float wv = vu[r] + d1[p][r] * et[p];
+                        yb[p][e] = yb[p][e] + vg[r];                          // + gY[k]
+                        const float wv = vu[r] + t2[p][r] * et[p];
                         const float wb = inside(wv, -vclip, vclip) ? Ub[p][e] : 0.0f;
-                        part[p][3] += wb * d1[p][r];
+                        part[p][3] += wb * t2[p][r];
                         const float db = gprev[r] * rh_next[p] + wb * et[p];
-                        d1b[p][r] = md1[p][r] ? db : 0.0f;
+                        t1[p][r] = ((md1 >> (4 * p + r)) & 1u) ? db : 0.0f;
                         Ub[p][e] = wb;
                     }
                 }
-                consensus_any<P, GRAPH>(d1b, c1b, msk, ord);   // 2 L d_bar
+                consensus_any<P, GRAPH>(t1, t2, mk, ord);   // t2 = 2 L d_bar
+#pragma unroll
+                for (int p = 0; p < P; ++p)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) yb[p][4 * tt + r] += t2[p][r];
+                fence();
+                // t1 = y_k; t2 = delta_k (k > 0: formed from y_k as the forward did; k = 0: d0)
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const f32x4 v = bload4(ryk, vrow, (uint32_t)(p * n * 4));
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) t1[p][r] = v[r];
+                }
                 if (k > 0) {
-                    consensus_any<P, GRAPH>(yk, dk, msk, ord);  // delta_k
-                    if (a.variant != 0) {
-#pragma unroll
-                        for (int p = 0; p < P; ++p)
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) dk[p][r] = tclamp(dk[p][r], -20.0f, 20.0f);
-                    }
+                    consensus_any<P, GRAPH>(t1, t2, mk, ord);
+                    clamp_delta(t2, a.variant);
                 } else {
 #pragma unroll
                     for (int p = 0; p < P; ++p) {
-                        f32x4 v = {0, 0, 0, 0};
-                        if (ok) v = bload4(rd0, (uint32_t)(((s * P + p) * n + n0) * 4), 0);
+                        const f32x4 v = bload4(rd0, vrow, (uint32_t)(p * n * 4));
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) dk[p][r] = v[r];
+                        for (int r = 0; r < 4; ++r) t2[p][r] = v[r];
                     }
                 }
+                fence();
                 // primal update + gradient clamp adjoint (:73-93)
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
-                    const uint32_t off = (uint32_t)(((s * P + p) * n + n0) * 4);
-                    f32x4 vgr = {0, 0, 0, 0};
-                    if (ok) vgr = bload4(rgr, off, 0);
+                    const f32x4 vgr = bload4(rgr, vrow, (uint32_t)(p * n * 4));
                     f32x4 gbv;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int e = 4 * tt + r;
+                        const float yk = t1[p][r];
                         const float gr = vgr[r];
                         const float g = tclamp(gr, -gclip, gclip);
-                        const float z = yk[p][r] - al[p] * g;
-                        const float ybar = yb[p][e] + c1b[p][r];
-                        const float zb = inside(z, -vclip, vclip) ? ybar : 0.0f;
+                        const float z = yk - al[p] * g;
+                        const float zb = inside(z, -vclip, vclip) ? yb[p][e] : 0.0f;
                         part[p][0] -= zb * g;
                         const float grb = inside(gr, -gclip, gclip) ? -al[p] * zb : 0.0f;
-                        const float sg = yk[p][r] > 0.0f ? 1.0f : (yk[p][r] < 0.0f ? -1.0f : 0.0f);
+                        const float sg = yk > 0.0f ? 1.0f : (yk < 0.0f ? -1.0f : 0.0f);
                         part[p][1] += grb * sg;
-                        part[p][2] += grb * dk[p][r];
+                        part[p][2] += grb * t2[p][r];
                         Ub[p][e] = Ub[p][e] + grb * dg[p];
                         yb[p][e] = zb;
-                        y1[p][e] = yk[p][r];
                         gbv[r] = ok ? grb : 0.0f;
                     }
                     *(f32x4*)(Glds + (p * BT + j) * YS + n0) = gbv;
@@ -253,20 +272,29 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
         }
         __syncthreads();
 
-        // ---- GEMM1: R_p = A_p gr_bar_p (this wave: m-block mb, agents HALF + AS*i) -----------
+        // ---- GEMM1: R_p = A_p gr_bar_p (this wave: m-block mb, agents HALF + AS*i); the A rows
+        //      of step t+1 load under the MFMAs of step t ----------------------------------------
         {
-            f32x4 acc[THA];
+            f32x4 acc[THA], av[2][THA];
 #pragma unroll
-            for (int i = 0; i < TH; ++i) acc[i] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 4
+            for (int i = 0; i < TH; ++i) {
+                acc[i] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+                av[0][i] = bload4(rA, voffA, (uint32_t)((HALF + AS * i) * MP * NP * 4));
+            }
+#pragma unroll
             for (int t = 0; t < NB; ++t) {
+                if (t + 1 < NB) {
+#pragma unroll
+                    for (int i = 0; i < TH; ++i)
+                        av[(t + 1) & 1][i] = bload4(rA, voffA + 64 * (t + 1),
+                                                    (uint32_t)((HALF + AS * i) * MP * NP * 4));
+                }
+                fence();
 #pragma unroll
                 for (int i = 0; i < TH; ++i) {
-                    const int p = HALF + AS * i;
-                    const f32x4 av = bload4(rA, voffA + 64 * t, (uint32_t)(p * MP * NP * 4));
-                    const f32x4 bv = *(const f32x4*)(brow + p * BT * YS + 16 * t);
+                    const f32x4 bv = *(const f32x4*)(brow + (HALF + AS * i) * BT * YS + 16 * t);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[i] = mfma4(av[r], bv[r], acc[i]);
+                    for (int r = 0; r < 4; ++r) acc[i] = mfma4(av[t & 1][i][r], bv[r], acc[i]);
                 }
             }
 #pragma unroll
@@ -275,28 +303,35 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
         }
         __syncthreads();
 
-        // ---- GEMM2: y_bar_p += A_p^T R_p on this wave's n-tiles ---------------------------------
+        // ---- GEMM2: y_bar_p += A_p^T R_p on this wave's n-tiles, as (agent, tile) chains of 16
+        //      MFMAs; the A^T rows of the next chain load under the current one ----------------
         if (has_tiles) {
+            constexpr int NS = P * T2;
+            f32x4 tring[2][MP / 16];
+            auto load_at = [&](f32x4 (&slot)[MP / 16], int c) {
+                const int p = c / T2, tt = c % T2;
+                const uint32_t vAt = voffAt + (uint32_t)(16 * (w * T2 + tt) * MP * 4);
 #pragma unroll
-            for (int p = 0; p < P; ++p) {
+                for (int t = 0; t < MP / 16; ++t)
+                    slot[t] = bload4(rAt, vAt + 64 * t, (uint32_t)(p * NP * MP * 4));
+            };
+            load_at(tring[0], 0);
+#pragma unroll
+            for (int c = 0; c < NS; ++c) {
+                const int p = c / T2, tt = c % T2;
+                if (c + 1 < NS) load_at(tring[(c + 1) & 1], c + 1);
+                fence();
                 f32x4 rv[MP / 16];
 #pragma unroll
                 for (int t = 0; t < MP / 16; ++t)
                     rv[t] = *(const f32x4*)(Rlds + (p * BT + j) * RS + 4 * h + 16 * t);
+                f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-                for (int tt = 0; tt < T2; ++tt) {
-                    const int nb = w * T2 + tt;
-                    const uint32_t vAt = voffAt + (uint32_t)(16 * nb * MP * 4);
-                    f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
+                for (int t = 0; t < MP / 16; ++t)
 #pragma unroll
-                    for (int t = 0; t < MP / 16; ++t) {
-                        const f32x4 av = bload4(rAt, vAt + 64 * t, (uint32_t)(p * NP * MP * 4));
+                    for (int r = 0; r < 4; ++r) gc = mfma4(tring[c & 1][t][r], rv[t][r], gc);
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) gc = mfma4(av[r], rv[t][r], gc);
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) yb[p][4 * tt + r] += gc[r];
-                }
+                for (int r = 0; r < 4; ++r) yb[p][4 * tt + r] += gc[r];
             }
         }
 
@@ -386,6 +421,9 @@ backward_fn_ptr pick_nt(int nt, int graph) {
 }  // namespace bwd
 
 backward_fn_ptr find_backward(int P, int nt, int graph) {
+#ifdef DADMM_ONLY_H   // compile-time experiments: instantiate the headline shape only
+    return (P == 5 && nt == 4 && graph == GRAPH_SHARED) ? &bwd::launch<5, 4, GRAPH_SHARED> : nullptr;
+#endif
     switch (P) {
         case 1: return bwd::pick_nt<1>(nt, graph);
         case 2: return bwd::pick_nt<2>(nt, graph);
