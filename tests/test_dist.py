@@ -1,0 +1,111 @@
+"""CPU, multi-process (gloo): the batch-sharded path of SURVEY.md §8(e) — shard ranges, the
+shard-size weighted loss all_reduce and the flattened gradient all_reduce — reproduce the
+full-batch loss and the full-batch gradient of seq_hyp.param.
+
+The forward inside each rank is the oracle's differentiable fp64 replay of the reference's ops
+(oracle/ref_torch.forward_autograd) standing in for the HIP forward (no GPU here); what is under
+test is the host-side data-parallel logic (dadmm_hip/dist.py) around it."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from dadmm_hip import dist as D
+
+MAXP = [0.1, 0.99, 0.99, 0.99]
+
+
+def test_shard_range_covers_batch():
+    for B in (1, 7, 8, 4096, 4099):
+        for W in (1, 2, 3, 8):
+            if B < W:
+                continue
+            spans = [D.shard_range(B, r, W) for r in range(W)]
+            assert spans[0][0] == 0 and spans[-1][1] == B
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(W - 1))
+            sizes = [hi - lo for lo, hi in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        D.shard_range(8, 2, 2)
+
+
+def _problem(seed=0):
+    import oracle as O
+    P, m, n, B, K = 4, 12, 32, 7, 6
+    A, b, x = O.make_problem(P, m, n, B, seed=seed)
+    graphs = [O.connected_er_graph(P, 0.5, seed=30 + s) for s in range(B)]
+    rng = np.random.default_rng(1)
+    y0, U0, d0 = (1e-2 * rng.standard_normal((3, B, P, n))).astype(np.float32)
+    param = (0.3 * rng.standard_normal((K, P, 4))).astype(np.float64)
+    return A, b, x, graphs, y0, U0, d0, param
+
+
+def _loss_and_grad(sl, A, b, x, graphs, y0, U0, d0, param):
+    """compute_loss of the forward on samples `sl`, and d loss_final / d param."""
+    import argparse
+
+    import gnn_dlasso_utils
+    import unfolded_DLASSO
+    from oracle import ref_torch
+    K, P = param.shape[:2]
+    args = argparse.Namespace(max_penalty_threshold=0.8, penalty_reduction_factor=0.95)
+    seq = unfolded_DLASSO.seq_hyperparam([K, P, 4], torch.tensor(MAXP, dtype=torch.float64), args)
+    seq.param = torch.nn.Parameter(torch.tensor(param))
+    seq.train()
+    table = seq.table(K)
+    Y, _, _, _ = ref_torch.forward_autograd(A, b[sl], [graphs[i] for i in range(*sl.indices(len(graphs)))],
+                                            table, y0[sl], U0[sl], d0[sl])
+    label = torch.as_tensor(x[sl], dtype=torch.float64)[..., None]
+    loss_mean, loss_final = gnn_dlasso_utils.compute_loss(Y[..., None], label)
+    loss_final.backward()
+    return loss_mean.detach(), loss_final.detach(), seq.param
+
+
+def _worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    r, w, _ = D.init_from_env("gloo")
+    assert (r, w) == (rank, world)
+    A, b, x, graphs, y0, U0, d0, param = _problem()
+    lo, hi = D.shard_range(b.shape[0], r, w)
+    lm, lf, p = _loss_and_grad(slice(lo, hi), A, b, x, graphs, y0, U0, d0, param)
+    gm, gf = D.global_losses(lm, lf, hi - lo)
+    D.allreduce_gradients([p], hi - lo, b.shape[0])
+    if r == 0:
+        np.savez(out_path, loss_mean=gm.numpy(), loss_final=gf.numpy(), grad=p.grad.numpy())
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_loss_and_gradient_equal_full_batch(tmp_path, world):
+    out = str(tmp_path / "r0.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    A, b, x, graphs, y0, U0, d0, param = _problem()
+    lm, lf, p = _loss_and_grad(slice(0, b.shape[0]), A, b, x, graphs, y0, U0, d0, param)
+    # compute_loss adds 1e-8 to each shard's loss; the weighted mean keeps exactly one 1e-8
+    np.testing.assert_allclose(got["loss_mean"], lm.numpy(), rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(got["loss_final"], lf.numpy(), rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(got["grad"], p.grad.numpy(), rtol=1e-9,
+                               atol=1e-12 * np.abs(p.grad.numpy()).max())
+
+
+def test_single_process_is_identity():
+    p = torch.nn.Parameter(torch.ones(3))
+    p.grad = torch.full((3,), 2.0)
+    D.allreduce_gradients([p], 5, 5)
+    assert torch.equal(p.grad, torch.full((3,), 2.0))
+    gm, gf = D.global_losses(torch.tensor(0.5), torch.tensor(0.25), 5)
+    assert float(gm) == 0.5 and float(gf) == 0.25
