@@ -234,6 +234,154 @@ int dadmm_backward(const dadmm_dims* d, const void* op, const uint64_t* nbr,
     return ok();
 }
 
+namespace {
+
+int gnn_common(const dadmm_dims* d, dadmm::GnnArgs* a) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (d->m > dadmm::M_PAD)
+        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
+                    dadmm::M_PAD);
+    if ((d->n & 3) != 0) return fail(DADMM_EUNSUPPORTED, "n=%d: needs n %% 4 == 0 (zero-pad n)", d->n);
+    *a = dadmm::GnnArgs{};
+    a->B = d->B;
+    a->P = d->P;
+    a->m = d->m;
+    a->n = d->n;
+    a->n_pad = n_pad_of(d);
+    a->K = d->K;
+    a->hyp_rows = d->hyp_rows;
+    a->variant = d->variant;
+    a->graph_shared = d->graph_shared;
+    return DADMM_OK;
+}
+
+void set_op(dadmm::GnnArgs* a, const void* op) {
+    a->A = (const float*)op;
+    a->At = a->A + (size_t)a->P * dadmm::M_PAD * a->n_pad;
+}
+
+int hip_rc(hipError_t e, const char* what) {
+    if (e != hipSuccess) return fail(DADMM_EHIP, "%s: %s", what, hipGetErrorString(e));
+    return ok();
+}
+
+}  // namespace
+
+size_t dadmm_gnn_flag_bytes(int32_t K) {
+    return K < 0 ? 0 : (size_t)GNN_FLAG_WORDS(K) * 4;
+}
+
+int dadmm_gnn_begin(const dadmm_dims* d, const void* op, const float* b, const float* y0,
+                    const float* U0, float* Atb, int32_t* flags, void* stream) {
+    dadmm::GnnArgs a;
+    int rc = gnn_common(d, &a);
+    if (rc) return rc;
+    if (!flags) return fail(DADMM_EINVAL, "flags is NULL");
+    if (d->B == 0) return hip_rc(hipMemsetAsync(flags, 0, dadmm_gnn_flag_bytes(d->K), (hipStream_t)stream), "memset");
+    if (!op || !b || !y0 || !U0 || !Atb) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(op) || !aligned16(y0) || !aligned16(U0) || !aligned16(Atb))
+        return fail(DADMM_EINVAL, "op, y0, U0 and Atb must be 16-byte aligned");
+    set_op(&a, op);
+    a.b = b;
+    a.U = U0;
+    a.flags = flags;
+    hipError_t e = hipMemsetAsync(flags, 0, dadmm_gnn_flag_bytes(d->K), (hipStream_t)stream);
+    if (e != hipSuccess) return hip_rc(e, "memset");
+    e = dadmm::gnn_launch_check0(a, y0, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_rc(e, "check0 launch");
+    return hip_rc(dadmm::gnn_launch_gram(a, 0, nullptr, Atb, 1, (hipStream_t)stream), "Atb launch");
+}
+
+int dadmm_gnn_gram(const dadmm_dims* d, const void* op, int32_t k, float* const* yptr,
+                   const int32_t* flags, const float* x, float* out, void* stream) {
+    dadmm::GnnArgs a;
+    int rc = gnn_common(d, &a);
+    if (rc) return rc;
+    if (d->B == 0) return ok();
+    if (!op || !out || (x == nullptr && (yptr == nullptr || flags == nullptr)))
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (x == nullptr && (k < 0 || k >= d->K)) return fail(DADMM_EINVAL, "k=%d outside [0, K)", k);
+    if (!aligned16(op) || !aligned16(out) || (x && !aligned16(x)))
+        return fail(DADMM_EINVAL, "op, x and out must be 16-byte aligned");
+    if (dadmm::gnn_gram_lds(a.n_pad) > 160 * 1024)
+        return fail(DADMM_EUNSUPPORTED, "n=%d too large for the gram tile", d->n);
+    set_op(&a, op);
+    a.yptr = yptr;
+    a.flags = const_cast<int32_t*>(flags);
+    return hip_rc(dadmm::gnn_launch_gram(a, k, x, out, 0, (hipStream_t)stream), "gram launch");
+}
+
+int dadmm_gnn_step(const dadmm_dims* d, int32_t k, const int32_t* visit_ptr, const uint8_t* visit_q,
+                   const float* deg, const float* hyp_k, float* const* yptr, const float* AtAy,
+                   const float* Atb, const float* U, const float* D, float* U_next, float* D_next,
+                   float* G, int32_t* flags, void* stream) {
+    dadmm::GnnArgs a;
+    int rc = gnn_common(d, &a);
+    if (rc) return rc;
+    if (k < 0 || k >= d->K) return fail(DADMM_EINVAL, "k=%d outside [0, K)", k);
+    if (d->B == 0) return ok();
+    if (!visit_ptr || !visit_q || !deg || !hyp_k || !yptr || !AtAy || !Atb || !U || !D || !U_next ||
+        !D_next || !G || !flags)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(AtAy) || !aligned16(Atb) || !aligned16(U) || !aligned16(D) || !aligned16(G))
+        return fail(DADMM_EINVAL, "AtAy, Atb, U, D and G must be 16-byte aligned");
+    a.vptr = visit_ptr;
+    a.vq = visit_q;
+    a.deg = deg;
+    a.hyp = hyp_k;
+    a.yptr = yptr;
+    a.AtAy = AtAy;
+    a.Atb = Atb;
+    a.U = U;
+    a.D = D;
+    a.U_next = U_next;
+    a.D_next = D_next;
+    a.G = G;
+    a.flags = flags;
+    return hip_rc(dadmm::gnn_launch_step(a, k, (hipStream_t)stream), "step launch");
+}
+
+int dadmm_gnn_finish(const dadmm_dims* d, float* const* yptr, int32_t* flags, int32_t* status,
+                     void* stream) {
+    dadmm::GnnArgs a;
+    int rc = gnn_common(d, &a);
+    if (rc) return rc;
+    if (d->K == 0) return ok();
+    if (!yptr || !flags) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    a.yptr = yptr;
+    a.flags = flags;
+    a.status = status;
+    return hip_rc(dadmm::gnn_launch_finish(a, (hipStream_t)stream), "finish launch");
+}
+
+int dadmm_gnn_step_backward(const dadmm_dims* d, int32_t k, const int32_t* visit_ptr,
+                            const uint8_t* visit_q, const float* deg, const float* hyp_k,
+                            const float* y_k, const float* AtAy, const float* Atb, const float* U,
+                            const float* D, const float* gy1, const float* gU1, const float* gd1,
+                            float* gy, float* gU, float* gd, float* gAtAy, float* ghyp,
+                            void* stream) {
+    dadmm::GnnArgs a;
+    int rc = gnn_common(d, &a);
+    if (rc) return rc;
+    if (k < 0 || k >= d->K) return fail(DADMM_EINVAL, "k=%d outside [0, K)", k);
+    if (d->B == 0) return ok();
+    if (!visit_ptr || !visit_q || !deg || !hyp_k || !y_k || !AtAy || !Atb || !U || !D || !gy ||
+        !gU || !gd || !gAtAy || !ghyp)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    a.vptr = visit_ptr;
+    a.vq = visit_q;
+    a.deg = deg;
+    a.hyp = hyp_k;
+    a.yk = y_k;
+    a.AtAy = AtAy;
+    a.Atb = Atb;
+    a.U = U;
+    a.D = D;
+    dadmm::GnnGrads g{gy1, gU1, gd1, gy, gU, gd, gAtAy, ghyp};
+    return hip_rc(dadmm::gnn_launch_step_backward(a, k, g, (hipStream_t)stream), "step backward launch");
+}
+
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d) {

@@ -1,0 +1,445 @@
+// dadmm_gnn.hip — per-iteration D-ADMM kernels for the GNN-hypernetwork model
+// (DLASSO_GNNHyp3_Progressive.forward, gnn_dlasso_models_progressive.py:131-243).
+//
+// There the hyper-parameters of iteration k come from a GNN evaluated on [A^T A y_k, A^T b], so
+// the K-step loop cannot be fused: each iteration is
+//   gram     AtAy_k = A^T (A y_k)            (:158-162; MFMA GEMM pair, f32 fma chains)
+//   [host]   hyp_k = GNN(cat(AtAy_k, Atb))   (torch / hipBLASLt; :165-196)
+//   grad     g_k = clamp(AtAy - Atb + sign(y) tau + U deg + delta rho, +-gclip)   (:205-213)
+//   update   y_{k+1} = clamp(y - alpha g); delta_{k+1} = clamp(2 L y_{k+1}); U_{k+1} = clamp(U +
+//            delta eta)                                                           (:221-232)
+// with the reference's batch-global NaN/Inf guards (:150-156, :216-218, :235-237) decided through
+// device flag words between launches (no host synchronisation), exactly as dadmm_stepwise.hip
+// does for the unfolded model. Y[k] stores y_{k+1}; a y_next guard that fired is resolved by
+// every later reader (y_source) and by dadmm_gnn_finish for Y[K-1].
+//
+// Operation order (restated bit-for-bit by oracle_forward_f32 with gram_mode = 1): AtAy is one
+// fma chain per row through R = A y (from +0) and A^T R (from +0), each in the fused kernel's
+// 16-block order; Atb = A^T b likewise; the gradient is ((((AtAy - Atb) + sign*tau) + U*deg) +
+// delta*rho), every operation rounded on its own (-ffp-contract=off).
+//
+// The adjoint of one iteration (dadmm_gnn_step_backward) recomputes the iteration from its
+// inputs and returns the gradients w.r.t. y_k, U_k, delta_k, AtAy_k and hyp_k; the gradient
+// w.r.t. y_k through AtAy_k is the caller's gram of the AtAy gradient (A^T A is symmetric).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dadmm_internal.h"
+
+namespace dadmm {
+namespace gnn {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int THREADS = 256;   // 4 waves
+constexpr int WAVES = 4;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// torch.clamp: NaN propagates, +-inf saturate
+__device__ __forceinline__ float clamp_t(float x, float lo, float hi) {
+    return x != x ? x : fminf(fmaxf(x, lo), hi);
+}
+__device__ __forceinline__ bool inside(float x, float lo, float hi) { return x >= lo && x <= hi; }
+__device__ __forceinline__ bool finitef(float x) { return __builtin_isfinite(x); }
+__device__ __forceinline__ int flag_ld(const int32_t* f) {
+    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void flag_or(int32_t* f, bool v) {
+    if (__ballot(v) != 0 && (threadIdx.x & 63) == 0)
+        __hip_atomic_fetch_or(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void clips(const GnnArgs& a, int k, float& gclip, float& vclip) {
+    if (a.variant == 0) {
+        gclip = fmaxf(1.0f, 30.0f - (float)k);          // unfolded_DLASSO.py:80
+        vclip = fmaxf(10.0f, 200.0f - (float)(k * 3));  // unfolded_DLASSO.py:92
+    } else {
+        gclip = 10.0f;                                   // gnn_dlasso_models_progressive.py:212
+        vclip = 100.0f;                                  // :224, :232
+    }
+}
+
+// y_k as the reference holds it at the top of iteration k: y_{j+1} (yptr[j+1]) for the last
+// j < k whose y_next passed its guard, else y0 — read as zeros when the k = 0 guard fired
+__device__ __forceinline__ const float* y_source(const GnnArgs& a, int k, bool& zero) {
+    for (int j = k - 1; j >= 0; --j)
+        if (!flag_ld(a.flags + GNN_F_YNB(j))) {
+            zero = false;
+            return a.yptr[j + 1];
+        }
+    zero = flag_ld(a.flags + GNN_F_Y0) != 0;
+    return a.yptr[0];
+}
+
+// hyp_k of sample s, agent p, component c (alpha, tau, rho, eta): [B][4][H] (view(B, 4, P|1))
+__device__ __forceinline__ float hyp_at(const GnnArgs& a, int s, int c, int p) {
+    return a.hyp[((size_t)s * 4 + c) * a.hyp_rows + (a.hyp_rows == 1 ? 0 : p)];
+}
+
+// ---- check0: the k = 0 guards on y0 / U0 (:150-156) --------------------------------------------
+__global__ __launch_bounds__(THREADS) void check0_kernel(GnnArgs a, const float* y0) {
+    const size_t S4 = (size_t)a.B * a.P * a.n / 4;
+    bool by = false, bu = false;
+    for (size_t i = (size_t)blockIdx.x * THREADS + threadIdx.x; i < S4; i += (size_t)gridDim.x * THREADS) {
+        const f32x4 y = ((const f32x4*)y0)[i];
+        const f32x4 u = ((const f32x4*)a.U)[i];
+        by |= !(finitef(y[0]) && finitef(y[1]) && finitef(y[2]) && finitef(y[3]));
+        bu |= !(finitef(u[0]) && finitef(u[1]) && finitef(u[2]) && finitef(u[3]));
+    }
+    flag_or(a.flags + GNN_F_Y0, by);
+    flag_or(a.flags + GNN_F_UBAD(0), bu);
+}
+
+// ---- gram: out = A^T (A x) per agent (mode 0), or out = A^T b (mode 1) --------------------------
+// item = (16-sample tile, agent p); x is y_k resolved through the guard flags (x_raw == nullptr)
+// or the raw operand x_raw (the adjoint's AtAy gradient).
+__global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const float* x_raw,
+                                                       float* out, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad;
+    const int tile = blockIdx.x / P, p = blockIdx.x % P;
+    const int YS = NP + 4, RS = M_PAD + 4;
+    float* Xlds = lds;               // [16][YS]
+    float* Rlds = lds + BT * YS;     // [16][RS]
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = lane & 15, h = lane >> 4;
+    const int s = tile * BT + j;
+    const bool sv = s < B;
+
+    if (mode == 0) {
+        bool zero = false;
+        const float* xs = x_raw != nullptr ? x_raw : y_source(a, k, zero);
+        const int nc4 = NP / 4;
+        for (int idx = threadIdx.x; idx < BT * nc4; idx += THREADS) {
+            const int jj = idx / nc4, c = 4 * (idx % nc4);
+            const int s2 = tile * BT + jj;
+            f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (s2 < B && c < n && !zero) v = *(const f32x4*)(xs + ((size_t)s2 * P + p) * n + c);
+            *(f32x4*)(Xlds + jj * YS + c) = v;
+        }
+        __syncthreads();
+        // GEMM1: R = A_p x (chain from +0); wave w = m-block w
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (16 * w < m) {
+            const float* arow = a.A + ((size_t)p * M_PAD + 16 * w + j) * NP + 4 * h;
+            const float* brow = Xlds + j * YS + 4 * h;
+            for (int t = 0; t < NP / 16; ++t) {
+                const f32x4 av = *(const f32x4*)(arow + 16 * t);
+                const f32x4 bv = *(const f32x4*)(brow + 16 * t);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc = mfma4(av[r], bv[r], acc);
+            }
+        }
+        *(f32x4*)(Rlds + j * RS + 16 * w + 4 * h) = acc;
+    } else {
+        // R = b_p (rows past m are zero)
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int mi = 16 * w + 4 * h + r;
+            v[r] = (sv && mi < m) ? a.b[((size_t)s * P + p) * m + mi] : 0.0f;
+        }
+        *(f32x4*)(Rlds + j * RS + 16 * w + 4 * h) = v;
+    }
+    __syncthreads();
+    // GEMM2: out = A_p^T R (chain from +0); wave w takes n-tiles w, w + 4, ...
+    f32x4 rv[M_PAD / 16];
+#pragma unroll
+    for (int t = 0; t < M_PAD / 16; ++t) rv[t] = *(const f32x4*)(Rlds + j * RS + 16 * t + 4 * h);
+    for (int nb = w; nb < NP / 16; nb += WAVES) {
+        const float* atrow = a.At + ((size_t)p * NP + 16 * nb + j) * M_PAD + 4 * h;
+        f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int t = 0; t < M_PAD / 16; ++t) {
+            const f32x4 av = *(const f32x4*)(atrow + 16 * t);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gc = mfma4(av[r], rv[t][r], gc);
+        }
+        const int n0 = 16 * nb + 4 * h;
+        if (sv && n0 < n) *(f32x4*)(out + ((size_t)s * P + p) * n + n0) = gc;
+    }
+}
+
+// ---- grad: g = clamp(((AtAy - Atb) + sign(y) tau) + U deg + delta rho) (:205-213) --------------
+__global__ __launch_bounds__(THREADS) void grad_kernel(GnnArgs a, int k) {
+    const int P = a.P, n = a.n;
+    const size_t S4 = (size_t)a.B * P * n / 4;
+    bool yzero = false;
+    const float* ys = y_source(a, k, yzero);
+    const bool uzero = flag_ld(a.flags + GNN_F_UBAD(k)) != 0;
+    float gclip, vclip;
+    clips(a, k, gclip, vclip);
+    bool bad = false;
+    for (size_t i = (size_t)blockIdx.x * THREADS + threadIdx.x; i < S4; i += (size_t)gridDim.x * THREADS) {
+        const size_t e = 4 * i;
+        const int s = (int)(e / ((size_t)P * n)), p = (int)((e / n) % P);
+        const float ta = hyp_at(a, s, 1, p), rh = hyp_at(a, s, 2, p);
+        const float dg = a.deg[(a.graph_shared ? 0 : (size_t)s * P) + p];
+        const f32x4 aty = ((const f32x4*)a.AtAy)[i];
+        const f32x4 atb = ((const f32x4*)a.Atb)[i];
+        const f32x4 yv = yzero ? (f32x4){0, 0, 0, 0} : ((const f32x4*)ys)[i];
+        const f32x4 uv = uzero ? (f32x4){0, 0, 0, 0} : ((const f32x4*)a.U)[i];
+        const f32x4 dv = ((const f32x4*)a.D)[i];
+        f32x4 gv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float y = yv[r];
+            const float st = y > 0.0f ? ta : (y < 0.0f ? -ta : 0.0f);   // sign(y) * tau
+            float g = aty[r] - atb[r];
+            g = g + st;
+            g = g + uv[r] * dg;
+            g = g + dv[r] * rh;
+            g = clamp_t(g, -gclip, gclip);
+            bad |= g != g;                                     // after the clamp only NaN (:216)
+            gv[r] = g;
+        }
+        ((f32x4*)a.G)[i] = gv;
+    }
+    flag_or(a.flags + GNN_F_GBAD(k), bad);
+}
+
+// ---- update: primal update, consensus and dual update of (sample, 64 columns) (:221-232) -------
+__global__ __launch_bounds__(THREADS) void update_kernel(GnnArgs a, int k, int items) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int item = blockIdx.x * WAVES + (threadIdx.x >> 6);
+    if (item >= items) return;
+    const int P = a.P, n = a.n;
+    const int nch = (n + 63) / 64;
+    const int s = item / nch, c = (item % nch) * 64 + (threadIdx.x & 63);
+    const bool cv = c < n;
+    const size_t base = (size_t)s * P * n + c;
+    bool yzero = false;
+    const float* ys = y_source(a, k, yzero);
+    const bool gzero = flag_ld(a.flags + GNN_F_GBAD(k)) != 0;
+    const bool uzero = flag_ld(a.flags + GNN_F_UBAD(k)) != 0;
+    float gclip, vclip;
+    clips(a, k, gclip, vclip);
+    float* yl = lds + (threadIdx.x >> 6) * (P * 64);
+    const int lane = threadIdx.x & 63;
+    float* Yk = a.yptr[k + 1];
+    bool bad_y = false;
+    for (int p = 0; p < P; ++p) {
+        float v = 0.0f;
+        if (cv) {
+            const float g = gzero ? 0.0f : a.G[base + (size_t)p * n];        // :216-218
+            const float y = yzero ? 0.0f : ys[base + (size_t)p * n];
+            v = clamp_t(y - hyp_at(a, s, 0, p) * g, -vclip, vclip);         // :221-225
+            Yk[base + (size_t)p * n] = v;
+            bad_y |= !finitef(v);
+        }
+        yl[p * 64 + lane] = v;
+    }
+    const int g0 = a.graph_shared ? 0 : s * P;
+    bool bad_u = false;
+    for (int p = 0; p < P; ++p) {
+        const float yp = yl[p * 64 + lane];
+        float acc = 0.0f;
+        const int t1 = a.vptr[g0 + p + 1];
+        for (int t = a.vptr[g0 + p]; t < t1; ++t) acc = acc + (yp - yl[(int)a.vq[t] * 64 + lane]);
+        if (a.variant != 0) acc = clamp_t(acc, -20.0f, 20.0f);             // :229
+        if (cv) {
+            const size_t off = base + (size_t)p * n;
+            const float u = uzero ? 0.0f : a.U[off];
+            const float un = clamp_t(u + acc * hyp_at(a, s, 3, p), -vclip, vclip);   // :231-232
+            a.U_next[off] = un;
+            a.D_next[off] = acc;
+            bad_u |= !finitef(un);
+        }
+    }
+    flag_or(a.flags + GNN_F_YNB(k), bad_y);
+    flag_or(a.flags + GNN_F_UBAD(k + 1), bad_u);
+}
+
+// ---- finish: Y[K-1] = y_{K-1} when the last y_next failed its guard; status bits ----------------
+__global__ __launch_bounds__(THREADS) void finish_kernel(GnnArgs a) {
+    const int K = a.K;
+    if (flag_ld(a.flags + GNN_F_YNB(K - 1))) {
+        bool zero = false;
+        const float* ys = y_source(a, K, zero);   // skips yptr[K]
+        const size_t S4 = (size_t)a.B * a.P * a.n / 4;
+        f32x4* dst = (f32x4*)a.yptr[K];
+        for (size_t i = (size_t)blockIdx.x * THREADS + threadIdx.x; i < S4; i += (size_t)gridDim.x * THREADS)
+            dst[i] = zero ? (f32x4){0.0f, 0.0f, 0.0f, 0.0f} : ((const f32x4*)ys)[i];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.status != nullptr) {
+        int st = flag_ld(a.flags + GNN_F_Y0) ? 1 : 0;
+        for (int k = 0; k < K; ++k) {
+            st |= flag_ld(a.flags + GNN_F_UBAD(k)) ? 2 : 0;
+            st |= flag_ld(a.flags + GNN_F_GBAD(k)) ? 4 : 0;
+            st |= flag_ld(a.flags + GNN_F_YNB(k)) ? 8 : 0;
+        }
+        *a.status = st;
+    }
+}
+
+// ---- adjoint of one iteration (no guard fired) ---------------------------------------------------
+// One wave per sample (lanes = columns, all P agents per lane: the consensus and its adjoint are
+// lane-local); the per-sample hyper-parameter gradients reduce over the sample's columns (wave
+// shuffles per 64-column chunk, accumulated in LDS in chunk order: deterministic).
+__global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k, GnnGrads gg) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int P = a.P, n = a.n, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int H = a.hyp_rows;
+    float* sl = lds + wv * (3 * P * 64 + 4 * P);
+    float* y1l = sl;                           // [P][64] y_{k+1}
+    float* dbl = sl + P * 64;                  // [P][64] d_bar_raw
+    float* ybl = sl + 2 * P * 64;              // [P][64] 2 L d_bar_raw
+    float* red = sl + 3 * P * 64;              // [4][H] per-sample hyp gradient
+    const int s = blockIdx.x * WAVES + wv;
+    if (s >= a.B) return;                      // whole waves only: no block barrier below
+    float gclip, vclip;
+    clips(a, k, gclip, vclip);
+    const float* ys = a.yk;
+    const int g0 = a.graph_shared ? 0 : s * P;
+    for (int i = lane; i < 4 * H; i += 64) red[i] = 0.0f;
+    auto accum = [&](int c, int p, float v) {   // wave-sum v into red[c][p or 0]
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) red[c * H + (H == 1 ? 0 : p)] += v;
+    };
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int c = c0 + lane;
+        const bool cv = c < n;
+        const size_t base = (size_t)s * P * n + c;
+        // recompute y_{k+1} for every agent of this column
+        for (int p = 0; p < P; ++p) {
+            float y1 = 0.0f;
+            if (cv) {
+                const size_t off = base + (size_t)p * n;
+                const float y = ys[off];
+                const float ta = hyp_at(a, s, 1, p);
+                const float st = y > 0.0f ? ta : (y < 0.0f ? -ta : 0.0f);
+                float gr = a.AtAy[off] - a.Atb[off];
+                gr = gr + st;
+                gr = gr + a.U[off] * a.deg[g0 + p];
+                gr = gr + a.D[off] * hyp_at(a, s, 2, p);
+                const float g = clamp_t(gr, -gclip, gclip);
+                y1 = clamp_t(y - hyp_at(a, s, 0, p) * g, -vclip, vclip);
+            }
+            y1l[p * 64 + lane] = y1;
+        }
+        // dual update adjoint; d_bar_raw (w.r.t. 2 L y_{k+1} before the GNN clamp)
+        for (int p = 0; p < P; ++p) {
+            const float yp = y1l[p * 64 + lane];
+            float acc = 0.0f;
+            const int t1 = a.vptr[g0 + p + 1];
+            for (int t = a.vptr[g0 + p]; t < t1; ++t) acc = acc + (yp - y1l[(int)a.vq[t] * 64 + lane]);
+            float dbr = 0.0f, pe = 0.0f;
+            if (cv) {
+                const size_t off = base + (size_t)p * n;
+                const float d1 = a.variant != 0 ? clamp_t(acc, -20.0f, 20.0f) : acc;
+                const float et = hyp_at(a, s, 3, p);
+                const float wvv = a.U[off] + d1 * et;
+                const float wb = (gg.gU1 != nullptr && inside(wvv, -vclip, vclip)) ? gg.gU1[off] : 0.0f;
+                pe = wb * d1;
+                const float db = (gg.gd1 != nullptr ? gg.gd1[off] : 0.0f) + wb * et;
+                dbr = (a.variant == 0 || inside(acc, -20.0f, 20.0f)) ? db : 0.0f;
+                gg.gU[off] = wb;
+            }
+            accum(3, p, pe);
+            dbl[p * 64 + lane] = dbr;
+        }
+        for (int p = 0; p < P; ++p) {   // 2 L d_bar_raw, same visit lists (the map is symmetric)
+            const float xp = dbl[p * 64 + lane];
+            float acc = 0.0f;
+            const int t1 = a.vptr[g0 + p + 1];
+            for (int t = a.vptr[g0 + p]; t < t1; ++t) acc = acc + (xp - dbl[(int)a.vq[t] * 64 + lane]);
+            ybl[p * 64 + lane] = acc;
+        }
+        // primal update + gradient clamp adjoint
+        for (int p = 0; p < P; ++p) {
+            float pa = 0.0f, pt = 0.0f, pr = 0.0f;
+            if (cv) {
+                const size_t off = base + (size_t)p * n;
+                const float al = hyp_at(a, s, 0, p), ta = hyp_at(a, s, 1, p), rh = hyp_at(a, s, 2, p);
+                const float y = ys[off];
+                const float sg = y > 0.0f ? 1.0f : (y < 0.0f ? -1.0f : 0.0f);
+                const float st = y > 0.0f ? ta : (y < 0.0f ? -ta : 0.0f);
+                float gr = a.AtAy[off] - a.Atb[off];
+                gr = gr + st;
+                gr = gr + a.U[off] * a.deg[g0 + p];
+                gr = gr + a.D[off] * rh;
+                const float g = clamp_t(gr, -gclip, gclip);
+                const float z = y - al * g;
+                const float yb = (gg.gy1 != nullptr ? gg.gy1[off] : 0.0f) + ybl[p * 64 + lane];
+                const float zb = inside(z, -vclip, vclip) ? yb : 0.0f;
+                pa = -zb * g;
+                const float grb = inside(gr, -gclip, gclip) ? -al * zb : 0.0f;
+                pt = grb * sg;
+                pr = grb * a.D[off];
+                gg.gy[off] = zb;
+                gg.gU[off] = gg.gU[off] + grb * a.deg[g0 + p];
+                gg.gd[off] = grb * rh;
+                gg.gAtAy[off] = grb;
+            }
+            accum(0, p, pa);
+            accum(1, p, pt);
+            accum(2, p, pr);
+        }
+    }
+    for (int i = lane; i < 4 * H; i += 64) gg.ghyp[(size_t)s * 4 * H + i] = red[i];
+}
+
+}  // namespace gnn
+
+// ---- launchers -----------------------------------------------------------------------------------
+static int grid_for(size_t work, int per_block, int cap) {
+    size_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    return (int)(g < (size_t)cap ? g : cap);
+}
+
+hipError_t gnn_launch_check0(const GnnArgs& a, const float* y0, hipStream_t st) {
+    const int g = grid_for((size_t)a.B * a.P * a.n / 4, gnn::THREADS, 2048);
+    hipLaunchKernelGGL(gnn::check0_kernel, dim3(g), dim3(gnn::THREADS), 0, st, a, y0);
+    return hipGetLastError();
+}
+
+size_t gnn_gram_lds(int n_pad) { return 4 * (size_t)(BT * (n_pad + 4) + BT * (M_PAD + 4)); }
+
+hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* out, int mode,
+                           hipStream_t st) {
+    const size_t lds = gnn_gram_lds(a.n_pad);
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)gnn::gram_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    const int items = ((a.B + BT - 1) / BT) * a.P;
+    hipLaunchKernelGGL(gnn::gram_kernel, dim3(items), dim3(gnn::THREADS), lds, st, a, k, x_raw, out,
+                       mode);
+    return hipGetLastError();
+}
+
+hipError_t gnn_launch_step(const GnnArgs& a, int k, hipStream_t st) {
+    const int g = grid_for((size_t)a.B * a.P * a.n / 4, gnn::THREADS, 4096);
+    hipLaunchKernelGGL(gnn::grad_kernel, dim3(g), dim3(gnn::THREADS), 0, st, a, k);
+    const int items = a.B * ((a.n + 63) / 64);
+    const size_t lds = 4 * (size_t)gnn::WAVES * a.P * 64;
+    hipLaunchKernelGGL(gnn::update_kernel, dim3((items + gnn::WAVES - 1) / gnn::WAVES),
+                       dim3(gnn::THREADS), lds, st, a, k, items);
+    return hipGetLastError();
+}
+
+hipError_t gnn_launch_finish(const GnnArgs& a, hipStream_t st) {
+    const int g = grid_for((size_t)a.B * a.P * a.n / 4, gnn::THREADS, 2048);
+    hipLaunchKernelGGL(gnn::finish_kernel, dim3(g), dim3(gnn::THREADS), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t gnn_launch_step_backward(const GnnArgs& a, int k, const GnnGrads& gg, hipStream_t st) {
+    const size_t lds = 4 * (size_t)gnn::WAVES * (3 * a.P * 64 + 4 * a.P);
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)gnn::step_backward_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(gnn::step_backward_kernel, dim3((a.B + gnn::WAVES - 1) / gnn::WAVES),
+                       dim3(gnn::THREADS), lds, st, a, k, gg);
+    return hipGetLastError();
+}
+
+}  // namespace dadmm

@@ -63,6 +63,54 @@ backward_fn_ptr find_backward(int P, int nt, int graph);
 hipError_t launch_backward_reduce(const float* partial, float* dhyp, int nwg, int K, int P, int H,
                                   hipStream_t stream);
 
+// ---- GNN-model per-iteration path (dadmm_gnn.hip) -----------------------------------------------
+// flag words (int32, zeroed by dadmm_gnn_begin): y0 guard, then U_k non-finite (k = 0..K),
+// gradient NaN and y_next non-finite (k = 0..K-1)
+#define GNN_F_Y0 0
+#define GNN_F_UBAD(k) (1 + 3 * (k))
+#define GNN_F_GBAD(k) (2 + 3 * (k))
+#define GNN_F_YNB(k) (3 + 3 * (k))
+#define GNN_FLAG_WORDS(K) (3 * (K) + 4)
+
+struct GnnArgs {
+    const float* A;         // prepared operator [P][M_PAD][n_pad]
+    const float* At;        // [P][n_pad][M_PAD]
+    const float* b;         // [B][P][m]
+    const int32_t* vptr;    // visit lists (as StepArgs)
+    const uint8_t* vq;
+    const float* deg;       // [G][P]
+    const float* hyp;       // [B][4][hyp_rows] of the current iteration
+    float* const* yptr;     // device table [K+1]: y0, y_1 .. y_K (Y[k] = y_{k+1})
+    const float* yk;        // adjoint: y_k itself
+    const float* AtAy;      // [B][P][n]
+    const float* Atb;       // [B][P][n]
+    const float* U;         // U_k (check0: U0)
+    const float* D;         // delta_k
+    float* U_next;          // U_{k+1}
+    float* D_next;          // delta_{k+1}
+    float* G;               // scratch [B][P][n]: clamped gradient of the iteration
+    int32_t* flags;         // [GNN_FLAG_WORDS(K)]
+    int32_t* status;        // nullable
+    int B, P, m, n, n_pad, K, hyp_rows, variant, graph_shared;
+};
+struct GnnGrads {
+    const float* gy1;       // dL/dy_{k+1} (nullable = 0)
+    const float* gU1;       // dL/dU_{k+1} (nullable)
+    const float* gd1;       // dL/ddelta_{k+1} (nullable)
+    float* gy;              // dL/dy_k (direct path; the AtAy path is the caller's gram)
+    float* gU;              // dL/dU_k
+    float* gd;              // dL/ddelta_k
+    float* gAtAy;           // dL/dAtAy_k
+    float* ghyp;            // dL/dhyp_k [B][4][hyp_rows]
+};
+hipError_t gnn_launch_check0(const GnnArgs& a, const float* y0, hipStream_t st);
+hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* out, int mode,
+                           hipStream_t st);
+hipError_t gnn_launch_step(const GnnArgs& a, int k, hipStream_t st);
+hipError_t gnn_launch_finish(const GnnArgs& a, hipStream_t st);
+hipError_t gnn_launch_step_backward(const GnnArgs& a, int k, const GnnGrads& gg, hipStream_t st);
+size_t gnn_gram_lds(int n_pad);
+
 // Operator preparation kernel launcher (dadmm_prepare.hip).
 hipError_t launch_prepare(const float* A, float* Apad, float* Atpad, int P, int m, int n,
                           int n_pad, hipStream_t stream);

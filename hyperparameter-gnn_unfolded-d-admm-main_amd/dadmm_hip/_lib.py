@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -29,6 +29,12 @@ EXPORTED_SYMBOLS = (
     "dadmm_forward_stepwise",
     "dadmm_backward_scratch_bytes",
     "dadmm_backward",
+    "dadmm_gnn_flag_bytes",
+    "dadmm_gnn_begin",
+    "dadmm_gnn_gram",
+    "dadmm_gnn_step",
+    "dadmm_gnn_finish",
+    "dadmm_gnn_step_backward",
 )
 
 
@@ -84,6 +90,17 @@ def load() -> ctypes.CDLL:
     L.dadmm_backward_scratch_bytes.argtypes = [ctypes.POINTER(Dims)]
     L.dadmm_backward.restype = ctypes.c_int
     L.dadmm_backward.argtypes = [ctypes.POINTER(Dims)] + [vp] * 14
+    D = ctypes.POINTER(Dims)
+    L.dadmm_gnn_flag_bytes.restype = ctypes.c_size_t
+    L.dadmm_gnn_flag_bytes.argtypes = [i32]
+    for name, args in (("dadmm_gnn_begin", [D] + [vp] * 7),
+                       ("dadmm_gnn_gram", [D, vp, i32] + [vp] * 5),
+                       ("dadmm_gnn_step", [D, i32] + [vp] * 14),
+                       ("dadmm_gnn_finish", [D] + [vp] * 4),
+                       ("dadmm_gnn_step_backward", [D, i32] + [vp] * 18)):
+        f = getattr(L, name)
+        f.restype = ctypes.c_int
+        f.argtypes = args
     v = L.dadmm_abi_version()
     if v != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {v}, expected {ABI_VERSION}")

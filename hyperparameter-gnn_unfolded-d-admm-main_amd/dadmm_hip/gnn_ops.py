@@ -1,0 +1,142 @@
+"""Per-iteration HIP path of the GNN-hypernetwork model (C ABI: the dadmm_gnn_* entry points of
+include/dadmm.h) and its autograd plumbing.
+
+The hypernetwork between iterations is torch (its linears run on hipBLASLt MFMA GEMMs); every
+D-ADMM operation — A^T A y, A^T b, the gradient assembly and clamps, the primal / consensus / dual
+updates and the reference's batch-global guards — runs in libdadmm.so.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .graph import GraphBatch
+from .ops import PreparedOperator, _dev_check, _pad_n, _ptr, _stream
+
+
+class GnnRun:
+    """Device state of one forward of DLASSO_GNNHyp3_Progressive: guard flags, Atb, the iterate
+    table (y0, y_1 .. y_K) and its device pointer array."""
+
+    def __init__(self, op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, K: int, H: int,
+                 variant: int, y0, U0, d0, grad: bool):
+        _dev_check(b, y0, U0, d0, graphs.deg)
+        B, P, m = b.shape
+        ns = op.n_store
+        dev = b.device
+        self.op, self.graphs, self.K, self.H, self.variant, self.grad = op, graphs, K, H, variant, grad
+        self.B, self.P, self.dev = B, P, dev
+        self.d = op.dims(B=B, K=K, variant=variant, hyp_rows=H, graph_shared=graphs.shared)
+        self.L = _lib.load()
+        self.y0 = _pad_n(y0.float(), ns).contiguous()
+        self.U0 = _pad_n(U0.float(), ns).contiguous()
+        self.d0 = _pad_n(d0.float(), ns).contiguous()
+        self.b = b.contiguous().float()
+        if grad:
+            self.ys = [self.y0] + [torch.empty((B, P, ns), device=dev) for _ in range(K)]
+            self.Y = None
+        else:
+            self.Y = torch.empty((K, B, P, ns), device=dev)
+            self.ys = [self.y0] + list(self.Y.unbind(0))
+        self.yptr = torch.tensor([t.data_ptr() for t in self.ys], dtype=torch.int64).to(
+            dev, non_blocking=False)
+        self.flags = torch.empty(max(self.L.dadmm_gnn_flag_bytes(K) // 4, 1), dtype=torch.int32,
+                                 device=dev)
+        self.Atb = torch.empty((B, P, ns), device=dev)
+        self.G = torch.empty((B, P, ns), device=dev)
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        with torch.cuda.device(dev):
+            _lib.check("dadmm_gnn_begin", self.L.dadmm_gnn_begin(
+                ctypes.byref(self.d), _ptr(op.workspace), _ptr(self.b), _ptr(self.y0),
+                _ptr(self.U0), _ptr(self.Atb), _ptr(self.flags), _stream(dev)))
+
+    def gram(self, k: int, x: torch.Tensor = None) -> torch.Tensor:
+        """A^T A y_k (guard-resolved y_k) or, with ``x``, A^T A x."""
+        out = torch.empty((self.B, self.P, self.op.n_store), device=self.dev)
+        if x is not None:
+            x = _pad_n(x.float(), self.op.n_store).contiguous()
+        with torch.cuda.device(self.dev):
+            _lib.check("dadmm_gnn_gram", self.L.dadmm_gnn_gram(
+                ctypes.byref(self.d), _ptr(self.op.workspace), k, _ptr(self.yptr), _ptr(self.flags),
+                _ptr(x), _ptr(out), _stream(self.dev)))
+        return out
+
+    def step(self, k: int, AtAy, hyp_k, U, D):
+        """One iteration; returns (y_{k+1}, U_{k+1}, delta_{k+1})."""
+        g = self.graphs
+        U_next = torch.empty_like(U)
+        D_next = torch.empty_like(D)
+        with torch.cuda.device(self.dev):
+            _lib.check("dadmm_gnn_step", self.L.dadmm_gnn_step(
+                ctypes.byref(self.d), k, _ptr(g.vptr), _ptr(g.vq), _ptr(g.deg), _ptr(hyp_k),
+                _ptr(self.yptr), _ptr(AtAy), _ptr(self.Atb), _ptr(U), _ptr(D), _ptr(U_next),
+                _ptr(D_next), _ptr(self.G), _ptr(self.flags), _stream(self.dev)))
+        return self.ys[k + 1], U_next, D_next
+
+    def finish(self) -> torch.Tensor:
+        with torch.cuda.device(self.dev):
+            _lib.check("dadmm_gnn_finish", self.L.dadmm_gnn_finish(
+                ctypes.byref(self.d), _ptr(self.yptr), _ptr(self.flags), _ptr(self.status),
+                _stream(self.dev)))
+        return self.status
+
+    def step_backward(self, k, y_k, AtAy, hyp_k, U, D, gy1, gU1, gd1):
+        g = self.graphs
+        mk = lambda t: None if t is None else t.contiguous()
+        gy1, gU1, gd1 = mk(gy1), mk(gU1), mk(gd1)
+        gy, gU, gd, gA = (torch.empty_like(U) for _ in range(4))
+        ghyp = torch.empty((self.B, 4, self.H), device=self.dev)
+        with torch.cuda.device(self.dev):
+            _lib.check("dadmm_gnn_step_backward", self.L.dadmm_gnn_step_backward(
+                ctypes.byref(self.d), k, _ptr(g.vptr), _ptr(g.vq), _ptr(g.deg), _ptr(hyp_k),
+                _ptr(y_k), _ptr(AtAy), _ptr(self.Atb), _ptr(U), _ptr(D), _ptr(gy1), _ptr(gU1),
+                _ptr(gd1), _ptr(gy), _ptr(gU), _ptr(gd), _ptr(gA), _ptr(ghyp), _stream(self.dev)))
+        return gy, gU, gd, gA, ghyp
+
+
+def _check_guards(run: GnnRun):
+    """Once per backward pass (one host sync): the adjoint assumes no guard fired."""
+    if getattr(run, "_checked", False):
+        return
+    st = int(run.status.item())
+    run._checked = True
+    if st:
+        from .autograd import GuardAdjointError
+        from .ops import describe_status
+        raise GuardAdjointError(
+            "backward through a forward in which the reference's NaN/Inf guards fired ("
+            + "; ".join(describe_status(st)) + ") is not supported")
+
+
+class GramFn(torch.autograd.Function):
+    """AtAy_k = A^T A y_k (gnn_dlasso_models_progressive.py:158-162); backward: A^T A g."""
+
+    @staticmethod
+    def forward(ctx, y_k, run, k):
+        ctx.run = run
+        return run.gram(k)
+
+    @staticmethod
+    def backward(ctx, g):
+        _check_guards(ctx.run)
+        return ctx.run.gram(0, x=g), None, None
+
+
+class StepFn(torch.autograd.Function):
+    """(y_{k+1}, U_{k+1}, delta_{k+1}) = one D-ADMM iteration (:205-237)."""
+
+    @staticmethod
+    def forward(ctx, y_k, U, D, AtAy, hyp_k, run, k):
+        y1, U1, D1 = run.step(k, AtAy, hyp_k, U, D)
+        ctx.run, ctx.k = run, k
+        ctx.save_for_backward(y_k, U, D, AtAy, hyp_k)
+        return y1, U1, D1
+
+    @staticmethod
+    def backward(ctx, gy1, gU1, gd1):
+        _check_guards(ctx.run)
+        y_k, U, D, AtAy, hyp_k = ctx.saved_tensors
+        gy, gU, gd, gA, ghyp = ctx.run.step_backward(ctx.k, y_k, AtAy, hyp_k, U, D, gy1, gU1, gd1)
+        return gy, gU, gd, gA, ghyp, None, None

@@ -1,0 +1,257 @@
+"""Drop-in ``gnn_dlasso_models_progressive``: ``GNNHypernetwork3`` and ``DLASSO_GNNHyp3_Progressive``.
+
+Mirrors the reference's public interface (gnn_dlasso_models_progressive.py:9-276): constructor
+``(A, args)`` (reads GHN_iter_num, GHyp_hidden, DADMM_mode, alpha/tau/rho/eta_max), forward
+``(b, graph_list, training_iterations=None) -> (Y [K,B,P,n,1], (alpha, tau, rho, eta))`` with each
+hyper-parameter ``[B, P|1, 1, 1]`` and ``K = training_iterations`` taken as given (no min with
+self.K, :137), and PyG-compatible state_dict names (``encoder.conv{1..5}.lin.weight``,
+``encoder.conv{i}.bias``, ``encoder.bn{i}.*``, ``encoder.norm.*``, ``decoder.{0,2,4,6,8,10}.*``,
+``fc.*``).
+
+Execution: every D-ADMM operation of the K-step loop — A^T A y_k, A^T b, gradient assembly,
+clamps, primal / consensus / dual updates and the batch-global NaN/Inf guards — runs in the HIP
+library one iteration at a time (``dadmm_hip.gnn_ops``); the hypernetwork between iterations is
+batched torch: all B per-sample graphs at once (the reference loops over samples in Python,
+:37-40), its linears on hipBLASLt (MFMA) GEMMs.
+
+GCNConv (torch_geometric; absent here, unpinned version) is restated from its
+published algorithm: out = D^-1/2 (Adj + I) D^-1/2 (X W^T) + bias, self-loops added where missing,
+D = degree with the self-loop — PARITY UNPINNED against torch_geometric itself. BatchNorm1d is
+applied per sample over its P nodes exactly as the reference's per-sample calls do (train mode:
+batch statistics of the P nodes; running statistics updated once per sample, in sample order,
+every iteration); Dropout(0.1) draws from torch's generator (not the reference's stream).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from dadmm_hip import _lib
+from dadmm_hip.gnn_ops import GnnRun, GramFn, StepFn
+from dadmm_hip.graph import ingest
+from dadmm_hip.ops import PreparedOperator
+
+
+class GCNConv(nn.Module):
+    """torch_geometric.nn.GCNConv(in, out) restated for dense per-sample normalized adjacency:
+    ``lin`` (no bias) then aggregation then ``bias`` (PyG parameter names)."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.lin = nn.Linear(in_channels, out_channels, bias=False)
+        self.bias = nn.Parameter(torch.zeros(out_channels))
+        nn.init.xavier_uniform_(self.lin.weight)
+
+    def forward(self, x, a_hat):
+        # x [B, P, Cin]; a_hat [B|1, P, P] = D^-1/2 (Adj + I) D^-1/2
+        return torch.matmul(a_hat, self.lin(x)) + self.bias
+
+
+def normalized_adjacency(nbr_bits: torch.Tensor, P: int, dtype=torch.float32) -> torch.Tensor:
+    """gcn_norm of each sample's graph: [G, P] int64 neighbour masks -> [G, P, P] ``dtype``.
+    Self-loops are added where missing (add_remaining_self_loops, fill value 1); the degree
+    counts the self-loop; both edge directions carry weight 1 (from_networkx of an nx.Graph)."""
+    q = torch.arange(P, device=nbr_bits.device, dtype=torch.int64)
+    adj = ((nbr_bits[..., :, None] >> q) & 1).to(dtype)
+    eye = torch.eye(P, device=nbr_bits.device, dtype=dtype)
+    adj = torch.maximum(adj, eye)
+    dinv = adj.sum(-1).rsqrt()
+    return dinv[..., :, None] * adj * dinv[..., None, :]
+
+
+def _per_sample_batch_norm(x: torch.Tensor, bn: nn.BatchNorm1d) -> torch.Tensor:
+    """bn applied to every sample's [P, C] block separately (the reference's per-sample call)."""
+    B, P, C = x.shape
+    if not bn.training:
+        return F.batch_norm(x.reshape(B * P, C), bn.running_mean, bn.running_var, bn.weight,
+                            bn.bias, False, 0.0, bn.eps).reshape(B, P, C)
+    if P < 2:
+        raise ValueError(f"Expected more than 1 value per channel when training, got input size "
+                         f"torch.Size([{P}, {C}])")
+    mean = x.mean(dim=1, keepdim=True)
+    var = x.var(dim=1, unbiased=False, keepdim=True)
+    y = (x - mean) * torch.rsqrt(var + bn.eps) * bn.weight + bn.bias
+    if bn.track_running_stats:
+        with torch.no_grad():
+            # B sequential updates r <- (1 - m) r + m s_i, in closed form
+            m = bn.momentum
+            w = m * (1.0 - m) ** torch.arange(B - 1, -1, -1, device=x.device, dtype=torch.float64)
+            decay = (1.0 - m) ** B
+            s_mean = mean[:, 0, :].double()
+            s_var = var[:, 0, :].double() * (P / (P - 1))
+            bn.running_mean.copy_((decay * bn.running_mean.double() + w @ s_mean).float())
+            bn.running_var.copy_((decay * bn.running_var.double() + w @ s_var).float())
+            bn.num_batches_tracked += B
+    return y
+
+
+class GNNHypernetwork3(nn.Module):
+    """Five GCNConv -> leaky_relu -> BatchNorm1d -> Dropout blocks, then LayerNorm
+    (reference gnn_dlasso_models_progressive.py:9-72). Input [B, P, m] node features
+    (m = 2n: [AtAy, Atb]); output [B, P * 4h]."""
+
+    def __init__(self, P, m, hidden_dim):
+        super().__init__()
+        self.P = P
+        self.m = m
+        h = hidden_dim
+        self.conv1 = GCNConv(self.m, h)
+        self.conv2 = GCNConv(h, 2 * h)
+        self.conv3 = GCNConv(2 * h, 4 * h)
+        self.conv4 = GCNConv(4 * h, 4 * h)
+        self.conv5 = GCNConv(4 * h, 4 * h)
+        self.dropout = nn.Dropout(0.1)
+        self.norm = nn.LayerNorm(4 * h)
+        self.bn1 = nn.BatchNorm1d(h)
+        self.bn2 = nn.BatchNorm1d(2 * h)
+        self.bn3 = nn.BatchNorm1d(4 * h)
+        self.bn4 = nn.BatchNorm1d(4 * h)
+        self.bn5 = nn.BatchNorm1d(4 * h)
+        for conv in [self.conv1, self.conv2, self.conv3, self.conv4, self.conv5]:
+            nn.init.xavier_uniform_(conv.lin.weight)
+
+    def forward(self, x, a_hat):
+        B = x.shape[0]
+        convs = (self.conv1, self.conv2, self.conv3, self.conv4, self.conv5)
+        bns = (self.bn1, self.bn2, self.bn3, self.bn4, self.bn5)
+        for i, (conv, bn) in enumerate(zip(convs, bns)):
+            x = F.leaky_relu(conv(x, a_hat))
+            x = _per_sample_batch_norm(x, bn)
+            if i < 4:
+                x = self.dropout(x)
+        x = self.norm(x)
+        return x.reshape(B, -1)
+
+
+class DLASSO_GNNHyp3_Progressive(nn.Module):
+    """Unfolded D-ADMM whose per-iteration (alpha, tau, rho, eta) come from a GCN hypernetwork
+    (reference gnn_dlasso_models_progressive.py:75-276)."""
+
+    def __init__(self, A, args):
+        super().__init__()
+        self.A = A                                   # plain attribute, as in the reference (:79)
+        _, self.P, self.m, self.n = self.A.shape
+        self.K = args.GHN_iter_num
+        hidden_dim = args.GHyp_hidden
+        self.DADMM_mode = args.DADMM_mode
+        self.encoder = GNNHypernetwork3(P=self.P, m=self.n * 2, hidden_dim=hidden_dim)
+        self.decoder = nn.Sequential(
+            nn.Linear(self.P * 4 * hidden_dim, 4 * hidden_dim),
+            nn.Dropout(0.1),
+            nn.LayerNorm(4 * hidden_dim),
+            nn.LeakyReLU(),
+            nn.Linear(4 * hidden_dim, 2 * hidden_dim),
+            nn.Dropout(0.1),
+            nn.LayerNorm(2 * hidden_dim),
+            nn.LeakyReLU(),
+            nn.Linear(2 * hidden_dim, hidden_dim),
+            nn.Dropout(0.1),
+            nn.LayerNorm(hidden_dim),
+            nn.LeakyReLU(),
+        )
+        if args.DADMM_mode == 'same':
+            self.fc = nn.Linear(hidden_dim, 4)
+        else:
+            self.fc = nn.Linear(hidden_dim, 4 * self.P)
+        nn.init.xavier_uniform_(self.fc.weight, gain=0.1)
+        nn.init.zeros_(self.fc.bias)
+        with torch.no_grad():
+            # fc index = c * P + p (view(B, 4, P)): these land on alpha of agents 0..3 in 'diff'
+            # mode exactly as in the reference (:119-123)
+            self.fc.bias.data[0] = -0.5
+            self.fc.bias.data[1] = -1.0
+            self.fc.bias.data[2] = -0.8
+            self.fc.bias.data[3] = -1.2
+        self.alpha_max = torch.tensor(args.alpha_max)
+        self.tau_max = torch.tensor(args.tau_max)
+        self.rho_max = torch.tensor(args.rho_max)
+        self.eta_max = torch.tensor(args.eta_max)
+        self._op = None
+        self._op_key = None
+        self.last_status = None
+
+    @property
+    def AtA(self):
+        A = self.A
+        return torch.matmul(A.transpose(-1, -2), A)
+
+    def operator(self) -> PreparedOperator:
+        A = self.A
+        key = (A.data_ptr(), A.device, tuple(A.shape), A._version)
+        if self._op is None or self._op_key != key:
+            self._op = PreparedOperator(A)
+            self._op_key = key
+        return self._op
+
+    def hypernetwork(self, AtAy, Atb, a_hat):
+        """(alpha, tau, rho, eta), each [B, H, 1, 1], from the features of one iteration
+        (:165-196)."""
+        B = AtAy.shape[0]
+        h = torch.cat([AtAy, Atb], dim=2)                  # [B, P, 2n]
+        h = self.encoder(h, a_hat)
+        h = self.decoder(h)
+        h = self.fc(h)
+        h = torch.sigmoid(h)
+        h = torch.clamp(h, min=1e-4, max=0.9999)
+        H = 1 if self.DADMM_mode == 'same' else self.P
+        h = h.view(B, 4, H, 1, 1)
+        dev = h.device
+        alpha_k = h[:, 0] * self.alpha_max.to(dev)
+        tau_k = torch.clamp(h[:, 1] * self.tau_max.to(dev), max=0.9999)
+        rho_k = torch.clamp(h[:, 2] * self.rho_max.to(dev), max=0.9999)
+        eta_k = torch.clamp(h[:, 3] * self.eta_max.to(dev), max=0.9999)
+        return alpha_k, tau_k, rho_k, eta_k
+
+    def forward(self, b, graph_list, training_iterations=None, *, inits=None):
+        batch_size = max(len(b), len(graph_list))
+        K = training_iterations if training_iterations is not None else self.K
+        if K <= 0:
+            raise RuntimeError(f"forward needs at least one iteration, got K={K}")
+        if len(graph_list) != batch_size:
+            # the reference's encoder indexes graph_list[i] for every sample (:39)
+            raise IndexError("list index out of range")
+        if b.dim() != 4 or b.shape[1] != self.P or b.shape[2] != self.m:
+            raise RuntimeError(f"b must be [B,{self.P},{self.m},1], got {tuple(b.shape)}")
+        device = b.device
+        bb = b[..., 0]
+        if len(b) != batch_size:
+            bb = bb.expand(batch_size, -1, -1)
+        graphs = ingest(graph_list, self.P, batch_size, device)
+        a_hat = normalized_adjacency(graphs.nbr, self.P)
+        if graphs.shared:
+            a_hat = a_hat[None]
+        if inits is None:
+            shape = (batch_size, self.P, self.n)
+            y0 = torch.empty(shape, device=device).normal_(0.0, 1e-2)
+            U0 = torch.empty(shape, device=device).normal_(0.0, 1e-2)
+            d0 = torch.empty(shape, device=device).normal_(0.0, 1e-2)
+        else:
+            y0, U0, d0 = (x.reshape(batch_size, self.P, self.n) for x in inits)
+        H = 1 if self.DADMM_mode == 'same' else self.P
+        grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        run = GnnRun(self.operator(), bb, graphs, K, H, _lib.VARIANT_GNN, y0, U0, d0, grad)
+        n = self.n
+        Atb = run.Atb[..., :n]
+        y, U, D = run.ys[0], run.U0, run.d0
+        ys = []
+        for k in range(K):
+            AtAy = GramFn.apply(y, run, k)
+            alpha_k, tau_k, rho_k, eta_k = self.hypernetwork(AtAy[..., :n], Atb, a_hat)
+            hyp_k = torch.stack([alpha_k, tau_k, rho_k, eta_k], dim=1).reshape(batch_size, 4, H)
+            y, U, D = StepFn.apply(y, U, D, AtAy, hyp_k.contiguous(), run, k)
+            ys.append(y)
+        self.last_status = run.finish()
+        Y = torch.stack(ys) if run.Y is None else run.Y
+        Y = Y[..., :n].unsqueeze(-1)
+        return Y, (alpha_k, tau_k, rho_k, eta_k)
+
+    # kept for API parity with the reference (:245-276); not used by the HIP forward
+    def compute_sum_neighbors(self, graph_list):
+        g = ingest(graph_list, self.P, len(graph_list), self.A.device)
+        deg = g.deg if not g.shared else g.deg.expand(len(graph_list), -1)
+        return deg.reshape(len(graph_list), self.P, 1, 1).float()
+
+    def compute_Atx(self, x):
+        A = self.A.to(x.device)
+        return torch.einsum('pmn,bpmc->bpnc', A[0], x)

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 3
+#define DADMM_ABI_VERSION 4
 
 enum {
     DADMM_OK = 0,
@@ -170,6 +170,49 @@ int dadmm_backward(const dadmm_dims* d, const void* op, const uint64_t* nbr,
                    const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
                    const float* d0, const float* Y, const float* Grec, const float* Urec,
                    const float* gY, float* dhyp, void* scratch, void* stream);
+
+/* ---- GNN-hypernetwork model: per-iteration entry points --------------------------------------
+ * DLASSO_GNNHyp3_Progressive.forward (gnn_dlasso_models_progressive.py:131-243) evaluates a GNN on
+ * [A^T A y_k, A^T b] between iterations, so its loop runs one iteration per call, the caller
+ * evaluating the hypernetwork in between:
+ *   dadmm_gnn_begin                 once: zero the flags, k = 0 guards, Atb = A^T b
+ *   for k in 0..K-1:
+ *     dadmm_gnn_gram(k)             AtAy_k = A^T (A y_k)        (:158-162)
+ *     [caller]                      hyp_k [B][4][H] from the hypernetwork (:165-196)
+ *     dadmm_gnn_step(k)             gradient, clamps, y/delta/U updates, guards (:205-237)
+ *   dadmm_gnn_finish                Y[K-1] guard fix-up, status bits
+ * Y storage: `yptr` is a DEVICE array of K+1 float pointers: y0, then y_1 .. y_K, each [B][P][n]
+ * (y_{k+1} = the reference's Y[k]; they may be the K slices of one [K][B][P][n] tensor). The
+ * guards are the reference's batch-global NaN/Inf resets (:150-156, :216-218, :235-237), decided
+ * on the device through `flags` (dadmm_gnn_flag_bytes(K) bytes): no host synchronisation.
+ * Graph operands are the stepwise path's visit lists and degrees; H = dims.hyp_rows (P for
+ * 'diff', 1 for 'same'); dims.variant selects the clamps (1 for this model). Shapes: P <= 64,
+ * m <= 64, n % 4 == 0. */
+size_t dadmm_gnn_flag_bytes(int32_t K);
+int dadmm_gnn_begin(const dadmm_dims* d, const void* op, const float* b, const float* y0,
+                    const float* U0, float* Atb, int32_t* flags, void* stream);
+/* out = A^T (A y_k) with y_k resolved through the guards (x == NULL), or out = A^T (A x) for an
+ * explicit x [B][P][n] (the adjoint of AtAy; flags / yptr unused then). */
+int dadmm_gnn_gram(const dadmm_dims* d, const void* op, int32_t k, float* const* yptr,
+                   const int32_t* flags, const float* x, float* out, void* stream);
+/* One iteration: reads y_k (resolved), U_k (U, reset by the guard), delta_k (D), AtAy_k, Atb and
+ * hyp_k [B][4][H]; writes y_{k+1} to yptr[k+1], U_{k+1} to U_next, delta_{k+1} to D_next.
+ * G: [B][P][n] scratch. */
+int dadmm_gnn_step(const dadmm_dims* d, int32_t k, const int32_t* visit_ptr, const uint8_t* visit_q,
+                   const float* deg, const float* hyp_k, float* const* yptr, const float* AtAy,
+                   const float* Atb, const float* U, const float* D, float* U_next, float* D_next,
+                   float* G, int32_t* flags, void* stream);
+int dadmm_gnn_finish(const dadmm_dims* d, float* const* yptr, int32_t* flags, int32_t* status,
+                     void* stream);
+/* The adjoint of one dadmm_gnn_step (no guard fired): from dL/d(y_{k+1}, U_{k+1}, delta_{k+1})
+ * (nullable = zero) to dL/d(y_k, U_k, delta_k, AtAy_k) [B][P][n] and dL/dhyp_k [B][4][H]
+ * (dL/dy_k excludes the path through AtAy_k: add dadmm_gnn_gram of dL/dAtAy_k). */
+int dadmm_gnn_step_backward(const dadmm_dims* d, int32_t k, const int32_t* visit_ptr,
+                            const uint8_t* visit_q, const float* deg, const float* hyp_k,
+                            const float* y_k, const float* AtAy, const float* Atb, const float* U,
+                            const float* D, const float* gy1, const float* gU1, const float* gd1,
+                            float* gy, float* gU, float* gd, float* gAtAy, float* ghyp,
+                            void* stream);
 
 #ifdef __cplusplus
 }

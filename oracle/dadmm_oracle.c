@@ -76,7 +76,8 @@ static int forward_f32_impl(int B, int P, int m, int n, int K, int variant, int 
                             const float* A, const float* b, const int32_t* nbr_ptr,
                             const int32_t* nbr_idx, const float* deg, const float* hyp,
                             const float* y0, const float* U0, const float* d0, float* Y,
-                            float* U_out, int32_t* status, float* Grec, float* Urec) {
+                            float* U_out, int32_t* status, float* Grec, float* Urec,
+                            int gram_mode) {
     if (B < 0 || P < 1 || m < 1 || n < 1 || K < 0 || (H != 1 && H != P)) return -1;
     const size_t S = (size_t)B * P * n;
     float* y = (float*)malloc(S * sizeof(float));
@@ -117,9 +118,10 @@ static int forward_f32_impl(int B, int P, int m, int n, int K, int variant, int 
                 const float* Ap = A + (size_t)p * m * n;
                 const float* yp = y + ((size_t)s * P + p) * n;
                 const float* bp = b + ((size_t)s * P + p) * m;
-                /* GEMM1: R = A_p y_p - b_p, one fma chain per row from -b */
+                /* GEMM1: R = A_p y_p - b_p, one fma chain per row from -b
+                 * (gram_mode: R = A_p y_p from +0, b enters through Atb below) */
                 for (int i = 0; i < m; ++i) {
-                    float acc = -bp[i];
+                    float acc = gram_mode ? 0.0f : -bp[i];
                     for (int idx = 0; idx < npad; ++idx) {
                         const int c = perm16(idx);
                         if (c < n) acc = fmaf(Ap[(size_t)i * n + c], yp[c], acc);
@@ -135,6 +137,16 @@ static int forward_f32_impl(int B, int P, int m, int n, int K, int variant, int 
                         if (i < m) g = fmaf(Ap[(size_t)i * n + c], R[i], g);
                     }
                     const size_t e = ((size_t)s * P + p) * n + c;
+                    if (gram_mode) {
+                        /* GNN model (gnn_dlasso_models_progressive.py:205-209): AtAy - Atb with
+                         * Atb = A_p^T b_p as its own chain from +0 */
+                        float atb = 0.0f;
+                        for (int idx = 0; idx < mpad; ++idx) {
+                            const int i = perm16(idx);
+                            if (i < m) atb = fmaf(Ap[(size_t)i * n + c], bp[i], atb);
+                        }
+                        g = g - atb;
+                    }
                     /* :73-77 left to right */
                     float t = g + signf_t(y[e]) * h4[1];
                     t = t + U[e] * dg;
@@ -208,7 +220,7 @@ int oracle_forward_f32(int B, int P, int m, int n, int K, int variant, int hyp_m
                        const float* y0, const float* U0, const float* d0, float* Y, float* U_out,
                        int32_t* status) {
     return forward_f32_impl(B, P, m, n, K, variant, hyp_mode, H, A, b, nbr_ptr, nbr_idx, deg, hyp,
-                            y0, U0, d0, Y, U_out, status, NULL, NULL);
+                            y0, U0, d0, Y, U_out, status, NULL, NULL, 0);
 }
 
 /* oracle_forward_f32 that also records the adjoint's trajectory (Grec, Urec: [K][B][P][n]). */
@@ -218,7 +230,19 @@ int oracle_forward_f32_rec(int B, int P, int m, int n, int K, int variant, int h
                            const float* y0, const float* U0, const float* d0, float* Y,
                            float* U_out, int32_t* status, float* Grec, float* Urec) {
     return forward_f32_impl(B, P, m, n, K, variant, hyp_mode, H, A, b, nbr_ptr, nbr_idx, deg, hyp,
-                            y0, U0, d0, Y, U_out, status, Grec, Urec);
+                            y0, U0, d0, Y, U_out, status, Grec, Urec, 0);
+}
+
+/* The GNN model's recurrence in the order of the per-iteration HIP path (dadmm_gnn.hip): gradient
+ * ((((AtAy - Atb) + sign*tau) + U*deg) + delta*rho) with AtAy = A^T (A y) and Atb = A^T b as
+ * separate fma chains. Usually hyp_mode 1 (the hypernetwork's per-sample [K][B][4][H]). */
+int oracle_forward_f32_gram(int B, int P, int m, int n, int K, int variant, int hyp_mode, int H,
+                            const float* A, const float* b, const int32_t* nbr_ptr,
+                            const int32_t* nbr_idx, const float* deg, const float* hyp,
+                            const float* y0, const float* U0, const float* d0, float* Y,
+                            float* U_out, int32_t* status) {
+    return forward_f32_impl(B, P, m, n, K, variant, hyp_mode, H, A, b, nbr_ptr, nbr_idx, deg, hyp,
+                            y0, U0, d0, Y, U_out, status, NULL, NULL, 1);
 }
 
 /* ------------------------------------------------------------------------------------------ */

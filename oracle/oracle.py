@@ -22,7 +22,7 @@ import numpy as np
 
 __all__ = [
     "lib", "hyp_table", "graph_arrays", "forward_f32", "forward_f64", "forward_np64",
-    "forward_f32_rec", "laplacians", "backward_np64",
+    "forward_f32_rec", "forward_f32_gram", "laplacians", "backward_np64",
     "compute_loss", "make_problem", "load_fixture_tensor", "er_graph", "connected_er_graph",
 ]
 
@@ -41,7 +41,7 @@ def lib() -> ctypes.CDLL:
         L = ctypes.CDLL(path)
         fp = ctypes.c_void_p
         i = ctypes.c_int
-        for name in ("oracle_forward_f32", "oracle_forward_f64"):
+        for name in ("oracle_forward_f32", "oracle_forward_f64", "oracle_forward_f32_gram"):
             f = getattr(L, name)
             f.restype = ctypes.c_int
             f.argtypes = [i, i, i, i, i, i, i, i] + [fp] * 12
@@ -145,6 +145,14 @@ def forward_f32_rec(A, b, graph_list, hyp, y0, U0, d0, variant=0, hyp_mode=0):
     Y, U, st = _run(lib().oracle_forward_f32_rec, np.float32, A, b, graph_list, hyp, y0, U0, d0,
                     variant, hyp_mode, rec)
     return Y, U, st, rec[0], rec[1]
+
+
+def forward_f32_gram(A, b, graph_list, hyp, y0, U0, d0, variant=1, hyp_mode=1):
+    """The GNN model's recurrence (gnn_dlasso_models_progressive.py:148-240) in the exact order of
+    the per-iteration HIP path: AtAy and Atb as separate chains, then AtAy - Atb. hyp_mode 1:
+    hyp [K][B][4][H] (the hypernetwork output of every iteration)."""
+    return _run(lib().oracle_forward_f32_gram, np.float32, A, b, graph_list, hyp, y0, U0, d0,
+                variant, hyp_mode)
 
 
 def forward_f64(A, b, graph_list, hyp, y0, U0, d0, variant=0, hyp_mode=0):

@@ -145,3 +145,37 @@ def _delta_autograd(graph_list, y, P):
                 acc[q] = acc[q] - diff
         rows.append(torch.stack(acc))
     return torch.stack(rows)
+
+
+def gnn_forward_autograd(model, A, b, graph_list, y0, U0, d0, K, a_hat, dtype=torch.float64):
+    """DLASSO_GNNHyp3_Progressive.forward's loop (gnn_dlasso_models_progressive.py:148-240) in
+    torch eager ops on the CPU, keeping the autograd graph (no guards: finite inputs only).
+    ``model`` supplies the hypernetwork (its ``hypernetwork(AtAy, Atb, a_hat)``), already in
+    ``dtype`` on the CPU. Returns (Y [K,B,P,n], (alpha, tau, rho, eta) of the last iteration)."""
+    A = torch.as_tensor(np.asarray(A), dtype=dtype)
+    if A.dim() == 3:
+        A = A[None]
+    _, P, m, n = A.shape
+    B = y0.shape[0]
+    b = torch.as_tensor(np.asarray(b), dtype=dtype).reshape(B, P, m, 1)
+    AtA = torch.stack([A[0, p].T @ A[0, p] for p in range(P)])[None]
+    Atb = _atx(A, b)
+    deg = torch.zeros((B, P, 1, 1), dtype=dtype)
+    for s in range(B):
+        for p in range(P):
+            deg[s, p] = len(list(graph_list[s].neighbors(p)))
+    y = torch.as_tensor(np.asarray(y0), dtype=dtype).reshape(B, P, n, 1)
+    U = torch.as_tensor(np.asarray(U0), dtype=dtype).reshape(B, P, n, 1)
+    d = torch.as_tensor(np.asarray(d0), dtype=dtype).reshape(B, P, n, 1)
+    Y = []
+    for k in range(K):
+        AtAy = torch.stack([AtA[0, p] @ y[:, p] for p in range(P)], dim=1)
+        al, ta, rh, et = model.hypernetwork(AtAy[..., 0], Atb[..., 0], a_hat)
+        grad = AtAy - Atb + y.sign() * ta + U * deg + d * rh
+        grad = torch.clamp(grad, -10.0, 10.0)
+        yn = torch.clamp(y - al * grad, -100.0, 100.0)
+        d = torch.clamp(_delta_autograd(graph_list, yn, P), -20.0, 20.0)
+        U = torch.clamp(U + d * et, -100.0, 100.0)
+        y = yn
+        Y.append(y)
+    return torch.stack(Y)[..., 0], (al, ta, rh, et)

@@ -1,0 +1,183 @@
+"""GPU: the GNN-hypernetwork model (DLASSO_GNNHyp3_Progressive) on the per-iteration HIP path.
+
+Bar:
+  * the D-ADMM recurrence, given the hyper-parameters the hypernetwork produced in every
+    iteration, is BIT-EXACT against oracle.forward_f32_gram (the reference's GNN-model loop,
+    gnn_dlasso_models_progressive.py:148-240, in the kernels' operation order), guards included;
+  * the hypernetwork (torch on the GPU, fp32) matches the numpy fp64 edge-list restatement of
+    GCNConv & co. (oracle/gnn_np.py) within 1e-4 relative — parity unpinned against
+    torch_geometric itself (absent);
+  * gradients of every parameter through loss.backward() (HIP adjoint of each iteration + gram
+    adjoint + torch autograd of the hypernetwork) match torch autograd of a CPU fp64 replay of the
+    reference's loop (oracle/ref_torch.gnn_forward_autograd) within 2e-3 of each parameter's
+    largest gradient, at a depth (K = 3) where fp32 and fp64 trajectories have not drifted apart.
+"""
+import argparse
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from oracle import gnn_np, ref_torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _args(K, mode="diff", hidden=16, alpha_max=0.1):
+    return argparse.Namespace(GHN_iter_num=K, GHyp_hidden=hidden, DADMM_mode=mode,
+                              alpha_max=alpha_max, tau_max=0.99, rho_max=0.99, eta_max=0.99)
+
+
+def _t(x, dev):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+def _setup(dev, P, m, n, B, K, mode, per_sample, seed=0, hidden=16):
+    import gnn_dlasso_models_progressive as G
+    A, b, x = O.make_problem(P, m, n, B, seed=seed + 5)
+    torch.manual_seed(seed)
+    model = G.DLASSO_GNNHyp3_Progressive(_t(A, dev)[None], _args(K, mode, hidden)).to(dev)
+    if per_sample:
+        graphs = [O.connected_er_graph(P, 0.5, seed=seed * 100 + s) for s in range(B)]
+    else:
+        graphs = [O.er_graph(P, 0.5, seed=seed + 7)] * B
+    rng = np.random.default_rng(seed)
+    y0, U0, d0 = (1e-2 * rng.standard_normal((3, B, P, n))).astype(np.float32)
+    return model, A, b, x, graphs, (y0, U0, d0)
+
+
+def _recording(model):
+    """Wrap model.hypernetwork to record (features, hyp) of every iteration."""
+    rec = []
+    orig = model.hypernetwork
+
+    def hook(AtAy, Atb, a_hat):
+        out = orig(AtAy, Atb, a_hat)
+        rec.append((AtAy.detach().clone(), Atb.detach().clone(), [o.detach().clone() for o in out]))
+        return out
+
+    model.hypernetwork = hook
+    return rec
+
+
+def _hyp_table(rec, B, H):
+    # [K][B][4][H] from each iteration's (alpha, tau, rho, eta) [B, H, 1, 1]
+    return np.stack([torch.stack([o[..., 0, 0] for o in r[2]], dim=1).cpu().numpy()
+                     for r in rec]).reshape(len(rec), B, 4, H).astype(np.float32)
+
+
+@pytest.mark.parametrize("mode,per_sample", [("diff", True), ("same", False), ("diff", False)])
+def test_recurrence_bit_exact_given_hypernetwork_outputs(cuda, mode, per_sample):
+    P, m, n, B, K = 5, 32, 64, 24, 6
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, mode, per_sample)
+    model.eval()
+    rec = _recording(model)
+    with torch.no_grad():
+        Y, hyp = model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in inits))
+    H = 1 if mode == "same" else P
+    assert Y.shape == (K, B, P, n, 1) and hyp[0].shape == (B, H, 1, 1)
+    assert int(model.last_status.item()) == 0
+    table = _hyp_table(rec, B, H)
+    Yo, _, st = O.forward_f32_gram(A, b, graphs, table, *inits, variant=1, hyp_mode=1)
+    assert st == 0
+    assert np.array_equal(Y[..., 0].cpu().numpy(), Yo), np.abs(Y[..., 0].cpu().numpy() - Yo).max()
+
+
+def test_hypernetwork_matches_numpy_restatement(cuda):
+    P, m, n, B, K = 5, 32, 64, 12, 2
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", True)
+    model.eval()
+    rec = _recording(model)
+    with torch.no_grad():
+        model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in inits))
+    sd = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in model.state_dict().items()}
+    maxima = tuple(float(np.float32(v)) for v in (0.1, 0.99, 0.99, 0.99))
+    for AtAy, Atb, out in rec:
+        feats = torch.cat([AtAy, Atb], dim=2).cpu().numpy().astype(np.float64)
+        want = gnn_np.hypernetwork(sd, feats, graphs, maxima, False)
+        for g, w in zip(out, want):
+            g = g[..., 0, 0].cpu().numpy()
+            np.testing.assert_allclose(g, w, rtol=1e-4, atol=1e-4 * np.abs(w).max())
+
+
+def test_features_are_the_reference_gram_and_atb(cuda):
+    """AtAy_0 = AtA @ y0 and Atb = compute_Atx(b) (fp64 check, fp32 tolerance)."""
+    P, m, n, B, K = 4, 24, 48, 10, 1
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", False)
+    model.eval()
+    rec = _recording(model)
+    with torch.no_grad():
+        model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in inits))
+    AtAy, Atb, _ = rec[0]
+    A64 = A.astype(np.float64)
+    want_g = np.einsum("pri,prj,bpj->bpi", A64, A64, inits[0].astype(np.float64))
+    want_b = np.einsum("pri,bpr->bpi", A64, b.astype(np.float64))
+    np.testing.assert_allclose(AtAy.cpu().numpy(), want_g, rtol=1e-4, atol=1e-4 * np.abs(want_g).max())
+    np.testing.assert_allclose(Atb.cpu().numpy(), want_b, rtol=1e-4, atol=1e-4 * np.abs(want_b).max())
+
+
+@pytest.mark.parametrize("mode", ["diff", "same"])
+def test_backward_matches_cpu_autograd(cuda, mode):
+    import gnn_dlasso_models_progressive as G
+    from dadmm_hip.graph import ingest
+    P, m, n, B, K = 4, 16, 32, 8, 3
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, mode, True, hidden=8)
+    model.eval()
+    gY = torch.randn(K, B, P, n, 1, generator=torch.Generator().manual_seed(2))
+    Y, _ = model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in inits))
+    (Y * gY.to(cuda)).sum().backward()
+    got = {k: p.grad.detach().cpu().numpy() for k, p in model.named_parameters()}
+
+    cpu = G.DLASSO_GNNHyp3_Progressive(torch.from_numpy(A)[None], _args(K, mode, 8)).double()
+    cpu.load_state_dict({k: v.cpu() for k, v in model.state_dict().items()})
+    cpu.eval()
+    a_hat = G.normalized_adjacency(ingest(graphs, P, B, "cpu").nbr, P, torch.float64)
+    Yc, _ = ref_torch.gnn_forward_autograd(cpu, A, b, graphs, *inits, K=K, a_hat=a_hat)
+    np.testing.assert_allclose(Y[..., 0].detach().cpu().numpy(), Yc.detach().numpy(), rtol=1e-4,
+                               atol=1e-4)
+    (Yc * gY[..., 0].double()).sum().backward()
+    for k, p in cpu.named_parameters():
+        w = p.grad.numpy()
+        scale = np.abs(w).max()
+        assert scale > 0, k
+        err = np.abs(got[k] - w).max() / scale
+        assert err <= 2e-3, (k, err)
+
+
+def test_guard_on_nonfinite_y0_bit_exact(cuda):
+    P, m, n, B, K = 4, 16, 32, 8, 4
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", True)
+    model.eval()
+    y0, U0, d0 = inits
+    y0 = y0.copy()
+    y0[3, 2, 7] = np.inf
+    rec = _recording(model)
+    with torch.no_grad():
+        Y, _ = model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in (y0, U0, d0)))
+    st = int(model.last_status.item())
+    table = _hyp_table(rec, B, P)
+    Yo, _, sto = O.forward_f32_gram(A, b, graphs, table, y0, U0, d0, variant=1, hyp_mode=1)
+    assert st == sto and st & 1
+    assert np.array_equal(Y[..., 0].cpu().numpy(), Yo)
+
+
+def test_train_mode_step_updates_bn_and_trains(cuda):
+    """train(): dropout on, per-sample BatchNorm statistics, running stats updated B*K times per
+    forward; loss.backward() + AdamW step run (progressive driver's loop, :196-214)."""
+    import gnn_dlasso_utils
+    P, m, n, B, K = 5, 32, 64, 16, 4
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", True)
+    model.train()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    nbt0 = int(model.encoder.bn1.num_batches_tracked)
+    Y, hyp = model(_t(b, cuda)[..., None], graphs, training_iterations=K + 2)
+    assert Y.shape[0] == K + 2                  # training_iterations is not capped by self.K
+    assert int(model.encoder.bn1.num_batches_tracked) == nbt0 + B * (K + 2)
+    _, loss_final = gnn_dlasso_utils.compute_loss(Y, _t(x, cuda)[..., None])
+    opt.zero_grad()
+    loss_final.backward()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), 100.0)
+    grads = [p.grad for p in model.parameters() if p.grad is not None]
+    assert grads and all(torch.isfinite(g).all() for g in grads)
+    opt.step()
