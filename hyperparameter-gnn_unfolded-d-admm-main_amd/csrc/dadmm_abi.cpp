@@ -382,6 +382,64 @@ int dadmm_gnn_step_backward(const dadmm_dims* d, int32_t k, const int32_t* visit
     return hip_rc(dadmm::gnn_launch_step_backward(a, k, g, (hipStream_t)stream), "step backward launch");
 }
 
+namespace {
+// torch's calc_execution_policy for its Philox distribution kernels on the current device
+int normal_policy(int64_t numel, int64_t* threads, uint64_t* step) {
+    int dev = 0, sms = 0, tpm = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&sms, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&tpm, hipDeviceAttributeMaxThreadsPerMultiProcessor, dev) != hipSuccess)
+        return -1;
+    const uint64_t block = 256, unroll = 4;
+    uint64_t grid = ((uint64_t)numel + block - 1) / block;
+    const uint64_t cap = (uint64_t)sms * ((uint64_t)tpm / block);
+    if (grid > cap) grid = cap;
+    if (grid < 1) grid = 1;
+    *threads = (int64_t)(grid * block);
+    *step = (((uint64_t)numel - 1) / (block * grid * unroll) + 1) * 4;   // already a multiple of 4
+    return 0;
+}
+}  // namespace
+
+uint64_t dadmm_normal_offset_step(int64_t numel) {
+    int64_t threads = 0;
+    uint64_t step = 0;
+    if (numel <= 0 || normal_policy(numel, &threads, &step) != 0) return 0;
+    return step;
+}
+
+int dadmm_prologue(uint64_t seed, uint64_t offset, int64_t numel, int32_t n, int32_t n_store,
+                   float mean, float stddev, float* y0, float* U0, float* d0, int32_t* zero,
+                   int64_t nzero, void* stream) {
+    if (numel < 0 || nzero < 0) return fail(DADMM_EINVAL, "negative size");
+    if (nzero > 0 && zero == nullptr) return fail(DADMM_EINVAL, "zero is NULL");
+    dadmm::PrologueArgs a{};
+    if (numel > 0) {
+        if (!y0 || !U0 || !d0) return fail(DADMM_EINVAL, "y0/U0/d0 is NULL");
+        if (n < 1 || n_store < n || numel % n != 0)
+            return fail(DADMM_EINVAL, "bad row length n=%d n_store=%d for numel=%lld", n, n_store,
+                        (long long)numel);
+        if (normal_policy(numel, &a.threads, &a.offset_step) != 0)
+            return fail(DADMM_EHIP, "device attribute query failed");
+        if ((offset & 3u) != 0) return fail(DADMM_EINVAL, "Philox offset must be a multiple of 4");
+    }
+    a.seed = seed;
+    a.offset = offset;
+    a.numel = numel;
+    a.n = n;
+    a.n_store = n_store;
+    a.mean = mean;
+    a.stddev = stddev;
+    a.y0 = y0;
+    a.U0 = U0;
+    a.d0 = d0;
+    a.zero = zero;
+    a.nzero = nzero;
+    hipError_t e = dadmm::launch_prologue(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "prologue launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d) {
@@ -397,8 +455,9 @@ int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
                            int32_t gate, void* scratch, void* stream) {
     int rc = check_dims(d);
     if (rc) return rc;
-    if (gate != 0 && gate != 1) return fail(DADMM_EINVAL, "gate must be 0 or 1");
-    if (gate && status == nullptr) return fail(DADMM_EINVAL, "gate = 1 needs the status word");
+    if (gate & ~(DADMM_GATE_ON | DADMM_FLAGS_ZEROED)) return fail(DADMM_EINVAL, "unknown gate bits %d", gate);
+    if ((gate & DADMM_GATE_ON) && status == nullptr)
+        return fail(DADMM_EINVAL, "DADMM_GATE_ON needs the status word");
     if (d->B == 0 || d->K == 0) return ok();
     if (!op || !b || !visit_ptr || !visit_q || !deg || !hyp || !y0 || !U0 || !d0 || !Y || !scratch)
         return fail(DADMM_EINVAL, "a required pointer is NULL");
@@ -446,7 +505,8 @@ int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
     a.hyp_rows = d->hyp_rows;
     a.variant = d->variant;
     a.graph_shared = d->graph_shared;
-    hipError_t e = dadmm::launch_stepwise(a, gate, (hipStream_t)stream);
+    hipError_t e = dadmm::launch_stepwise(a, gate & DADMM_GATE_ON, (gate & DADMM_FLAGS_ZEROED) != 0,
+                                          (hipStream_t)stream);
     if (e != hipSuccess) return fail(DADMM_EHIP, "stepwise launch: %s", hipGetErrorString(e));
     return ok();
 }

@@ -111,6 +111,21 @@ hipError_t gnn_launch_finish(const GnnArgs& a, hipStream_t st);
 hipError_t gnn_launch_step_backward(const GnnArgs& a, int k, const GnnGrads& gg, hipStream_t st);
 size_t gnn_gram_lds(int n_pad);
 
+// ---- forward prologue (dadmm_rng.hip) -----------------------------------------------------------
+struct PrologueArgs {
+    uint64_t seed, offset, offset_step;   // torch Philox state; per-tensor offset increment
+    int64_t numel;                        // B*P*n per tensor (0: no draw)
+    int64_t threads;                      // torch's 256 * grid virtual threads
+    int64_t n, n_store;                   // row length drawn / stored
+    float mean, stddev;
+    float* y0;
+    float* U0;
+    float* d0;
+    int32_t* zero;                        // words zeroed by the same launch
+    int64_t nzero;
+};
+hipError_t launch_prologue(const PrologueArgs& a, hipStream_t stream);
+
 // Operator preparation kernel launcher (dadmm_prepare.hip).
 hipError_t launch_prepare(const float* A, float* Apad, float* Atpad, int P, int m, int n,
                           int n_pad, hipStream_t stream);
@@ -150,7 +165,7 @@ struct StepArgs {
 
 size_t stepwise_flag_bytes(int K);
 // gate = 1: one persistent launch that runs only if *status != 0 when it starts
-hipError_t launch_stepwise(const StepArgs& a, int gate, hipStream_t stream);
+hipError_t launch_stepwise(const StepArgs& a, int gate, bool flags_zeroed, hipStream_t stream);
 
 inline int fused_nt(int n) {
     const int nt = (n + 63) / 64;

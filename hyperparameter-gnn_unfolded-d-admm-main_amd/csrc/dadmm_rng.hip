@@ -1,0 +1,96 @@
+// dadmm_rng.hip — the forward's prologue: the reference's random inits and the per-forward
+// zeroing of the guard words, in ONE launch.
+//
+// The reference draws y_k, U_k, delta = torch.randn((B, P, n, 1)) * 1e-2, in that order
+// (unfolded_DLASSO.py:49-51). On a ROCm device that is three calls of torch's Philox normal
+// kernel (ATen/native/hip/DistributionTemplates.h, distribution_elementwise_grid_stride_kernel
+// with unroll 4): a grid of G blocks of 256 threads; virtual thread idx runs hiprand_init(seed,
+// subsequence = idx, offset) and, for it = 0, 1, ..., writes hiprand_normal4's four values to
+// elements idx + T (4 it + ii) (T = 256 G); each call advances the generator's offset by
+// 4 ceil(numel / 4T). This kernel replays exactly that mapping for all three tensors at once (one
+// real thread per (tensor, virtual idx)), so its output is bit-identical to
+//   torch.randn(shape) * 1e-2  ==  torch.empty(shape).normal_(0, 1e-2)
+// (tests/test_gpu_parity.py::test_prologue_draws_match_torch), and zeroes `nzero` int32 words
+// (the status word and the stepwise guard flags) — replacing 3 RNG launches, 2 fills and a memset.
+// Outputs may use a padded row length n_store >= n (padding columns are left untouched).
+
+#include <hip/hip_runtime.h>
+#include <hiprand/hiprand_kernel.h>
+#include <stdint.h>
+
+#include "dadmm_internal.h"
+
+namespace dadmm {
+namespace {
+
+// hiprand_normal4 (rocrand box_muller on the four Philox words) evaluated exactly as torch's own
+// build of it rounds — established on the device by tests/hip/probe_rng.hip + scripts/rng_probe.py
+// over 2M draws: the uniforms u, v contracted to one fma each, then logf, a correctly rounded
+// sqrtf, __sincosf and two separately rounded products (this file: -ffp-contract=off).
+__device__ __forceinline__ float2 box_muller(unsigned x, unsigned y) {
+    const float u = __builtin_fmaf((float)x, 2.3283064e-10f, 2.3283064e-10f);     // ROCRAND_2POW32_INV
+    const float v = __builtin_fmaf((float)y, 1.46291807e-09f, 1.46291807e-09f);   // ..._INV_2PI
+    const float s = sqrtf(-2.0f * logf(u));
+    float sn, cs;
+    __sincosf(v, &sn, &cs);
+    return make_float2(sn * s, cs * s);
+}
+
+__device__ __forceinline__ float4 normal4(hiprandStatePhilox4_32_10_t* st) {
+    const uint4 r = hiprand4(st);
+    const float2 a = box_muller(r.x, r.y), b = box_muller(r.z, r.w);
+    return make_float4(a.x, a.y, b.x, b.y);
+}
+
+// 32-bit index arithmetic (numel < 2^31 is checked by the launcher): the 64-bit divisions of a
+// straightforward port cost more than the Philox rounds themselves.
+template <bool PADDED>
+__global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
+    const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+    if (gid < (uint32_t)a.nzero) a.zero[gid] = 0;
+    if (a.numel == 0) return;
+    const uint32_t T = (uint32_t)a.threads;       // torch's 256 G virtual threads per tensor
+    const uint32_t t = gid / T;                   // tensor 0, 1, 2 = y0, U0, delta0
+    if (t >= 3) return;
+    const uint32_t idx = gid - t * T;
+    float* out = t == 0 ? a.y0 : (t == 1 ? a.U0 : a.d0);
+    hiprandStatePhilox4_32_10_t st;
+    hiprand_init(a.seed, (unsigned long long)idx, a.offset + (uint64_t)t * a.offset_step, &st);
+    const uint32_t numel = (uint32_t)a.numel, n = (uint32_t)a.n, ns = (uint32_t)a.n_store;
+    const uint32_t iters = (numel - 1) / (T * 4) + 1;
+    uint32_t li = idx;
+    for (uint32_t it = 0; it < iters; ++it) {
+        const float4 r = normal4(&st);
+        const float v[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii, li += T) {
+            if (li < numel) {
+                uint32_t o = li;
+                if (PADDED) {
+                    const uint32_t row = li / n;
+                    o = row * ns + (li - row * n);
+                }
+                // transformation::normal (val * std + mean), contracted as torch's build does
+                out[o] = __builtin_fmaf(v[ii], a.stddev, a.mean);
+            }
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_prologue(const PrologueArgs& a, hipStream_t stream) {
+    int64_t work = a.numel > 0 ? 3 * a.threads : 0;
+    if (work < a.nzero) work = a.nzero;
+    if (work == 0) return hipSuccess;
+    if (a.numel >= ((int64_t)1 << 31) || work >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    if (a.n_store != a.n)
+        hipLaunchKernelGGL(prologue_kernel<true>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
+                           stream, a);
+    else
+        hipLaunchKernelGGL(prologue_kernel<false>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
+                           stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace dadmm

@@ -375,9 +375,10 @@ size_t update_lds_bytes(int P) { return 4 * (size_t)SW_WAVES * P * 64; }
 
 size_t stepwise_flag_bytes(int K) { return (size_t)SW_FLAG_WORDS(K) * 4; }
 
-hipError_t launch_stepwise(const StepArgs& a, int gate, hipStream_t stream) {
-    hipError_t e = hipMemsetAsync(a.flags, 0, stepwise_flag_bytes(a.K), stream);
-    if (e != hipSuccess) return e;
+hipError_t launch_stepwise(const StepArgs& a, int gate, bool flags_zeroed, hipStream_t stream) {
+    hipError_t e = hipSuccess;
+    if (!flags_zeroed && (e = hipMemsetAsync(a.flags, 0, stepwise_flag_bytes(a.K), stream)) != hipSuccess)
+        return e;
     const size_t lds_g = grad_lds_bytes(a.n_pad), lds_u = update_lds_bytes(a.P);
     const size_t lds = lds_g > lds_u ? lds_g : lds_u;
     if (lds > 160 * 1024) return hipErrorInvalidConfiguration;

@@ -11,11 +11,12 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
 STATUS_BARRIER_TIMEOUT = 0x100
+GATE_ON, FLAGS_ZEROED = 1, 2
 
 # every symbol include/dadmm.h declares
 EXPORTED_SYMBOLS = (
@@ -35,6 +36,8 @@ EXPORTED_SYMBOLS = (
     "dadmm_gnn_step",
     "dadmm_gnn_finish",
     "dadmm_gnn_step_backward",
+    "dadmm_normal_offset_step",
+    "dadmm_prologue",
 )
 
 
@@ -91,6 +94,11 @@ def load() -> ctypes.CDLL:
     L.dadmm_backward.restype = ctypes.c_int
     L.dadmm_backward.argtypes = [ctypes.POINTER(Dims)] + [vp] * 14
     D = ctypes.POINTER(Dims)
+    u64, i64, f32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_float
+    L.dadmm_normal_offset_step.restype = u64
+    L.dadmm_normal_offset_step.argtypes = [i64]
+    L.dadmm_prologue.restype = ctypes.c_int
+    L.dadmm_prologue.argtypes = [u64, u64, i64, i32, i32, f32, f32, vp, vp, vp, vp, i64, vp]
     L.dadmm_gnn_flag_bytes.restype = ctypes.c_size_t
     L.dadmm_gnn_flag_bytes.argtypes = [i32]
     for name, args in (("dadmm_gnn_begin", [D] + [vp] * 7),

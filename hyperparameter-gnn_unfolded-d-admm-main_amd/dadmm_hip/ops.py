@@ -73,8 +73,38 @@ def _pad_n(t, n_store):
     return torch.nn.functional.pad(t, (0, n_store - t.shape[-1]))
 
 
+def _sw_flag_bytes(K):
+    return 4 * (8 + 4 * K)   # SW_FLAG_WORDS(K) of csrc/dadmm_internal.h
+
+
+def draw_inits(shape, device, n_store=None, zero=None, nzero=0):
+    """(y0, U0, d0) = torch.randn(shape) * 1e-2 x 3 in that order (unfolded_DLASSO.py:49-51),
+    bit-identical to torch's own draws, from the device's default generator (advanced exactly as
+    the three torch calls would), in ONE launch that also zeroes ``nzero`` int32 words at
+    ``zero``. shape = (B, P, n); outputs are [B, P, n_store] (padding columns zero)."""
+    B, P, n = shape
+    ns = n if n_store is None else n_store
+    L = _lib.load()
+    alloc = torch.zeros if ns != n else torch.empty
+    y0, U0, d0 = (alloc((B, P, ns), dtype=torch.float32, device=device) for _ in range(3))
+    numel = B * P * n
+    gen = torch.cuda.default_generators[device.index if device.index is not None
+                                        else torch.cuda.current_device()]
+    seed, off = gen.initial_seed(), gen.get_offset()
+    if numel > 0:
+        step = L.dadmm_normal_offset_step(numel)
+        if step == 0:
+            _lib.check("dadmm_normal_offset_step", _lib.DADMM_EHIP)
+        gen.set_offset(off + 3 * step)
+    with torch.cuda.device(device):
+        _lib.check("dadmm_prologue", L.dadmm_prologue(
+            seed, off, numel, n, ns, 0.0, 1e-2, _ptr(y0), _ptr(U0), _ptr(d0),
+            _ptr(zero), nzero, _stream(device)))
+    return y0, U0, d0
+
+
 def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: torch.Tensor,
-                y0: torch.Tensor, U0: torch.Tensor, d0: torch.Tensor, *,
+                y0: torch.Tensor = None, U0: torch.Tensor = None, d0: torch.Tensor = None, *,
                 variant: int = _lib.VARIANT_UNFOLDED, want_U: bool = False, path: str = "auto",
                 record: bool = False):
     """The K-step forward with the reference's NaN/Inf guards, enqueued on the current stream
@@ -87,9 +117,15 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
 
     record: also store the trajectory the adjoint consumes (training; dadmm_forward_record).
 
+    y0 = U0 = d0 = None: the reference's random inits are drawn by the prologue launch
+    (draw_inits; bit-identical to torch.randn * 1e-2 from the device's default generator).
+
     Returns (Y [K,B,P,n], U_K [B,P,n] or None, status int32 device tensor [1]), plus, with
     ``record``, a ``Trajectory`` as a fourth element."""
     _dev_check(b, hyp, y0, U0, d0, graphs.nbr, graphs.deg)
+    draw = y0 is None
+    if draw != (U0 is None) or draw != (d0 is None):
+        raise ValueError("pass all of y0, U0, d0 or none of them")
     if path not in ("auto", "fused", "stepwise"):
         raise ValueError(f"unknown path {path!r}")
     B, P, m = b.shape
@@ -99,21 +135,34 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     ns = op.n_store
     b = b.contiguous().float()
     hyp = hyp.contiguous().float()
-    y0, U0, d0 = (_pad_n(x, ns).contiguous().float() for x in (y0, U0, d0))
+    if not draw:
+        y0, U0, d0 = (_pad_n(x, ns).contiguous().float() for x in (y0, U0, d0))
     Y = torch.empty((K, B, P, ns), dtype=torch.float32, device=b.device)
     U = torch.empty((B, P, ns), dtype=torch.float32, device=b.device) if want_U else None
     Grec = Urec = None
     if record:
         Grec = torch.empty((K, B, P, ns), dtype=torch.float32, device=b.device)
         Urec = torch.empty((K, B, P, ns), dtype=torch.float32, device=b.device)
-    status = torch.zeros(1, dtype=torch.int32, device=b.device)
     d = op.dims(B=B, K=K, variant=variant, hyp_rows=H, graph_shared=graphs.shared)
     L = _lib.load()
+    if path == "fused" and not graphs.fused_ok:
+        raise ValueError("the fused kernel follows non-ascending adjacency orders only for "
+                         "P <= 8; use path='auto' or 'stepwise'")
+    # one device allocation: [status word | 252 B pad | stepwise scratch (guard flags first)];
+    # the prologue zeroes the status word and the flags in the same launch as the draws
+    nbytes = L.dadmm_stepwise_scratch_bytes(ctypes.byref(d)) if path != "fused" else 0
+    words = torch.empty(256 + max(nbytes, 256), dtype=torch.uint8, device=b.device)
+    status = words[:4].view(torch.int32)
+    scratch = words[256:]
+    nzero = (256 + (_sw_flag_bytes(K) if path != "fused" else 0)) // 4
+    if draw:
+        y0, U0, d0 = draw_inits((B, P, op.n), b.device, ns, zero=words, nzero=nzero)
+    else:
+        with torch.cuda.device(b.device):
+            _lib.check("dadmm_prologue", L.dadmm_prologue(
+                0, 0, 0, 1, 1, 0.0, 0.0, None, None, None, _ptr(words), nzero, _stream(b.device)))
     with torch.cuda.device(b.device):
         stream = _stream(b.device)
-        if path == "fused" and not graphs.fused_ok:
-            raise ValueError("the fused kernel follows non-ascending adjacency orders only for "
-                             "P <= 8; use path='auto' or 'stepwise'")
         fused = path != "stepwise" and graphs.fused_ok
         if fused:
             if record:
@@ -131,12 +180,11 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
             else:
                 _lib.check("dadmm_forward_record" if record else "dadmm_forward", rc)
         if path != "fused":
-            nbytes = L.dadmm_stepwise_scratch_bytes(ctypes.byref(d))
-            scratch = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=b.device)
+            gate = _lib.FLAGS_ZEROED | (_lib.GATE_ON if fused else 0)
             _lib.check("dadmm_forward_stepwise", L.dadmm_forward_stepwise(
                 ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.vptr), _ptr(graphs.vq),
                 _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U),
-                _ptr(Grec), _ptr(Urec), _ptr(status), 1 if fused else 0, _ptr(scratch), stream))
+                _ptr(Grec), _ptr(Urec), _ptr(status), gate, _ptr(scratch), stream))
     traj = Trajectory(Y, Grec, Urec, y0, d0, hyp, variant) if record else None
     if ns != op.n:
         Y = Y[..., : op.n]

@@ -100,16 +100,12 @@ class DLASSO_unfolded(nn.Module):
         graphs = ingest(graph_list, self.P, batch_size, device)
 
         if inits is None:
-            # == torch.randn(shape) * 1e-2 value for value (same generator stream, same
-            # product rounding; tests/test_gpu_parity.py::test_init_draws_match_randn), one
-            # kernel per tensor instead of two
-            shape = (batch_size, self.P, self.n, 1)
-            y0 = torch.empty(shape, device=device).normal_(0.0, 1e-2)
-            U0 = torch.empty(shape, device=device).normal_(0.0, 1e-2)
-            d0 = torch.empty(shape, device=device).normal_(0.0, 1e-2)
+            # drawn by the forward's prologue launch: == torch.randn((B,P,n,1)) * 1e-2 x 3 value
+            # for value, same generator stream (tests/test_gpu_parity.py::
+            # test_prologue_draws_match_torch)
+            y0 = U0 = d0 = None
         else:
-            y0, U0, d0 = inits
-        y0, U0, d0 = (x.reshape(batch_size, self.P, self.n) for x in (y0, U0, d0))
+            y0, U0, d0 = (x.reshape(batch_size, self.P, self.n) for x in inits)
 
         table = self.hyp_table(K)                       # [K, H, 4]
         Y, self.last_status = dadmm_unfolded_apply(self.operator(), bb, graphs, table, y0, U0,

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 4
+#define DADMM_ABI_VERSION 5
 
 enum {
     DADMM_OK = 0,
@@ -133,6 +133,29 @@ int dadmm_forward_record(const dadmm_dims* d, const void* op, const float* b, co
                          const float* y0, const float* U0, const float* d0, float* Y, float* Grec,
                          float* Urec, float* U_out, int32_t* status, void* stream);
 
+/* Bits of the `gate` argument of dadmm_forward_stepwise. */
+enum {
+    DADMM_GATE_ON = 1,        /* run only if *status != 0 when the launch starts (see below)     */
+    DADMM_FLAGS_ZEROED = 2    /* the scratch's flag words are already zero (dadmm_prologue)      */
+};
+
+/* Philox offset increment torch's normal_ consumes per tensor of `numel` float elements on the
+ * current device (ATen/native/hip/DistributionTemplates.h calc_execution_policy). */
+uint64_t dadmm_normal_offset_step(int64_t numel);
+
+/* The forward's prologue, one launch:
+ *   - when numel > 0, the reference's random inits (unfolded_DLASSO.py:49-51)
+ *       y0, U0, d0 = torch.randn((B, P, n, 1)) * 1e-2, drawn in that order,
+ *     bit-identical to three torch normal_(mean, stddev) calls on the generator state (seed,
+ *     offset), the k-th at offset + k * dadmm_normal_offset_step(numel) (the caller advances its
+ *     generator by 3 steps). numel = B*P*n; rows of n values are stored with stride n_store >= n
+ *     (padding columns untouched);
+ *   - zeroes `nzero` int32 words at `zero` (the status word / guard flags of the forward).
+ * Replaces: the three torch.randn(...) * 1e-2 draws (6 eager kernels) and the status / flag fills. */
+int dadmm_prologue(uint64_t seed, uint64_t offset, int64_t numel, int32_t n, int32_t n_store,
+                   float mean, float stddev, float* y0, float* U0, float* d0, int32_t* zero,
+                   int64_t nzero, void* stream);
+
 /* Bytes of device scratch dadmm_forward_stepwise needs for `d` (256-byte aligned pointer). */
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d);
 
@@ -141,6 +164,7 @@ size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d);
  * kernel, so on guard-free inputs its Y is bit-identical to dadmm_forward's.
  * Replaces: the same loop as dadmm_forward (unfolded_DLASSO.py:45, 53-109), for every shape.
  * Graph: visit_ptr / visit_q (layout above) and deg ([P] when graph_shared, else [B][P]).
+ * gate bits DADMM_GATE_ON / DADMM_FLAGS_ZEROED (the latter skips the flag memset).
  * gate = 0: always runs (2K + 2 launches).
  * gate = 1: ONE persistent launch that returns at once unless *status != 0 when it starts: the
  *           exact recomputation of a batch the fused dadmm_forward flagged, enqueued right after it

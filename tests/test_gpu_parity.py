@@ -383,3 +383,27 @@ def test_module_default_inits_follow_the_seed(cuda):
         Y2, _ = model(bt, [G] * B, inits=inits)
     assert torch.equal(Y1, Y2)
     assert model.guard_warnings() == []
+
+
+@pytest.mark.parametrize("shape", [(4096, 5, 256), (32768, 5, 256), (7, 3, 62), (1, 1, 4),
+                                   (300, 16, 512)])
+def test_prologue_draws_match_torch(cuda, shape):
+    """dadmm_prologue (one launch) == three torch.randn(shape + (1,)) * 1e-2 draws bit for bit,
+    leaves the generator where torch would (the next draw agrees too), pads rows with zeros and
+    zeroes the requested words."""
+    from dadmm_hip.ops import draw_inits
+    B, P, n = shape
+    ns = (n + 3) & ~3
+    torch.manual_seed(4321)
+    torch.randn(5, device=cuda)                               # a non-zero starting offset
+    ref = [torch.randn(shape + (1,), device=cuda)[..., 0] * 1e-2 for _ in range(3)]
+    nxt = torch.randn(17, device=cuda)
+    torch.manual_seed(4321)
+    torch.randn(5, device=cuda)
+    words = torch.full((70,), 7, dtype=torch.int32, device=cuda)
+    got = draw_inits(shape, cuda, ns, zero=words, nzero=64)
+    assert torch.equal(torch.randn(17, device=cuda), nxt)
+    for r, g in zip(ref, got):
+        assert torch.equal(g[..., :n], r)
+        assert bool((g[..., n:] == 0).all())
+    assert bool((words[:64] == 0).all()) and bool((words[64:] == 7).all())
