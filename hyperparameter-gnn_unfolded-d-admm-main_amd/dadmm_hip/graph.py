@@ -24,6 +24,9 @@ Quirks of the reference kept on purpose (it never checks ``len(graph_list) == le
 """
 from __future__ import annotations
 
+import gc
+import itertools
+
 import numpy as np
 import torch
 
@@ -145,6 +148,84 @@ def _batch(infos, P: int, device) -> GraphBatch:
     return GraphBatch(t[0], t[1], False, t[4] if ordered else None, t[2], t[3], fused_ok)
 
 
+def _adjacency(g, P: int):
+    """graph.neighbors(p) for p = 0..P-1, as lists (networkx's adjacency dict when present)."""
+    adj = getattr(g, "_adj", None)
+    if adj is not None:
+        return [list(adj[p]) for p in range(P)]
+    return [list(g.neighbors(p)) for p in range(P)]
+
+
+def _batch_vectorized(graph_list, P: int, device) -> GraphBatch:
+    """Per-sample layouts for many distinct graphs: one Python pass collects the adjacency lists,
+    everything else (masks, degrees, order nibbles, the reference-order visit lists) is numpy over
+    the flattened (sample, agent, position) entries — the replacement for the per-sample,
+    per-agent loops of compute_sum_neighbors / compute_delta at B in the thousands."""
+    B = len(graph_list)
+    gc_on = gc.isenabled()
+    gc.disable()          # B*P short-lived lists would trigger full cyclic-GC passes
+    try:
+        lists = [nb for g in graph_list for nb in _adjacency(g, P)]      # B*P lists
+    finally:
+        if gc_on:
+            gc.enable()
+    cnt = np.fromiter((len(nb) for nb in lists), np.int64, count=B * P)
+    q = np.fromiter(itertools.chain.from_iterable(lists), np.int64, count=int(cnt.sum()))
+    if q.size and (q.min() < 0 or q.max() >= P):
+        bad = q[(q < 0) | (q >= P)][0]
+        raise ValueError(f"neighbour id {bad}: must be an agent 0..{P - 1}")
+    row = np.repeat(np.arange(B * P), cnt)                 # (s, a) flattened
+    start = np.zeros(B * P + 1, np.int64)
+    np.cumsum(cnt, out=start[1:])
+    t = np.arange(q.size) - start[row]                     # position in the adjacency list
+    s_, a_ = row // P, row % P
+    nbr = np.zeros(B * P, np.uint64)
+    np.add.at(nbr, row, np.left_shift(np.uint64(1), q.astype(np.uint64)))   # unique per (s,a)
+    deg = cnt.reshape(B, P).astype(np.float32)
+    # ascending adjacency? (erdos_renyi_graph lists are; appended edges break it)
+    desc = (t[1:] > 0) & (q[1:] < q[:-1]) if q.size > 1 else np.zeros(0, bool)
+    ordered = bool(desc.any())
+    fused_ok = not (ordered and P > 8)
+    ordered &= fused_ok
+    order = None
+    if ordered:
+        order = np.zeros(B * P, np.uint32)
+        keep = t < 8
+        np.add.at(order, row[keep], (q[keep] & 15).astype(np.uint32) << (4 * t[keep]).astype(np.uint32))
+    # visit lists (see _visit_lists): for agent p of sample s, entries in the order compute_delta
+    # accumulates them. For an undirected graph "p in N(p')" <=> "p' in N(p)", so they are
+    #   N(p) n [0, p) ascending | N(p) in adjacency order (a self-loop twice) | N(p) n (p, P) ascending
+    # and are placed without sorting: nonzero() of the dense neighbour matrix is row-major.
+    dense = np.zeros((B * P, P), bool)
+    dense[row, q] = True
+    if not np.array_equal(dense.reshape(B, P, P), dense.reshape(B, P, P).transpose(0, 2, 1)):
+        return None                                  # not symmetric: caller takes the exact path
+    col = np.arange(P)
+    below = dense & (col[None, :] < (np.arange(B * P) % P)[:, None])
+    above = dense & (col[None, :] > (np.arange(B * P) % P)[:, None])
+    loop = q == a_
+    c0, c2 = below.sum(1), above.sum(1)
+    c1 = cnt + np.bincount(row[loop], minlength=B * P)
+    vptr = np.zeros(B * P + 1, np.int64)
+    np.cumsum(c0 + c1 + c2, out=vptr[1:])
+    vq = np.empty(int(vptr[-1]), np.uint8)
+    r0, q0 = np.nonzero(below)
+    vq[vptr[r0] + (np.arange(r0.size) - np.repeat(np.cumsum(c0) - c0, c0))] = q0
+    # own lists: position t, shifted by the self-loop duplicates earlier in the same list
+    before = np.cumsum(loop) - loop                 # self-loops strictly before each entry
+    pos1 = vptr[row] + c0[row] + t + (before - before[start[row]]) if q.size else row
+    vq[pos1] = q
+    vq[pos1[loop] + 1] = q[loop]
+    r2, q2 = np.nonzero(above)
+    vq[vptr[r2] + c0[r2] + c1[r2] + (np.arange(r2.size) - np.repeat(np.cumsum(c2) - c2, c2))] = q2
+    vptr = vptr.astype(np.int32)
+    arrays = [nbr.view(np.int64).reshape(B, P), deg, vptr, _vq_nonempty(vq)]
+    if ordered:
+        arrays.append(order.view(np.int32).reshape(B, P))
+    t_ = _to_device(arrays, device)
+    return GraphBatch(t_[0], t_[1], False, t_[4] if ordered else None, t_[2], t_[3], fused_ok)
+
+
 def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
     if P > 64:
         raise ValueError(f"P={P} > 64 agents does not fit the uint64 neighbour mask")
@@ -157,11 +238,15 @@ def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
             f"The size of tensor a ({batch_size}) must match the size of tensor b ({G}) at "
             "non-singleton dimension 0")
     g0 = graph_list[0]
-    same = (graph_list.count(g0) if hasattr(graph_list, "count")      # C-speed identity scan
-            else sum(1 for g in graph_list if g is g0))
+    same = sum(1 for g in graph_list if g is g0)   # object identity (list.count would call __eq__)
     if same == G:                   # one object repeated
         per = {id(g0): _info(g0, P)}
     else:
+        ids = {id(g) for g in graph_list}
+        if len(ids) > 64 and G == batch_size:
+            gb = _batch_vectorized(graph_list, P, device)      # many distinct graphs
+            if gb is not None:
+                return gb
         per = {}
         for g in graph_list:
             if id(g) not in per:

@@ -200,3 +200,36 @@ def test_compute_loss_matches_oracle_and_nan_fallback():
     mean, final = gnn_dlasso_utils.compute_loss(torch.from_numpy(Y)[..., None],
                                                 torch.from_numpy(x)[..., None])
     assert mean.item() == 1.0 and final.item() == 1.0
+
+
+@pytest.mark.parametrize("P,B,prob,loops", [(5, 200, 0.5, False), (16, 150, 0.3, False),
+                                           (9, 120, 0.4, True), (50, 80, 0.5, False)])
+def test_vectorized_ingestion_equals_per_graph_path(P, B, prob, loops):
+    """The batch builder for many distinct graphs (numpy over flattened adjacency entries) gives
+    exactly the per-graph reference-order layouts: masks, degrees, order nibbles, visit lists."""
+    from dadmm_hip import graph as Gm
+    graphs = []
+    for s in range(B):
+        g = O.connected_er_graph(P, prob, seed=s)      # patched graphs: non-ascending adjacency
+        if loops and s % 3 == 0:
+            g.add_edge(s % P, s % P)
+        graphs.append(g)
+    fast = Gm._batch_vectorized(graphs, P, "cpu")
+    ref = Gm._batch([Gm._info(g, P) for g in graphs], P, "cpu")
+    for k in ("nbr", "deg", "vptr", "vq"):
+        np.testing.assert_array_equal(getattr(fast, k).numpy(), getattr(ref, k).numpy(), err_msg=k)
+    assert (fast.order is None) == (ref.order is None) and fast.fused_ok == ref.fused_ok
+    if fast.order is not None:
+        np.testing.assert_array_equal(fast.order.numpy(), ref.order.numpy())
+    assert Gm.ingest(graphs, P, B, "cpu").vq.numel() == ref.vq.numel()
+
+
+def test_vectorized_ingestion_rejects_asymmetric_graphs():
+    from dadmm_hip import graph as Gm
+    P = 4
+    graphs = [nx.DiGraph([(0, 1), (1, 2)]) for _ in range(70)]
+    for g in graphs:
+        g.add_nodes_from(range(P))
+    assert Gm._batch_vectorized(graphs, P, "cpu") is None
+    gb = Gm.ingest(graphs, P, 70, "cpu")                # falls back to the per-graph path
+    assert gb.deg.numpy()[0].tolist() == [1, 1, 0, 0]
