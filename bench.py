@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--graph-prob", type=float, default=0.5)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the secondary measurements (training step, GNN model, P=16 path)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written from a rocprofv3 --pmc pass)")
     return ap.parse_args()
@@ -87,6 +89,7 @@ def main():
     gen = torch.Generator().manual_seed(4321 + rank)
     x = 2 * torch.randn(B, n, generator=gen) * (torch.rand(B, n, generator=gen) <= 0.25)
     b = torch.einsum("pmn,bn->bpm", torch.from_numpy(A), x)
+    x = x.float()
     At = torch.from_numpy(A)[None].to(dev)
     bt = b[..., None].to(dev)
     G = O.er_graph(P, a.graph_prob, seed=7)
@@ -181,6 +184,7 @@ def main():
         parity = check_parity(O, model, A, b, G, dev, P, n, m, K)
         cpu = None if a.no_cpu_baseline else cpu_baseline(O, A, b, G, model, P, n, m, K,
                                                           a.cpu_baseline_seconds)
+        extras = None if a.no_extras else secondary(O, dev, A, b, x, G, model, P, n, m, K, B)
         out = {
             "metric": "ADMM-iters/sec (node), batch=4096 P=5 n=256 K=25; final-iter MSE vs ref",
             "value": value,
@@ -211,10 +215,105 @@ def main():
                                        "frac": tflops / PEAK_FP32_TFLOPS}},
             "cpu_baseline": cpu,
             "parity": parity,
+            "extras": extras,
         }
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _event_ms(fn, reps, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
+    """Secondary measurements on the same box, outside the timed region (not the headline):
+    the training step at the headline shape (recording forward + adjoint kernel, and the module's
+    forward + compute_loss + loss.backward()), the GNN-hypernetwork model's forward
+    (DLASSO_GNNHyp3_Progressive, h = 100) and BASELINE configs[2]'s P=16, n=512 shape, which the
+    stepwise path serves."""
+    out = {}
+    try:
+        import gnn_dlasso_utils
+        from dadmm_hip.ops import backward_raw, forward_raw
+        bt = b[..., None].to(dev)
+        label = x.to(dev)[..., None]
+        op = model.operator()
+        from dadmm_hip.graph import ingest
+        g = ingest([G] * B, P, B, dev)
+        table = model.hyp_table(K).detach()
+        bb = b.to(dev)
+        out["train_forward_record_ms"] = _event_ms(
+            lambda: forward_raw(op, bb, g, table, record=True), 10)
+        _, _, _, tr = forward_raw(op, bb, g, table, record=True)
+        gY = torch.randn(K, B, P, n, device=dev)
+        out["adjoint_ms"] = _event_ms(lambda: backward_raw(op, g, tr, gY), 10)
+        model.train()
+
+        def step():
+            Y, _ = model(bt, [G] * B)
+            _, lf = gnn_dlasso_utils.compute_loss(Y, label)
+            model.zero_grad()
+            lf.backward()
+        out["module_train_step_ms"] = _event_ms(step, 5)
+        out["train_units_per_s"] = B * K / (out["module_train_step_ms"] * 1e-3)
+        model.eval()
+    except Exception as e:  # secondary numbers never break the headline line
+        out["train_error"] = repr(e)[:300]
+    try:
+        import argparse as _ap
+
+        import gnn_dlasso_models_progressive as GM
+        args = _ap.Namespace(GHN_iter_num=K, GHyp_hidden=100, DADMM_mode="diff", alpha_max=0.1,
+                             tau_max=0.99, rho_max=0.99, eta_max=0.99)
+        gnn = GM.DLASSO_GNNHyp3_Progressive(torch.from_numpy(A)[None].to(dev), args).to(dev).eval()
+        Bg = 1024
+        graphs = [O.connected_er_graph(P, 0.5, seed=100 + s) for s in range(Bg)]
+        bg = b[:Bg, ..., None].to(dev)
+
+        def gfwd():
+            with torch.no_grad():
+                gnn(bg, graphs)
+        ms = _event_ms(gfwd, 3, warm=1)
+        out["gnn_forward"] = {"B": Bg, "P": P, "n": n, "m": m, "K": K, "hidden": 100, "ms": ms,
+                              "units_per_s": Bg * K / (ms * 1e-3)}
+    except Exception as e:
+        out["gnn_error"] = repr(e)[:300]
+    try:
+        import unfolded_DLASSO
+        P3, n3, m3, B3, K3 = 16, 512, 64, 4096, 25
+        A3, b3, _ = O.make_problem(P3, m3, n3, B3, seed=77)
+        mod = unfolded_DLASSO.DLASSO_unfolded(torch.from_numpy(A3)[None].to(dev),
+                                              argparse.Namespace(**{**vars(model.args), "GHN_iter_num": K3}))
+        mod = mod.to(dev).eval()
+        graphs3 = [O.connected_er_graph(P3, 0.3, seed=s) for s in range(B3)]
+        b3t = torch.from_numpy(b3)[..., None].to(dev)
+
+        def f3():
+            with torch.no_grad():
+                mod(b3t, graphs3)
+        t0 = time.perf_counter()
+        from dadmm_hip.graph import ingest as _ing
+        _ing(graphs3, P3, B3, dev)
+        ingest_ms = 1e3 * (time.perf_counter() - t0)
+        ms = _event_ms(f3, 3, warm=1)
+        out["c3_stepwise"] = {"B": B3, "P": P3, "n": n3, "m": m3, "K": K3, "graph_prob": 0.3,
+                              "ms_per_forward": ms, "units_per_s": B3 * K3 / (ms * 1e-3),
+                              "alg_bytes_per_unit": 4 * P3 * (4 * n3 + m3),
+                              "alg_GBs": 4 * P3 * (4 * n3 + m3) * B3 * K3 / (ms * 1e-3) / 1e9,
+                              "graph_ingest_ms_cold": ingest_ms}
+    except Exception as e:
+        out["c3_error"] = repr(e)[:300]
+    return out
 
 
 def check_parity(O, model, A, b, G, dev, P, n, m, K, Bs=32):
