@@ -49,6 +49,8 @@ int check_dims(const dadmm_dims* d) {
 
 int n_pad_of(const dadmm_dims* d) { return 64 * dadmm::fused_nt(d->n); }
 
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 }  // namespace
 
 extern "C" {
@@ -440,7 +442,61 @@ int dadmm_prologue(uint64_t seed, uint64_t offset, int64_t numel, int32_t n, int
     return ok();
 }
 
-static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t dadmm_tiled_scratch_bytes(const dadmm_dims* d) {
+    if (check_dims(d) != DADMM_OK) return 0;
+    return 2 * align256(sizeof(float) * (size_t)d->B * d->P * d->n);
+}
+
+int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
+                        const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
+                        const float* hyp, const float* y0, const float* U0, const float* d0,
+                        float* Y, float* U_out, int32_t* status, void* scratch, void* stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (d->B == 0 || d->K == 0) return ok();
+    if (!op || !b || !visit_ptr || !visit_q || !deg || !hyp || !y0 || !U0 || !d0 || !Y || !scratch)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(op) || !aligned16(Y) || !aligned16(y0) || !aligned16(U0) || !aligned16(d0) ||
+        (U_out != nullptr && !aligned16(U_out)))
+        return fail(DADMM_EINVAL, "op, Y, y0, U0, d0 and U_out must be 16-byte aligned");
+    if (((uintptr_t)scratch & 255u) != 0) return fail(DADMM_EINVAL, "scratch must be 256-byte aligned");
+    if (d->m > dadmm::M_PAD)
+        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m, dadmm::M_PAD);
+    if ((d->n & 3) != 0) return fail(DADMM_EUNSUPPORTED, "n=%d: needs n %% 4 == 0 (zero-pad n)", d->n);
+    const int np = n_pad_of(d);
+    if (dadmm::tiled_lds_bytes(np) > 160 * 1024)
+        return fail(DADMM_EUNSUPPORTED, "n=%d: the y tile does not fit the LDS", d->n);
+    const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);
+    dadmm::TiledArgs a{};
+    a.A = (const float*)op;
+    a.At = a.A + (size_t)d->P * dadmm::M_PAD * np;
+    a.b = b;
+    a.vptr = visit_ptr;
+    a.vq = visit_q;
+    a.deg = deg;
+    a.hyp = hyp;
+    a.y0 = y0;
+    a.U0 = U0;
+    a.d0 = d0;
+    a.Y = Y;
+    a.Ubuf[0] = (float*)scratch;
+    a.Ubuf[1] = (float*)((char*)scratch + state);
+    a.U_out = U_out;
+    a.status = status;
+    a.B = d->B;
+    a.P = d->P;
+    a.m = d->m;
+    a.n = d->n;
+    a.n_pad = np;
+    a.K = d->K;
+    a.hyp_rows = d->hyp_rows;
+    a.variant = d->variant;
+    a.graph_shared = d->graph_shared;
+    hipError_t e = dadmm::launch_tiled(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "tiled launch: %s", hipGetErrorString(e));
+    return ok();
+}
 
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;

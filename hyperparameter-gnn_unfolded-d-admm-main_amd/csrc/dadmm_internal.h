@@ -111,6 +111,27 @@ hipError_t gnn_launch_finish(const GnnArgs& a, hipStream_t st);
 hipError_t gnn_launch_step_backward(const GnnArgs& a, int k, const GnnGrads& gg, hipStream_t st);
 size_t gnn_gram_lds(int n_pad);
 
+// ---- one launch per iteration, state in HBM (dadmm_tiled.hip) ---------------------------------
+struct TiledArgs {
+    const float* A;         // prepared operator [P][M_PAD][n_pad]
+    const float* At;        // [P][n_pad][M_PAD]
+    const float* b;         // [B][P][m]
+    const int32_t* vptr;    // visit lists (as StepArgs)
+    const uint8_t* vq;
+    const float* deg;       // [G][P]
+    const float* hyp;       // [K][hyp_rows][4]
+    const float* y0;        // [B][P][n]
+    const float* U0;
+    const float* d0;
+    float* Y;               // [K][B][P][n]
+    float* Ubuf[2];         // ping-pong U_k buffers [B][P][n] (scratch)
+    float* U_out;           // [B][P][n] or nullptr
+    int32_t* status;        // or nullptr (OR-ed DADMM_STATUS_* bits)
+    int B, P, m, n, n_pad, K, hyp_rows, variant, graph_shared;
+};
+size_t tiled_lds_bytes(int n_pad);
+hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream);
+
 // ---- forward prologue (dadmm_rng.hip) -----------------------------------------------------------
 struct PrologueArgs {
     uint64_t seed, offset, offset_step;   // torch Philox state; per-tensor offset increment

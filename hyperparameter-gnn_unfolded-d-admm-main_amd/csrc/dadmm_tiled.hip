@@ -1,0 +1,332 @@
+// dadmm_tiled.hip — one launch per iteration for the shapes the fused kernel cannot hold on chip
+// (many agents / long signals, e.g. BASELINE configs[2]: P = 16, n = 512; configs[4]: P = 50,
+// n = 1024): the state lives in HBM, every (16-sample tile, agent) workgroup does a whole
+// iteration of its agent in one pass.
+//
+// Reference semantics: unfolded_DLASSO.py:53-107 / :127-140 (and the GNN variant's clamps,
+// gnn_dlasso_models_progressive.py:205-232). Iteration k of workgroup (tile, p):
+//   delta_k[p] = sum over p's visit list of (y_p - y_q), from y_k of the neighbours (their tiles
+//                are read by the sibling workgroups of the same tile at the same time: L2 hits)
+//                (k = 0: the caller's d0);
+//   U_k[p]     = clamp(U_{k-1}[p] + delta_k[p] eta_{k-1}, +-vclip_{k-1})   (the dual update of
+//                iteration k-1, deferred to here as in the fused kernel; k = 0: U0);
+//   R          = A_p y_k - b_p;  G = A_p^T R                (f32 MFMA fma chains, the fused
+//                kernel's / the oracle's order);
+//   y_{k+1}    = clamp(y_k - alpha clamp(G + sign(y) tau + U_k deg + delta_k rho)) -> Y[k].
+// So per unit of work the HBM traffic is read y_k, U_{k-1}, b, write y_{k+1}, U_k: SURVEY.md
+// §8(d)'s algorithmic 4 P (4n + m) bytes (the neighbour tiles come from L2).
+//
+// Guards: like the fused kernel, this path does not apply the reference's batch-global NaN/Inf
+// guards; it ORs the status bits of every case where one would fire, and the caller enqueues the
+// gated stepwise recomputation behind it (dadmm_forward_stepwise, DADMM_GATE_ON). On guard-free
+// inputs its output is bit-identical to the stepwise path and to oracle_forward_f32.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dadmm_internal.h"
+
+namespace dadmm {
+namespace tiled {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int THREADS = 256;   // 4 waves: GEMM1 = one 16-row m-block per wave
+constexpr int WAVES = 4;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float tclamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+__device__ __forceinline__ bool finitef(float x) { return __builtin_isfinite(x); }
+
+__device__ __forceinline__ void clips(int variant, int k, float& gclip, float& vclip) {
+    if (variant == 0) {
+        gclip = fmaxf(1.0f, 30.0f - (float)k);          // unfolded_DLASSO.py:80
+        vclip = fmaxf(10.0f, 200.0f - (float)(k * 3));  // unfolded_DLASSO.py:92
+    } else {
+        gclip = 10.0f;                                   // gnn_dlasso_models_progressive.py:212
+        vclip = 100.0f;                                  // :224, :232
+    }
+}
+
+constexpr int HALVES = 2;            // 16-sample MFMA column blocks per workgroup (32 samples):
+                                     // every A / A^T operand load feeds two fma chains
+constexpr int ST = HALVES * BT;      // samples per workgroup
+constexpr int VMAX = 128;            // visit-list entries cached per sample (2P <= 128)
+
+// delta_k rows n0..n0+3 of the lane's two samples (halves) for agent p: the sum over each
+// sample's visit list (in LDS) of (y_p - y_q) in list order; the neighbour loads of both samples
+// are issued together, four entries at a time (eight 16-B loads in flight per lane)
+__device__ __forceinline__ void consensus_rows2(const float* yk, const size_t (&srow)[2], int n,
+                                                int n0, const uint8_t* const (&vl)[2],
+                                                const int (&len)[2], const f32x4 (&yp)[2],
+                                                f32x4 (&acc)[2]) {
+    acc[0] = acc[1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    const int L = len[0] > len[1] ? len[0] : len[1];
+    for (int t = 0; t < L; t += 4) {
+        f32x4 yq[2][4];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (t + u < len[hh]) yq[hh][u] = *(const f32x4*)(yk + (srow[hh] + vl[hh][t + u]) * n + n0);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (t + u < len[hh]) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[hh][r] = acc[hh][r] + (yp[hh][r] - yq[hh][u][r]);
+                }
+    }
+}
+
+// blockIdx -> (tile, agent) so that the P workgroups of one sample tile run on the same XCD
+// (dispatch is round-robin over the 8 XCDs, each with its own L2): the neighbour tiles a
+// workgroup reads for delta are its siblings' own tiles, hot in that L2.
+__device__ __forceinline__ int xcd_swizzle(int bid, int G) {
+    constexpr int NX = 8;
+    const int xcd = bid % NX, i = bid / NX, q = G / NX, r = G % NX;
+    return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
+}
+
+// k >= 0: one iteration (see header). k == K: the final dual update only (U_K into U_out).
+// Workgroup = (32-sample tile, agent p).
+__global__ __launch_bounds__(THREADS) void iter_kernel(TiledArgs a, int k) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad;
+    const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int tile = wg / P, p = wg % P;
+    const int RS = M_PAD + 4;
+    float* Rlds = lds;                               // [ST][RS]
+    uint8_t* Vlds = (uint8_t*)(Rlds + ST * RS);      // [ST][VMAX] visit lists of agent p
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = lane & 15, h = lane >> 4;
+    const size_t S = (size_t)B * P * n;
+    const float* yk = k == 0 ? a.y0 : a.Y + (size_t)(k - 1) * S;   // y_k of every agent
+    const bool final_only = k == a.K;
+    const int H = a.hyp_rows;
+    const int hp = H == 1 ? 0 : p;
+    uint32_t status = 0;
+
+    // visit lists of the workgroup's samples for agent p -> LDS
+    if (k > 0) {
+        for (int i = threadIdx.x; i < ST * VMAX; i += THREADS) {
+            const int sl = i / VMAX, t = i % VMAX;
+            const int s2 = tile * ST + sl;
+            if (s2 < B) {
+                const int g0 = a.graph_shared ? 0 : s2 * P;
+                const int v0 = a.vptr[g0 + p], len = a.vptr[g0 + p + 1] - v0;
+                if (t < len) Vlds[i] = a.vq[v0 + t];
+            }
+        }
+    }
+    if (!final_only) {
+        if (k == 0) {   // :55 guard on y0 (the only iteration where it can fire)
+            const int nc4 = n / 4;
+            bool bad = false;
+            for (int idx = threadIdx.x; idx < ST * nc4; idx += THREADS) {
+                const int s2 = tile * ST + idx / nc4, c = 4 * (idx % nc4);
+                if (s2 < B) {
+                    const f32x4 v = *(const f32x4*)(yk + ((size_t)s2 * P + p) * n + c);
+                    bad |= !(finitef(v[0]) && finitef(v[1]) && finitef(v[2]) && finitef(v[3]));
+                }
+            }
+            status |= bad ? 1u : 0u;
+        }
+        // GEMM1: R = A_p y - b_p, one fma chain per row from -b (wave w = m-block w), one chain
+        // per 16-sample half sharing every A load
+        f32x4 acc[HALVES];
+#pragma unroll
+        for (int hh = 0; hh < HALVES; ++hh) {
+            const int s = tile * ST + hh * BT + j;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int mi = 16 * w + 4 * h + r;
+                acc[hh][r] = (s < B && mi < m) ? -a.b[((size_t)s * P + p) * m + mi] : 0.0f;
+            }
+        }
+        if (16 * w < m) {
+            // the B operand (y_k, 16 columns per half) straight from L2/HBM; columns past n and
+            // samples past B read as 0 (the padded operator columns are 0 too)
+            const float* arow = a.A + ((size_t)p * M_PAD + 16 * w + j) * NP + 4 * h;
+            const float* brow[HALVES];
+            bool bok[HALVES];
+#pragma unroll
+            for (int hh = 0; hh < HALVES; ++hh) {
+                const int s = tile * ST + hh * BT + j;
+                bok[hh] = s < B;
+                brow[hh] = yk + ((size_t)(bok[hh] ? s : 0) * P + p) * n + 4 * h;
+            }
+            auto ldb = [&](int hh, int t) -> f32x4 {
+                return (bok[hh] && 16 * t + 4 * h < n) ? *(const f32x4*)(brow[hh] + 16 * t)
+                                                       : (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+            };
+            f32x4 av = *(const f32x4*)arow;
+            f32x4 bv[HALVES];
+#pragma unroll
+            for (int hh = 0; hh < HALVES; ++hh) bv[hh] = ldb(hh, 0);
+            for (int t = 0; t < NP / 16; ++t) {
+                const bool more = t + 1 < NP / 16;
+                const f32x4 an = more ? *(const f32x4*)(arow + 16 * (t + 1)) : av;
+                f32x4 bn[HALVES];
+#pragma unroll
+                for (int hh = 0; hh < HALVES; ++hh) bn[hh] = more ? ldb(hh, t + 1) : bv[hh];
+#pragma unroll
+                for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[hh] = mfma4(av[r], bv[hh][r], acc[hh]);
+                av = an;
+#pragma unroll
+                for (int hh = 0; hh < HALVES; ++hh) bv[hh] = bn[hh];
+            }
+        }
+#pragma unroll
+        for (int hh = 0; hh < HALVES; ++hh)
+            *(f32x4*)(Rlds + (hh * BT + j) * RS + 16 * w + 4 * h) = acc[hh];
+    }
+    __syncthreads();
+
+    float al = 0, ta = 0, rh = 0, et = 0, et_prev = 0, gclip = 0, vclip = 0, vclip_prev = 0;
+    if (!final_only) {
+        const float* hk = a.hyp + ((size_t)k * H + hp) * 4;
+        al = hk[0]; ta = hk[1]; rh = hk[2]; et = hk[3];
+        status |= (finitef(al) && finitef(ta) && finitef(rh) && finitef(et)) ? 0u : 8u;
+        clips(a.variant, k, gclip, vclip);
+    }
+    if (k > 0) {
+        et_prev = a.hyp[((size_t)(k - 1) * H + hp) * 4 + 3];
+        float gtmp;
+        clips(a.variant, k - 1, gtmp, vclip_prev);
+    }
+    const float* Uprev = a.Ubuf[(k + 1) & 1];     // U_{k-1}   (k = 0: unused)
+    float* Ucur = final_only ? a.U_out : a.Ubuf[k & 1];   // U_k
+
+    // per-lane data of the two samples this lane serves
+    float dg[HALVES];
+    int vlen[HALVES];
+    f32x4 rv[HALVES][M_PAD / 16];
+#pragma unroll
+    for (int hh = 0; hh < HALVES; ++hh) {
+        const int s = tile * ST + hh * BT + j;
+        const int g0 = a.graph_shared ? 0 : s * P;
+        dg[hh] = s < B ? a.deg[g0 + p] : 0.0f;
+        vlen[hh] = s < B ? a.vptr[g0 + p + 1] - a.vptr[g0 + p] : 0;
+        if (!final_only) {
+#pragma unroll
+            for (int t = 0; t < M_PAD / 16; ++t)
+                rv[hh][t] = *(const f32x4*)(Rlds + (hh * BT + j) * RS + 16 * t + 4 * h);
+        }
+    }
+    bool bad_u0 = false, bad_g = false, bad_y = false;
+    const float* atbase = a.At + ((size_t)p * NP + j) * M_PAD + 4 * h;
+    for (int nb = w; nb < NP / 16; nb += WAVES) {
+        const int n0 = 16 * nb + 4 * h;
+        f32x4 atv[M_PAD / 16];
+        if (!final_only) {
+#pragma unroll
+            for (int t = 0; t < M_PAD / 16; ++t) atv[t] = *(const f32x4*)(atbase + (size_t)16 * nb * M_PAD + 16 * t);
+        }
+        // this tile's rows of both samples: y_k, and (k > 0) delta_k from the neighbours
+        f32x4 ypv[HALVES], dvv[HALVES];
+        {
+            size_t srow[HALVES];
+            const uint8_t* vl[HALVES];
+            int len[HALVES];
+#pragma unroll
+            for (int hh = 0; hh < HALVES; ++hh) {
+                const int s = tile * ST + hh * BT + j;
+                const bool ok = s < B && n0 < n;
+                srow[hh] = (size_t)(ok ? s : 0) * P;
+                vl[hh] = Vlds + (hh * BT + j) * VMAX;
+                len[hh] = ok && k > 0 ? vlen[hh] : 0;
+                ypv[hh] = ok ? *(const f32x4*)(yk + (srow[hh] + p) * n + n0) : (f32x4){0, 0, 0, 0};
+            }
+            consensus_rows2(yk, srow, n, n0, vl, len, ypv, dvv);
+        }
+#pragma unroll
+        for (int hh = 0; hh < HALVES; ++hh) {
+            const int s = tile * ST + hh * BT + j;
+            const bool ok = s < B && n0 < n;
+            const size_t off = ((size_t)s * P + p) * n + n0;
+            // delta_k and U_k of these 4 rows
+            f32x4 dv = {0, 0, 0, 0}, uv = {0, 0, 0, 0};
+            if (ok) {
+                if (k == 0) {
+                    dv = *(const f32x4*)(a.d0 + off);
+                    uv = *(const f32x4*)(a.U0 + off);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) bad_u0 |= !finitef(uv[r]);
+                } else {
+                    dv = dvv[hh];
+                    if (a.variant != 0) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) dv[r] = tclamp(dv[r], -20.0f, 20.0f);   // :229
+                    }
+                    const f32x4 up = *(const f32x4*)(Uprev + off);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) uv[r] = tclamp(up[r] + dv[r] * et_prev, -vclip_prev, vclip_prev);
+                }
+                *(f32x4*)(Ucur + off) = uv;             // U_k (the ping-pong buffer / U_out)
+            }
+            if (final_only) continue;
+            // GEMM2 rows of this tile + gradient assembly + primal update (:69-93)
+            f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int t = 0; t < M_PAD / 16; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gc = mfma4(atv[t][r], rv[hh][t][r], gc);
+            if (ok) {
+                const f32x4 yv = ypv[hh];
+                f32x4 yn;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float y = yv[r];
+                    const float st = y > 0.0f ? ta : (y < 0.0f ? -ta : 0.0f);   // sign(y) * tau
+                    float g = gc[r] + st;
+                    g = g + uv[r] * dg[hh];
+                    g = g + dv[r] * rh;
+                    bad_g |= g != g;
+                    g = tclamp(g, -gclip, gclip);
+                    const float v = tclamp(y - al * g, -vclip, vclip);
+                    bad_y |= !finitef(v);
+                    yn[r] = v;
+                }
+                *(f32x4*)(a.Y + (size_t)k * S + off) = yn;
+            }
+        }
+    }
+    status |= (bad_u0 ? 2u : 0u) | (bad_g ? 4u : 0u) | (bad_y ? 8u : 0u);
+    if (a.status != nullptr) {
+        uint32_t ws = status;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) ws |= __shfl_xor(ws, o);
+        if (lane == 0 && ws) atomicOr((unsigned int*)a.status, ws);
+    }
+}
+
+}  // namespace tiled
+
+size_t tiled_lds_bytes(int n_pad) {
+    (void)n_pad;
+    return 4 * (size_t)(tiled::ST * (M_PAD + 4)) + tiled::ST * tiled::VMAX;
+}
+
+hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream) {
+    const size_t lds = tiled_lds_bytes(a.n_pad);
+    if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)tiled::iter_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    const int items = ((a.B + tiled::ST - 1) / tiled::ST) * a.P;
+    for (int k = 0; k < a.K; ++k)
+        hipLaunchKernelGGL(tiled::iter_kernel, dim3(items), dim3(tiled::THREADS), lds, stream, a, k);
+    if (a.U_out != nullptr)
+        hipLaunchKernelGGL(tiled::iter_kernel, dim3(items), dim3(tiled::THREADS), lds, stream, a, a.K);
+    return hipGetLastError();
+}
+
+}  // namespace dadmm

@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -38,6 +38,8 @@ EXPORTED_SYMBOLS = (
     "dadmm_gnn_step_backward",
     "dadmm_normal_offset_step",
     "dadmm_prologue",
+    "dadmm_tiled_scratch_bytes",
+    "dadmm_forward_tiled",
 )
 
 
@@ -99,6 +101,10 @@ def load() -> ctypes.CDLL:
     L.dadmm_normal_offset_step.argtypes = [i64]
     L.dadmm_prologue.restype = ctypes.c_int
     L.dadmm_prologue.argtypes = [u64, u64, i64, i32, i32, f32, f32, vp, vp, vp, vp, i64, vp]
+    L.dadmm_tiled_scratch_bytes.restype = ctypes.c_size_t
+    L.dadmm_tiled_scratch_bytes.argtypes = [D]
+    L.dadmm_forward_tiled.restype = ctypes.c_int
+    L.dadmm_forward_tiled.argtypes = [D] + [vp] * 14
     L.dadmm_gnn_flag_bytes.restype = ctypes.c_size_t
     L.dadmm_gnn_flag_bytes.argtypes = [i32]
     for name, args in (("dadmm_gnn_begin", [D] + [vp] * 7),

@@ -110,10 +110,11 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     """The K-step forward with the reference's NaN/Inf guards, enqueued on the current stream
     (no host synchronisation). Shapes: b [B,P,m], hyp [K,H,4], y0/U0/d0 [B,P,n].
 
-    path "auto": the fused kernel when the shape is compiled, followed by the device-gated
-    stepwise recomputation (runs only if the fused kernel flagged a guard event); otherwise the
-    stepwise kernels. "fused" / "stepwise" force one path ("fused" alone does NOT apply the
-    guards: its status only flags them).
+    path "auto": the fused kernel when the shape is compiled, otherwise the tiled kernel (one
+    launch per iteration); either is followed by the device-gated stepwise recomputation (runs only
+    if a guard event was flagged). Training (record) outside the fused shapes: the stepwise
+    kernels. "fused" / "tiled" / "stepwise" force one path ("fused" / "tiled" alone do NOT apply
+    the guards: their status only flags them).
 
     record: also store the trajectory the adjoint consumes (training; dadmm_forward_record).
 
@@ -126,7 +127,7 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     draw = y0 is None
     if draw != (U0 is None) or draw != (d0 is None):
         raise ValueError("pass all of y0, U0, d0 or none of them")
-    if path not in ("auto", "fused", "stepwise"):
+    if path not in ("auto", "fused", "tiled", "stepwise"):
         raise ValueError(f"unknown path {path!r}")
     B, P, m = b.shape
     if P != op.P or m != op.m:
@@ -150,11 +151,12 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
                          "P <= 8; use path='auto' or 'stepwise'")
     # one device allocation: [status word | 252 B pad | stepwise scratch (guard flags first)];
     # the prologue zeroes the status word and the flags in the same launch as the draws
-    nbytes = L.dadmm_stepwise_scratch_bytes(ctypes.byref(d)) if path != "fused" else 0
+    gated = path in ("auto", "stepwise")
+    nbytes = L.dadmm_stepwise_scratch_bytes(ctypes.byref(d)) if gated else 0
     words = torch.empty(256 + max(nbytes, 256), dtype=torch.uint8, device=b.device)
     status = words[:4].view(torch.int32)
     scratch = words[256:]
-    nzero = (256 + (_sw_flag_bytes(K) if path != "fused" else 0)) // 4
+    nzero = (256 + (_sw_flag_bytes(K) if gated else 0)) // 4
     if draw:
         y0, U0, d0 = draw_inits((B, P, op.n), b.device, ns, zero=words, nzero=nzero)
     else:
@@ -163,7 +165,7 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
                 0, 0, 0, 1, 1, 0.0, 0.0, None, None, None, _ptr(words), nzero, _stream(b.device)))
     with torch.cuda.device(b.device):
         stream = _stream(b.device)
-        fused = path != "stepwise" and graphs.fused_ok
+        fused = path in ("auto", "fused") and graphs.fused_ok
         if fused:
             if record:
                 rc = L.dadmm_forward_record(
@@ -179,8 +181,20 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
                 fused = False
             else:
                 _lib.check("dadmm_forward_record" if record else "dadmm_forward", rc)
-        if path != "fused":
-            gate = _lib.FLAGS_ZEROED | (_lib.GATE_ON if fused else 0)
+        tiled = path == "tiled" or (path == "auto" and not fused and not record)
+        if tiled:
+            tb = L.dadmm_tiled_scratch_bytes(ctypes.byref(d))
+            tscratch = torch.empty(max(tb, 256), dtype=torch.uint8, device=b.device)
+            rc = L.dadmm_forward_tiled(
+                ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.vptr), _ptr(graphs.vq),
+                _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U),
+                _ptr(status), _ptr(tscratch), stream)
+            if rc == _lib.DADMM_EUNSUPPORTED and path == "auto":
+                tiled = False
+            else:
+                _lib.check("dadmm_forward_tiled", rc)
+        if gated:
+            gate = _lib.FLAGS_ZEROED | (_lib.GATE_ON if (fused or tiled) else 0)
             _lib.check("dadmm_forward_stepwise", L.dadmm_forward_stepwise(
                 ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.vptr), _ptr(graphs.vq),
                 _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U),

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 5
+#define DADMM_ABI_VERSION 6
 
 enum {
     DADMM_OK = 0,
@@ -155,6 +155,23 @@ uint64_t dadmm_normal_offset_step(int64_t numel);
 int dadmm_prologue(uint64_t seed, uint64_t offset, int64_t numel, int32_t n, int32_t n_store,
                    float mean, float stddev, float* y0, float* U0, float* d0, int32_t* zero,
                    int64_t nzero, void* stream);
+
+/* Bytes of device scratch dadmm_forward_tiled needs for `d` (256-byte aligned pointer). */
+size_t dadmm_tiled_scratch_bytes(const dadmm_dims* d);
+
+/* The K-step forward, one launch per iteration with the state in HBM — the path for shapes the fused
+ * kernel cannot hold on chip (P > 6 or n > 256; e.g. P = 16, n = 512). Each (16-sample tile, agent)
+ * workgroup forms delta_k from its neighbours' y_k (visit lists, the reference's order), applies
+ * the deferred dual update, the factored gradient GEMM pair and the primal update; Y is
+ * bit-identical to dadmm_forward_stepwise's on guard-free inputs.
+ * Replaces: the same loop as dadmm_forward (unfolded_DLASSO.py:45, 53-109).
+ * Like dadmm_forward it only FLAGS the reference's guards in `status` (OR-ed; caller zeroes it):
+ * enqueue dadmm_forward_stepwise with DADMM_GATE_ON behind it for the exact guarded result.
+ * Graph: visit_ptr / visit_q / deg as dadmm_forward_stepwise. P <= 64, m <= 64, n % 4 == 0. */
+int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
+                        const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
+                        const float* hyp, const float* y0, const float* U0, const float* d0,
+                        float* Y, float* U_out, int32_t* status, void* scratch, void* stream);
 
 /* Bytes of device scratch dadmm_forward_stepwise needs for `d` (256-byte aligned pointer). */
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d);

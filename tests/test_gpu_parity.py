@@ -138,7 +138,7 @@ BIG_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("path", ["auto", "stepwise"])
+@pytest.mark.parametrize("path", ["auto", "stepwise", "tiled"])
 @pytest.mark.parametrize("P,m,n,B,K,prob,per_sample", SHAPES + BIG_SHAPES)
 def test_shapes_bit_exact(cuda, P, m, n, B, K, prob, per_sample, path):
     A, b, _ = O.make_problem(P, m, n, B, seed=P * 100 + n)
@@ -172,13 +172,14 @@ def test_same_mode_and_gnn_variant(cuda, path):
         assert np.array_equal(U, Uo)
 
 
-def test_nonfinite_inputs_are_flagged_by_the_fused_kernel(cuda):
+@pytest.mark.parametrize("path", ["fused", "tiled"])
+def test_nonfinite_inputs_are_flagged_by_the_fast_kernels(cuda, path):
     P, m, n, B, K = 3, 16, 64, 8, 3
     A, b, _ = O.make_problem(P, m, n, B, seed=1)
     G = O.er_graph(P, 0.5, seed=1)
     y0, U0, d0 = _inits(B, P, n)
     hyp = O.hyp_table(np.zeros((K, P, 4), np.float32), MAXP)
-    run = lambda *a: _run_hip(cuda, A, *a, path="fused")[2]   # noqa: E731
+    run = lambda *a: _run_hip(cuda, A, *a, path=path)[2]   # noqa: E731
     b2 = b.copy(); b2[3, 1, 2] = np.nan
     assert run(b2, [G] * B, hyp, y0, U0, d0) & 4
     y2 = y0.copy(); y2[0, 0, 0] = np.inf
@@ -227,6 +228,19 @@ def test_guards_bit_exact(cuda, path):
     for name, A, b, hyp, y0, U0, d0 in _guard_cases(P, m, n, B, K, seed=11):
         Y, U, st, _ = _run_hip(cuda, A, b, [G] * B, hyp, y0, U0, d0, path=path)
         Yo, Uo, sto = O.forward_f32(A, b, [G] * B, hyp, y0, U0, d0)
+        assert st == sto, (name, st, sto)
+        np.testing.assert_array_equal(Y, Yo, err_msg=name)
+        np.testing.assert_array_equal(U, Uo, err_msg=name)
+
+
+def test_guards_bit_exact_tiled_shapes(cuda):
+    """Shapes beyond the fused kernel (P = 9, n = 320): the tiled per-iteration kernel flags, the
+    gated persistent recomputation makes every guard exact."""
+    P, m, n, B, K = 9, 40, 320, 37, 5
+    graphs = [O.connected_er_graph(P, 0.4, seed=70 + s) for s in range(B)]
+    for name, A, b, hyp, y0, U0, d0 in _guard_cases(P, m, n, B, K, seed=13):
+        Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0, path="auto")
+        Yo, Uo, sto = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
         assert st == sto, (name, st, sto)
         np.testing.assert_array_equal(Y, Yo, err_msg=name)
         np.testing.assert_array_equal(U, Uo, err_msg=name)
