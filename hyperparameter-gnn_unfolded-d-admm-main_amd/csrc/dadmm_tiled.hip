@@ -55,33 +55,6 @@ constexpr int HALVES = 2;            // 16-sample MFMA column blocks per workgro
 constexpr int ST = HALVES * BT;      // samples per workgroup
 constexpr int VMAX = 128;            // visit-list entries cached per sample (2P <= 128)
 
-// delta_k rows n0..n0+3 of the lane's two samples (halves) for agent p: the sum over each
-// sample's visit list (in LDS) of (y_p - y_q) in list order; the neighbour loads of both samples
-// are issued together, four entries at a time (eight 16-B loads in flight per lane)
-__device__ __forceinline__ void consensus_rows2(const float* yk, const size_t (&srow)[2], int n,
-                                                int n0, const uint8_t* const (&vl)[2],
-                                                const int (&len)[2], const f32x4 (&yp)[2],
-                                                f32x4 (&acc)[2]) {
-    acc[0] = acc[1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-    const int L = len[0] > len[1] ? len[0] : len[1];
-    for (int t = 0; t < L; t += 4) {
-        f32x4 yq[2][4];
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (t + u < len[hh]) yq[hh][u] = *(const f32x4*)(yk + (srow[hh] + vl[hh][t + u]) * n + n0);
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (t + u < len[hh]) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[hh][r] = acc[hh][r] + (yp[hh][r] - yq[hh][u][r]);
-                }
-    }
-}
-
 // blockIdx -> (tile, agent) so that the P workgroups of one sample tile run on the same XCD
 // (dispatch is round-robin over the 8 XCDs, each with its own L2): the neighbour tiles a
 // workgroup reads for delta are its siblings' own tiles, hot in that L2.
@@ -163,23 +136,31 @@ __global__ __launch_bounds__(THREADS) void iter_kernel(TiledArgs a, int k) {
                 return (bok[hh] && 16 * t + 4 * h < n) ? *(const f32x4*)(brow[hh] + 16 * t)
                                                        : (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
             };
-            f32x4 av = *(const f32x4*)arow;
-            f32x4 bv[HALVES];
+            // operand ring of depth D: the loads of step t + D are issued after step t's MFMAs
+            // (NP / 16 is a multiple of 4)
+            constexpr int D = 4;
+            const int T = NP / 16;
+            f32x4 ar[D], br[D][HALVES];
 #pragma unroll
-            for (int hh = 0; hh < HALVES; ++hh) bv[hh] = ldb(hh, 0);
-            for (int t = 0; t < NP / 16; ++t) {
-                const bool more = t + 1 < NP / 16;
-                const f32x4 an = more ? *(const f32x4*)(arow + 16 * (t + 1)) : av;
-                f32x4 bn[HALVES];
+            for (int u = 0; u < D; ++u) {
+                ar[u] = *(const f32x4*)(arow + 16 * u);
 #pragma unroll
-                for (int hh = 0; hh < HALVES; ++hh) bn[hh] = more ? ldb(hh, t + 1) : bv[hh];
+                for (int hh = 0; hh < HALVES; ++hh) br[u][hh] = ldb(hh, u);
+            }
+            for (int t0 = 0; t0 < T; t0 += D) {
 #pragma unroll
-                for (int hh = 0; hh < HALVES; ++hh)
+                for (int u = 0; u < D; ++u) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[hh] = mfma4(av[r], bv[hh][r], acc[hh]);
-                av = an;
+                    for (int hh = 0; hh < HALVES; ++hh)
 #pragma unroll
-                for (int hh = 0; hh < HALVES; ++hh) bv[hh] = bn[hh];
+                        for (int r = 0; r < 4; ++r) acc[hh] = mfma4(ar[u][r], br[u][hh][r], acc[hh]);
+                    const int tn = t0 + u + D;
+                    if (tn < T) {
+                        ar[u] = *(const f32x4*)(arow + 16 * tn);
+#pragma unroll
+                        for (int hh = 0; hh < HALVES; ++hh) br[u][hh] = ldb(hh, tn);
+                    }
+                }
             }
         }
 #pragma unroll
@@ -221,79 +202,121 @@ __global__ __launch_bounds__(THREADS) void iter_kernel(TiledArgs a, int k) {
     }
     bool bad_u0 = false, bad_g = false, bad_y = false;
     const float* atbase = a.At + ((size_t)p * NP + j) * M_PAD + 4 * h;
-    for (int nb = w; nb < NP / 16; nb += WAVES) {
-        const int n0 = 16 * nb + 4 * h;
-        f32x4 atv[M_PAD / 16];
-        if (!final_only) {
+    // The wave's n-tiles nb = w, w + 4, ... are processed CH at a time; each chunk issues its
+    // loads together (y_k rows, U_{k-1} rows, A^T rows, and the neighbour rows of the consensus
+    // four visit-list entries at a time for all CH tiles x 2 samples): memory-level parallelism
+    // instead of one dependent round trip per tile.
+    constexpr int CH = 2;
+    constexpr int RG = CH * HALVES;            // row groups per chunk
+    const int ntw = (NP / 16 - w + WAVES - 1) / WAVES;   // tiles of this wave
+    size_t srow[HALVES];
+    const uint8_t* vl[HALVES];
+    int len[HALVES];
 #pragma unroll
-            for (int t = 0; t < M_PAD / 16; ++t) atv[t] = *(const f32x4*)(atbase + (size_t)16 * nb * M_PAD + 16 * t);
-        }
-        // this tile's rows of both samples: y_k, and (k > 0) delta_k from the neighbours
-        f32x4 ypv[HALVES], dvv[HALVES];
-        {
-            size_t srow[HALVES];
-            const uint8_t* vl[HALVES];
-            int len[HALVES];
+    for (int hh = 0; hh < HALVES; ++hh) {
+        const int s = tile * ST + hh * BT + j;
+        srow[hh] = (size_t)(s < B ? s : 0) * P;
+        vl[hh] = Vlds + (hh * BT + j) * VMAX;
+        len[hh] = (s < B && k > 0) ? vlen[hh] : 0;
+    }
+    const int L = len[0] > len[1] ? len[0] : len[1];
+    for (int c0 = 0; c0 < ntw; c0 += CH) {
+        int n0[CH];
+        bool okr[RG];
+        size_t off[RG];
+        f32x4 yp[RG], up[RG], dv[RG], uv[RG];
+        f32x4 atv[CH][M_PAD / 16];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int nb = w + WAVES * (c0 + i);
+            n0[i] = 16 * nb + 4 * h;
+            const bool tile_ok = c0 + i < ntw;
+            if (!final_only && tile_ok) {
+#pragma unroll
+                for (int t = 0; t < M_PAD / 16; ++t)
+                    atv[i][t] = *(const f32x4*)(atbase + (size_t)16 * nb * M_PAD + 16 * t);
+            }
 #pragma unroll
             for (int hh = 0; hh < HALVES; ++hh) {
+                const int g = i * HALVES + hh;
                 const int s = tile * ST + hh * BT + j;
-                const bool ok = s < B && n0 < n;
-                srow[hh] = (size_t)(ok ? s : 0) * P;
-                vl[hh] = Vlds + (hh * BT + j) * VMAX;
-                len[hh] = ok && k > 0 ? vlen[hh] : 0;
-                ypv[hh] = ok ? *(const f32x4*)(yk + (srow[hh] + p) * n + n0) : (f32x4){0, 0, 0, 0};
+                okr[g] = tile_ok && s < B && n0[i] < n;
+                off[g] = (srow[hh] + p) * n + n0[i];
+                yp[g] = up[g] = dv[g] = (f32x4){0, 0, 0, 0};
+                if (okr[g]) {
+                    yp[g] = *(const f32x4*)(yk + off[g]);
+                    up[g] = *(const f32x4*)((k == 0 ? a.U0 : Uprev) + off[g]);
+                    if (k == 0) dv[g] = *(const f32x4*)(a.d0 + off[g]);
+                }
             }
-            consensus_rows2(yk, srow, n, n0, vl, len, ypv, dvv);
+        }
+        // delta_k: visit lists in order, 4 entries x RG row groups of loads in flight
+        for (int t = 0; t < L; t += 4) {
+            f32x4 yq[4][RG];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int g = 0; g < RG; ++g) {
+                    const int hh = g % HALVES, i = g / HALVES;
+                    if (okr[g] && t + u < len[hh])
+                        yq[u][g] = *(const f32x4*)(yk + (srow[hh] + vl[hh][t + u]) * n + n0[i]);
+                }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int g = 0; g < RG; ++g) {
+                    const int hh = g % HALVES;
+                    if (okr[g] && t + u < len[hh]) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) dv[g][r] = dv[g][r] + (yp[g][r] - yq[u][g][r]);
+                    }
+                }
         }
 #pragma unroll
-        for (int hh = 0; hh < HALVES; ++hh) {
-            const int s = tile * ST + hh * BT + j;
-            const bool ok = s < B && n0 < n;
-            const size_t off = ((size_t)s * P + p) * n + n0;
-            // delta_k and U_k of these 4 rows
-            f32x4 dv = {0, 0, 0, 0}, uv = {0, 0, 0, 0};
-            if (ok) {
-                if (k == 0) {
-                    dv = *(const f32x4*)(a.d0 + off);
-                    uv = *(const f32x4*)(a.U0 + off);
+        for (int g = 0; g < RG; ++g) {
+            if (!okr[g]) continue;
+            if (k == 0) {
+                uv[g] = up[g];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) bad_u0 |= !finitef(uv[r]);
-                } else {
-                    dv = dvv[hh];
-                    if (a.variant != 0) {
+                for (int r = 0; r < 4; ++r) bad_u0 |= !finitef(uv[g][r]);
+            } else {
+                if (a.variant != 0) {
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) dv[r] = tclamp(dv[r], -20.0f, 20.0f);   // :229
-                    }
-                    const f32x4 up = *(const f32x4*)(Uprev + off);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) uv[r] = tclamp(up[r] + dv[r] * et_prev, -vclip_prev, vclip_prev);
+                    for (int r = 0; r < 4; ++r) dv[g][r] = tclamp(dv[g][r], -20.0f, 20.0f);   // :229
                 }
-                *(f32x4*)(Ucur + off) = uv;             // U_k (the ping-pong buffer / U_out)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    uv[g][r] = tclamp(up[g][r] + dv[g][r] * et_prev, -vclip_prev, vclip_prev);
             }
-            if (final_only) continue;
-            // GEMM2 rows of this tile + gradient assembly + primal update (:69-93)
+            *(f32x4*)(Ucur + off[g]) = uv[g];          // U_k (the ping-pong buffer / U_out)
+        }
+        if (final_only) continue;
+        // GEMM2 rows of these tiles + gradient assembly + primal update (:69-93)
+#pragma unroll
+        for (int g = 0; g < RG; ++g) {
+            const int hh = g % HALVES, i = g / HALVES;
+            if (c0 + i >= ntw) continue;
             f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
             for (int t = 0; t < M_PAD / 16; ++t)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) gc = mfma4(atv[t][r], rv[hh][t][r], gc);
-            if (ok) {
-                const f32x4 yv = ypv[hh];
+                for (int r = 0; r < 4; ++r) gc = mfma4(atv[i][t][r], rv[hh][t][r], gc);
+            if (okr[g]) {
                 f32x4 yn;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float y = yv[r];
+                    const float y = yp[g][r];
                     const float st = y > 0.0f ? ta : (y < 0.0f ? -ta : 0.0f);   // sign(y) * tau
-                    float g = gc[r] + st;
-                    g = g + uv[r] * dg[hh];
-                    g = g + dv[r] * rh;
-                    bad_g |= g != g;
-                    g = tclamp(g, -gclip, gclip);
-                    const float v = tclamp(y - al * g, -vclip, vclip);
+                    float gr = gc[r] + st;
+                    gr = gr + uv[g][r] * dg[hh];
+                    gr = gr + dv[g][r] * rh;
+                    bad_g |= gr != gr;
+                    gr = tclamp(gr, -gclip, gclip);
+                    const float v = tclamp(y - al * gr, -vclip, vclip);
                     bad_y |= !finitef(v);
                     yn[r] = v;
                 }
-                *(f32x4*)(a.Y + (size_t)k * S + off) = yn;
+                *(f32x4*)(a.Y + (size_t)k * S + off[g]) = yn;
             }
         }
     }
