@@ -498,6 +498,58 @@ int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
     return ok();
 }
 
+size_t dadmm_loss_scratch_bytes(int32_t K, int64_t rows, int32_t n) {
+    if (K < 1 || rows < 0 || n < 1) return 0;
+    return 4 * dadmm::loss_scratch_floats(K, rows, n);
+}
+
+static int loss_args(int32_t K, int32_t B, int32_t P, int32_t n, int32_t n_store, const float* Y,
+                     const float* label, dadmm::LossArgs* a) {
+    if (K < 1 || B < 1 || P < 1 || n < 1 || n_store < n)
+        return fail(DADMM_EINVAL, "bad loss dims K=%d B=%d P=%d n=%d n_store=%d", K, B, P, n, n_store);
+    if (!Y || !label) return fail(DADMM_EINVAL, "Y/label is NULL");
+    if ((int64_t)B * P * n_store >= ((int64_t)1 << 31))
+        return fail(DADMM_EUNSUPPORTED, "B*P*n_store >= 2^31 values per layer");
+    *a = dadmm::LossArgs{};
+    a->Y = Y;
+    a->label = label;
+    a->K = K;
+    a->P = P;
+    a->n = n;
+    a->n_store = n_store;
+    a->rows = (int64_t)B * P;
+    return DADMM_OK;
+}
+
+int dadmm_loss(int32_t K, int32_t B, int32_t P, int32_t n, int32_t n_store, const float* Y,
+               const float* label, float* losses, float* out, int32_t* flags, void* scratch,
+               void* stream) {
+    dadmm::LossArgs a;
+    int rc = loss_args(K, B, P, n, n_store, Y, label, &a);
+    if (rc) return rc;
+    if (!losses || !out || !flags || !scratch) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    a.partial = (float*)scratch;
+    a.losses = losses;
+    a.out = out;
+    a.flags = flags;
+    hipError_t e = dadmm::launch_loss(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "loss launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_loss_grad(int32_t K, int32_t B, int32_t P, int32_t n, int32_t n_store, const float* Y,
+                    const float* label, const int32_t* flags, const float* gout, float* dY,
+                    void* stream) {
+    dadmm::LossArgs a;
+    int rc = loss_args(K, B, P, n, n_store, Y, label, &a);
+    if (rc) return rc;
+    if (!flags || !gout || !dY) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    a.flags = const_cast<int32_t*>(flags);
+    hipError_t e = dadmm::launch_loss_grad(a, gout, dY, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "loss grad launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;
     const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);

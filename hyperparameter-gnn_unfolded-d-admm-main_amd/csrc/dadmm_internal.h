@@ -132,6 +132,21 @@ struct TiledArgs {
 size_t tiled_lds_bytes(int n_pad);
 hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream);
 
+// ---- fused loss (dadmm_loss.hip) ----------------------------------------------------------------
+struct LossArgs {
+    const float* Y;         // [K][rows][n_store], rows = B * P
+    const float* label;     // [B][n]
+    float* partial;         // scratch: loss_scratch_floats(K, rows, n)
+    float* losses;          // [K] per-layer losses (nullable)
+    float* out;             // [2]: loss_mean, loss_final
+    int32_t* flags;         // [2]: non-finite seen, fallback fired
+    int K, P, n, n_store;
+    int64_t rows;
+};
+size_t loss_scratch_floats(int K, int64_t rows, int n);
+hipError_t launch_loss(const LossArgs& a, hipStream_t st);
+hipError_t launch_loss_grad(const LossArgs& a, const float* gout, float* dY, hipStream_t st);
+
 // ---- forward prologue (dadmm_rng.hip) -----------------------------------------------------------
 struct PrologueArgs {
     uint64_t seed, offset, offset_step;   // torch Philox state; per-tensor offset increment

@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -40,6 +40,9 @@ EXPORTED_SYMBOLS = (
     "dadmm_prologue",
     "dadmm_tiled_scratch_bytes",
     "dadmm_forward_tiled",
+    "dadmm_loss_scratch_bytes",
+    "dadmm_loss",
+    "dadmm_loss_grad",
 )
 
 
@@ -105,6 +108,12 @@ def load() -> ctypes.CDLL:
     L.dadmm_tiled_scratch_bytes.argtypes = [D]
     L.dadmm_forward_tiled.restype = ctypes.c_int
     L.dadmm_forward_tiled.argtypes = [D] + [vp] * 14
+    L.dadmm_loss_scratch_bytes.restype = ctypes.c_size_t
+    L.dadmm_loss_scratch_bytes.argtypes = [i32, i64, i32]
+    L.dadmm_loss.restype = ctypes.c_int
+    L.dadmm_loss.argtypes = [i32] * 5 + [vp] * 7
+    L.dadmm_loss_grad.restype = ctypes.c_int
+    L.dadmm_loss_grad.argtypes = [i32] * 5 + [vp] * 6
     L.dadmm_gnn_flag_bytes.restype = ctypes.c_size_t
     L.dadmm_gnn_flag_bytes.argtypes = [i32]
     for name, args in (("dadmm_gnn_begin", [D] + [vp] * 7),

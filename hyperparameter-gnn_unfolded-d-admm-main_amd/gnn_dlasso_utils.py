@@ -40,7 +40,13 @@ def compute_loss(Y, label):
     """Y [K,B,P,n,1], label [B,n,1] -> (loss_mean, loss_final) as 0-dim tensors.
 
     Returns (1.0, 1.0) if Y, the label or any layer loss is non-finite (reference :36-43,
-    :69-71, :83-86)."""
+    :69-71, :83-86). Iterates in the HIP forward's layout go through the fused loss kernels
+    (dadmm_hip.loss: one pass forward, one pass for dL/dY); anything else (e.g. CPU tensors)
+    through the same formula in torch."""
+    from dadmm_hip.loss import fused_compute_loss
+    fused = fused_compute_loss(Y, label)
+    if fused is not None:
+        return fused
     losses = layer_losses(Y, label)
     ok = torch.isfinite(Y).all() & torch.isfinite(label).all() & torch.isfinite(losses).all()
     one = torch.ones((), dtype=losses.dtype, device=losses.device)

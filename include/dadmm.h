@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 6
+#define DADMM_ABI_VERSION 7
 
 enum {
     DADMM_OK = 0,
@@ -254,6 +254,24 @@ int dadmm_gnn_step_backward(const dadmm_dims* d, int32_t k, const int32_t* visit
                             const float* D, const float* gy1, const float* gU1, const float* gd1,
                             float* gy, float* gU, float* gd, float* gAtAy, float* ghyp,
                             void* stream);
+
+/* ---- the drivers' loss, fused ----------------------------------------------------------------
+ * gnn_dlasso_utils.compute_loss (gnn_dlasso_utils.py:27-88) on the iterates Y [K][B*P][n_store]
+ * (row stride n_store >= n; padding columns ignored) and label [B][n]:
+ *   losses[k] = sum_{b,p,c} (Y[k,b,p,c] - label[b,c])^2 / (B P n),
+ *   out = (mean_k losses + 1e-8, losses[K-1] + 1e-8), or (1, 1) when Y, the label or a loss is
+ *   non-finite (flags[1] = 1 then). Deterministic (fixed-order sums). No host synchronisation.
+ * Replaces: compute_loss's K*P F.mse_loss calls and its NaN/Inf checks. */
+size_t dadmm_loss_scratch_bytes(int32_t K, int64_t rows, int32_t n);
+int dadmm_loss(int32_t K, int32_t B, int32_t P, int32_t n, int32_t n_store, const float* Y,
+               const float* label, float* losses, float* out, int32_t* flags, void* scratch,
+               void* stream);
+/* dL/dY of dadmm_loss for the upstream gradients gout = (dL/dloss_mean, dL/dloss_final) (device
+ * [2]): dY[k] = (gout[0]/K + [k == K-1] gout[1]) * 2 (Y[k] - label) / (B P n), 0 in padding
+ * columns and when the fallback fired (flags from dadmm_loss). dY: [K][B*P][n_store]. */
+int dadmm_loss_grad(int32_t K, int32_t B, int32_t P, int32_t n, int32_t n_store, const float* Y,
+                    const float* label, const int32_t* flags, const float* gout, float* dY,
+                    void* stream);
 
 #ifdef __cplusplus
 }
