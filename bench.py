@@ -284,10 +284,39 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
             with torch.no_grad():
                 gnn(bg, graphs)
         ms = _event_ms(gfwd, 3, warm=1)
+        gnn.hyper_backend = "torch"
+        ms_torch = _event_ms(gfwd, 2, warm=1)
+        gnn.hyper_backend = "auto"
         out["gnn_forward"] = {"B": Bg, "P": P, "n": n, "m": m, "K": K, "hidden": 100, "ms": ms,
-                              "units_per_s": Bg * K / (ms * 1e-3)}
+                              "units_per_s": Bg * K / (ms * 1e-3),
+                              "hypernetwork": "fused HIP (dadmm_hyper_*)",
+                              "ms_torch_hypernetwork": ms_torch}
     except Exception as e:
         out["gnn_error"] = repr(e)[:300]
+    try:
+        # BASELINE configs[4]'s per-GPU shard of the GNN model: P=50, n=1024, m=32, K=50,
+        # B=8192/8 per GPU, graph_prob 0.5, h=100 (eval forward, fused hypernetwork)
+        import argparse as _ap
+
+        import gnn_dlasso_models_progressive as GM
+        P5, n5, m5, B5, K5 = 50, 1024, 32, 1024, 50
+        A5, b5, _ = O.make_problem(P5, m5, n5, B5, seed=55)
+        args5 = _ap.Namespace(GHN_iter_num=K5, GHyp_hidden=100, DADMM_mode="diff", alpha_max=0.1,
+                              tau_max=0.99, rho_max=0.99, eta_max=0.99)
+        g5 = GM.DLASSO_GNNHyp3_Progressive(torch.from_numpy(A5)[None].to(dev), args5).to(dev).eval()
+        graphs5 = [O.connected_er_graph(P5, 0.5, seed=500 + s) for s in range(B5)]
+        b5t = torch.from_numpy(b5)[..., None].to(dev)
+
+        def g5fwd():
+            with torch.no_grad():
+                g5(b5t, graphs5)
+        ms5 = _event_ms(g5fwd, 1, warm=1)
+        out["c5_gnn_forward"] = {"B": B5, "P": P5, "n": n5, "m": m5, "K": K5, "hidden": 100,
+                                 "graph_prob": 0.5, "ms": ms5,
+                                 "units_per_s": B5 * K5 / (ms5 * 1e-3)}
+        del g5, b5t
+    except Exception as e:
+        out["c5_error"] = repr(e)[:300]
     try:
         import unfolded_DLASSO
         P3, n3, m3, B3, K3 = 16, 512, 64, 4096, 25

@@ -550,6 +550,148 @@ int dadmm_loss_grad(int32_t K, int32_t B, int32_t P, int32_t n, int32_t n_store,
     return ok();
 }
 
+static int hyper_input(int32_t rows, int32_t K, int32_t N, const float* x1, int32_t ld1, int32_t K1,
+                       const float* x2, int32_t ld2, const float* W, const float* y, int32_t ldy,
+                       dadmm::HyperArgs* a) {
+    if (rows < 0 || K < 1 || N < 1 || K1 < 1 || K1 > K)
+        return fail(DADMM_EINVAL, "bad linear dims rows=%d K=%d N=%d K1=%d", rows, K, N, K1);
+    if (!x1 || !W || !y || (K1 < K && !x2)) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if ((K & 3) || (K1 & 3) || (ld1 & 3) || (K1 < K && (ld2 & 3)) || ld1 < K1 ||
+        (K1 < K && ld2 < K - K1) || ldy < N)
+        return fail(DADMM_EUNSUPPORTED, "K, K1 and the input row strides must be multiples of 4 "
+                    "(K=%d K1=%d ld1=%d ld2=%d, ldy=%d >= N=%d)", K, K1, ld1, ld2, ldy, N);
+    if (K1 < K && (K1 & 15))
+        return fail(DADMM_EUNSUPPORTED, "a split input needs K1 %% 16 == 0 (K1=%d)", K1);
+    if (!aligned16(x1) || (x2 && !aligned16(x2)) || !aligned16(W))
+        return fail(DADMM_EINVAL, "x1, x2 and W must be 16-byte aligned");
+    if ((int64_t)rows * (ld1 > ld2 ? ld1 : ld2) >= ((int64_t)1 << 31) ||
+        (int64_t)rows * ldy >= ((int64_t)1 << 31))
+        return fail(DADMM_EUNSUPPORTED, "operand larger than 2^31 floats");
+    *a = dadmm::HyperArgs{};
+    a->x1 = x1;
+    a->x2 = x2;
+    a->ld1 = ld1;
+    a->ld2 = ld2;
+    a->K1 = K1;
+    a->W = W;
+    a->y = const_cast<float*>(y);
+    a->ldy = ldy;
+    a->rows = rows;
+    a->K = K;
+    a->N = N;
+    return DADMM_OK;
+}
+
+int dadmm_hyper_linear(int32_t rows, int32_t K, int32_t N, const float* x1, int32_t ld1,
+                       int32_t K1, const float* x2, int32_t ld2, const float* W, const float* bias,
+                       float* y, int32_t ldy, void* stream) {
+    dadmm::HyperArgs a;
+    int rc = hyper_input(rows, K, N, x1, ld1, K1, x2, ld2, W, y, ldy, &a);
+    if (rc) return rc;
+    a.bias = bias;
+    a.P = 1;
+    a.B = rows;
+    a.splits = 1;
+    hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_BIAS, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "linear launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_hyper_gcn(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1, int32_t ld1,
+                    int32_t K1, const float* x2, int32_t ld2, const float* W, const float* bias,
+                    const float* ahat, int32_t ahat_per_sample, const float* bn_mean,
+                    const float* bn_var, const float* bn_weight, const float* bn_bias, float bn_eps,
+                    float slope, float* y, int32_t ldy, void* stream) {
+    if (B < 0 || P < 1 || P > 64) return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d", B, P);
+    dadmm::HyperArgs a;
+    int rc = hyper_input(B * P, K, N, x1, ld1, K1, x2, ld2, W, y, ldy, &a);
+    if (rc) return rc;
+    if (!bias || !ahat || !bn_mean || !bn_var || !bn_weight || !bn_bias)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    a.bias = bias;
+    a.B = B;
+    a.P = P;
+    a.ahat = ahat;
+    a.ahat_per_sample = ahat_per_sample ? 1 : 0;
+    a.bn_mean = bn_mean;
+    a.bn_var = bn_var;
+    a.bn_w = bn_weight;
+    a.bn_b = bn_bias;
+    a.bn_eps = bn_eps;
+    a.slope = slope;
+    hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_GCN, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "gcn launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_hyper_head(int32_t B, int32_t K, int32_t H, const float* x, int32_t ldx, const float* W,
+                     const float* bias, float alpha_max, float tau_max, float rho_max,
+                     float eta_max, float* hyp, void* stream) {
+    if (H < 1) return fail(DADMM_EINVAL, "bad head rows H=%d", H);
+    dadmm::HyperArgs a;
+    int rc = hyper_input(B, K, 4 * H, x, ldx, K, nullptr, 0, W, hyp, 4 * H, &a);
+    if (rc) return rc;
+    if (!bias) return fail(DADMM_EINVAL, "bias is NULL");
+    a.bias = bias;
+    a.P = 1;
+    a.B = B;
+    a.H = H;
+    a.maxv[0] = alpha_max;
+    a.maxv[1] = tau_max;
+    a.maxv[2] = rho_max;
+    a.maxv[3] = eta_max;
+    hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_HEAD, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "head launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_hyper_rownorm(int32_t rows, int32_t C, const float* x, const float* weight,
+                        const float* bias, float eps, int32_t act, float slope, float* y,
+                        void* stream) {
+    if (rows < 0 || C < 1) return fail(DADMM_EINVAL, "bad rownorm dims rows=%d C=%d", rows, C);
+    if ((C & 3) || C > 2048) return fail(DADMM_EUNSUPPORTED, "rownorm needs C %% 4 == 0, C <= 2048 (C=%d)", C);
+    if (!x || !weight || !bias || !y) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(x) || !aligned16(weight) || !aligned16(bias) || !aligned16(y))
+        return fail(DADMM_EINVAL, "rownorm operands must be 16-byte aligned");
+    dadmm::RowNormArgs a{x, weight, bias, y, rows, C, act ? 1 : 0, eps, slope, 1, 0, nullptr};
+    hipError_t e = dadmm::launch_rownorm(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "rownorm launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+size_t dadmm_hyper_linear_ln_scratch_bytes(int32_t rows, int32_t K, int32_t N) {
+    if (rows < 0 || K < 1 || N < 1) return 0;
+    return 4 * (size_t)dadmm::hyper_linear_splits(rows, K, N) * rows * N;
+}
+
+int dadmm_hyper_linear_ln(int32_t rows, int32_t K, int32_t N, const float* x, int32_t ldx,
+                          const float* W, const float* bias, const float* ln_weight,
+                          const float* ln_bias, float eps, int32_t act, float slope, float* y,
+                          void* scratch, void* stream) {
+    dadmm::HyperArgs a;
+    int rc = hyper_input(rows, K, N, x, ldx, K, nullptr, 0, W, y, N, &a);
+    if (rc) return rc;
+    if ((N & 3) || N > 2048) return fail(DADMM_EUNSUPPORTED, "LayerNorm width N=%d: N %% 4 == 0, N <= 2048", N);
+    if (!bias || !ln_weight || !ln_bias || !scratch) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(scratch) || !aligned16(y) || !aligned16(bias) || !aligned16(ln_weight) ||
+        !aligned16(ln_bias))
+        return fail(DADMM_EINVAL, "y, scratch, bias and the LayerNorm parameters must be 16-byte aligned");
+    if (rows == 0) return ok();
+    a.splits = dadmm::hyper_linear_splits(rows, K, N);
+    a.split_stride = (size_t)rows * N;
+    a.y = (float*)scratch;
+    a.ldy = N;
+    a.P = 1;
+    a.B = rows;
+    hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_BIAS, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "linear launch: %s", hipGetErrorString(e));
+    dadmm::RowNormArgs r{(const float*)scratch, ln_weight, ln_bias, y, rows, N, act ? 1 : 0, eps,
+                         slope, a.splits, a.split_stride, bias};
+    e = dadmm::launch_rownorm(r, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "rownorm launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;
     const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);

@@ -202,51 +202,100 @@ __global__ __launch_bounds__(THREADS) void grad_kernel(GnnArgs a, int k) {
 }
 
 // ---- update: primal update, consensus and dual update of (sample, 64 columns) (:221-232) -------
+// One wave per (sample, 64 columns); the item is wave-uniform, so the visit lists and the
+// hyper-parameters are scalar loads. The per-agent global loads are issued UP_CH agents at a time
+// (memory-level parallelism for large P: P = 50 at BASELINE configs[4]); the sample's visit lists
+// are staged in LDS next to y_{k+1}.
+constexpr int UP_CH = 8;
+// LDS words for one sample's visit lists: at most 2 P entries per agent (each incident edge is
+// visited from both of its ends; a self-loop twice), one byte each
+__host__ __device__ constexpr int update_visit_words(int P) { return (2 * P * P + 3) / 4; }
 __global__ __launch_bounds__(THREADS) void update_kernel(GnnArgs a, int k, int items) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int item = blockIdx.x * WAVES + (threadIdx.x >> 6);
+    const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + (threadIdx.x >> 6));
     if (item >= items) return;
     const int P = a.P, n = a.n;
     const int nch = (n + 63) / 64;
-    const int s = item / nch, c = (item % nch) * 64 + (threadIdx.x & 63);
+    const int s = item / nch, lane = threadIdx.x & 63;
+    const int c = (item % nch) * 64 + lane;
     const bool cv = c < n;
-    const size_t base = (size_t)s * P * n + c;
+    const size_t base = (size_t)s * P * n + (cv ? c : 0);
     bool yzero = false;
-    const float* ys = y_source(a, k, yzero);
+    const float* __restrict__ ys = y_source(a, k, yzero);
     const bool gzero = flag_ld(a.flags + GNN_F_GBAD(k)) != 0;
     const bool uzero = flag_ld(a.flags + GNN_F_UBAD(k)) != 0;
     float gclip, vclip;
     clips(a, k, gclip, vclip);
-    float* yl = lds + (threadIdx.x >> 6) * (P * 64);
-    const int lane = threadIdx.x & 63;
-    float* Yk = a.yptr[k + 1];
-    bool bad_y = false;
-    for (int p = 0; p < P; ++p) {
-        float v = 0.0f;
-        if (cv) {
-            const float g = gzero ? 0.0f : a.G[base + (size_t)p * n];        // :216-218
-            const float y = yzero ? 0.0f : ys[base + (size_t)p * n];
-            v = clamp_t(y - hyp_at(a, s, 0, p) * g, -vclip, vclip);         // :221-225
-            Yk[base + (size_t)p * n] = v;
-            bad_y |= !finitef(v);
-        }
-        yl[p * 64 + lane] = v;
-    }
+    // per-wave LDS: y_{k+1} rows [P][64], then the sample's visit lists
+    float* yl = lds + (threadIdx.x >> 6) * (P * 64 + update_visit_words(P));
+    uint8_t* vl = (uint8_t*)(yl + P * 64);
     const int g0 = a.graph_shared ? 0 : s * P;
+    const int vb = a.vptr[g0], vlen = a.vptr[g0 + P] - vb;
+    for (int i = lane; i < vlen; i += 64) vl[i] = a.vq[vb + i];
+    const float* __restrict__ G = a.G;
+    const float* __restrict__ U = a.U;
+    float* __restrict__ Yk = a.yptr[k + 1];
+    bool bad_y = false;
+    for (int p0 = 0; p0 < P; p0 += UP_CH) {
+        float gv[UP_CH], yv[UP_CH];
+#pragma unroll
+        for (int u = 0; u < UP_CH; ++u) {
+            const int p = p0 + u;
+            gv[u] = 0.0f;
+            yv[u] = 0.0f;
+            if (p < P && cv) {
+                if (!gzero) gv[u] = G[base + (size_t)p * n];                 // :216-218
+                if (!yzero) yv[u] = ys[base + (size_t)p * n];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UP_CH; ++u) {
+            const int p = p0 + u;
+            if (p >= P) break;
+            float v = 0.0f;
+            if (cv) {
+                v = clamp_t(yv[u] - hyp_at(a, s, 0, p) * gv[u], -vclip, vclip);   // :221-225
+                Yk[base + (size_t)p * n] = v;
+                bad_y |= !finitef(v);
+            }
+            yl[p * 64 + lane] = v;
+        }
+    }
     bool bad_u = false;
-    for (int p = 0; p < P; ++p) {
-        const float yp = yl[p * 64 + lane];
-        float acc = 0.0f;
-        const int t1 = a.vptr[g0 + p + 1];
-        for (int t = a.vptr[g0 + p]; t < t1; ++t) acc = acc + (yp - yl[(int)a.vq[t] * 64 + lane]);
-        if (a.variant != 0) acc = clamp_t(acc, -20.0f, 20.0f);             // :229
-        if (cv) {
-            const size_t off = base + (size_t)p * n;
-            const float u = uzero ? 0.0f : a.U[off];
-            const float un = clamp_t(u + acc * hyp_at(a, s, 3, p), -vclip, vclip);   // :231-232
-            a.U_next[off] = un;
-            a.D_next[off] = acc;
-            bad_u |= !finitef(un);
+    for (int p0 = 0; p0 < P; p0 += UP_CH) {
+        float uv[UP_CH];
+#pragma unroll
+        for (int u = 0; u < UP_CH; ++u) {
+            const int p = p0 + u;
+            uv[u] = (p < P && cv && !uzero) ? U[base + (size_t)p * n] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < UP_CH; ++u) {
+            const int p = p0 + u;
+            if (p >= P) break;
+            const float yp = yl[p * 64 + lane];
+            float acc = 0.0f;
+            // the agent's visit list from LDS, four entries' y reads in flight, summed in order
+            const uint8_t* vp = vl + (a.vptr[g0 + p] - vb);
+            const int len = a.vptr[g0 + p + 1] - a.vptr[g0 + p];
+            int t = 0;
+            for (; t + 4 <= len; t += 4) {
+                const float y0 = yl[(int)vp[t] * 64 + lane], y1 = yl[(int)vp[t + 1] * 64 + lane];
+                const float y2 = yl[(int)vp[t + 2] * 64 + lane], y3 = yl[(int)vp[t + 3] * 64 + lane];
+                acc = acc + (yp - y0);
+                acc = acc + (yp - y1);
+                acc = acc + (yp - y2);
+                acc = acc + (yp - y3);
+            }
+            for (; t < len; ++t) acc = acc + (yp - yl[(int)vp[t] * 64 + lane]);
+            if (a.variant != 0) acc = clamp_t(acc, -20.0f, 20.0f);             // :229
+            if (cv) {
+                const size_t off = base + (size_t)p * n;
+                const float un = clamp_t(uv[u] + acc * hyp_at(a, s, 3, p), -vclip, vclip);   // :231-232
+                a.U_next[off] = un;
+                a.D_next[off] = acc;
+                bad_u |= !finitef(un);
+            }
         }
     }
     flag_or(a.flags + GNN_F_YNB(k), bad_y);
@@ -418,9 +467,15 @@ hipError_t gnn_launch_step(const GnnArgs& a, int k, hipStream_t st) {
     const int g = grid_for((size_t)a.B * a.P * a.n / 4, gnn::THREADS, 4096);
     hipLaunchKernelGGL(gnn::grad_kernel, dim3(g), dim3(gnn::THREADS), 0, st, a, k);
     const int items = a.B * ((a.n + 63) / 64);
-    const size_t lds = 4 * (size_t)gnn::WAVES * a.P * 64;
-    hipLaunchKernelGGL(gnn::update_kernel, dim3((items + gnn::WAVES - 1) / gnn::WAVES),
-                       dim3(gnn::THREADS), lds, st, a, k, items);
+    const size_t lds = 4 * (size_t)gnn::WAVES * (a.P * 64 + gnn::update_visit_words(a.P));
+    auto kern = gnn::update_kernel;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3((items + gnn::WAVES - 1) / gnn::WAVES), dim3(gnn::THREADS), lds, st,
+                       a, k, items);
     return hipGetLastError();
 }
 

@@ -1,0 +1,442 @@
+// dadmm_hyper.hip — the GNN hypernetwork of DLASSO_GNNHyp3_Progressive, inference mode, as
+// f32 MFMA GEMMs with fused epilogues (gnn_dlasso_models_progressive.py:9-72 GNNHypernetwork3,
+// :93-123 decoder / fc, :165-196 the hyper-parameter head).
+//
+// Per iteration the hypernetwork is (B samples of P nodes, h = GHyp_hidden):
+//   x0 = cat(AtAy_k, Atb)                         [B*P, 2n]
+//   x_i = BN_i(leaky(A_hat (x_{i-1} W_i^T) + b_i))  i = 1..5   (GCNConv -> leaky_relu -> bn_i;
+//                                                   Dropout is the identity in eval mode)
+//   e = LayerNorm(x_5)                            per node, 4h
+//   d = LReLU(LN(e.view(B, P*4h) D1^T + c1)) ... three decoder blocks
+//   hyp = head(sigmoid(d fc^T + f))               clamp [1e-4, 0.9999], * max, clamp <= 0.9999
+// The reference runs it per sample through torch_geometric (from_networkx + GCNConv) in a Python
+// loop; here every stage is ONE launch over the whole batch:
+//   linear_kernel<MB, EPI_GCN>  : Z = X W^T on v_mfma_f32_16x16x4_f32 (exact f32 fma chains), then
+//                                 in the epilogue, per sample, the normalised-adjacency mix
+//                                 sum_q A_hat[p][q] Z[q] + bias, leaky_relu, BatchNorm (running
+//                                 statistics) — the tile holds whole samples, so the mix never
+//                                 leaves the workgroup;
+//   linear_kernel<MB, EPI_BIAS> : decoder linears;
+//   linear_kernel<MB, EPI_HEAD> : fc + sigmoid + clamps + maxima, written as hyp_k [B][4][H]
+//                                 (the reference's view(B, 4, H) layout);
+//   rownorm_kernel              : LayerNorm (+ LeakyReLU) of every row, one wave per row.
+// Tile: 16*MB rows (whole samples for the GCN epilogue) x 64 output columns, 4 waves (one
+// 16-column block each, all MB row blocks); operands stream from L2 through a register ring.
+// Numerics: f32 throughout; results match torch's eager hypernetwork to f32 rounding (the sums
+// run in a different order than hipBLASLt's), not bit-for-bit.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dadmm_internal.h"
+
+namespace dadmm {
+namespace hyper {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int THREADS = 256;
+constexpr int TN = 64;            // output columns per workgroup (4 waves x 16)
+constexpr int ZS = TN + 4;        // LDS row stride of the GCN epilogue tile (float4 rows)
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// Ablation knobs (timing builds only, never shipped): operand loads replaced by register values
+#ifdef HYPER_ABL_A_CONST
+#define HYPER_ABL_A(v) ((f32x4){(float)t, 0.5f, 0.25f, 0.125f})
+#else
+#define HYPER_ABL_A(v) (v)
+#endif
+#ifdef HYPER_ABL_W_CONST
+#define HYPER_ABL_W(v) ((f32x4){(float)u, 0.5f, 0.25f, 0.125f})
+#else
+#define HYPER_ABL_W(v) (v)
+#endif
+// scheduling barrier: pins where the ring's loads issue (between the steps' MFMAs)
+__device__ __forceinline__ void mem_fence() { __builtin_amdgcn_sched_barrier(0); }
+
+// XCD-aware tile order: the dispatcher deals blocks round-robin over the 8 XCDs (each with its
+// own L2); consecutive tile numbers — the column tiles of one row tile, which read the same input
+// rows — are given to blocks of one XCD.
+__device__ __forceinline__ int xcd_tile(int bid, int G) {
+    constexpr int NX = 8;
+    const int xcd = bid % NX, i = bid / NX, q = G / NX, r = G % NX;
+    return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
+}
+
+// Workgroup tile: 32 WR rows x 64 columns, 4 waves in a 2 x 2 layout; wave (wr, wc) owns row
+// blocks wr WR .. wr WR + WR - 1 and column blocks 2 wc, 2 wc + 1 (16 x 16 each, WR x 2 MFMA
+// accumulators). Operands stream from L2 into a register ring D k-steps (16 k) deep; rows past the
+// tile / columns past N load clamped (valid) rows whose results are never stored, so the main loop
+// has no masks; a K tail that is not a multiple of 16 runs as one masked step.
+template <int WR, int EPI, bool SPLIT>
+__global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
+    constexpr int D = 4;                           // operand ring depth (k-steps in flight)
+    constexpr int TM = 32 * WR;                    // rows per workgroup tile
+    extern __shared__ __attribute__((aligned(16))) float zt[];   // GCN epilogue (dynamic)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = lane & 15, h = lane >> 4;
+    const int wr = w >> 1, wcol = w & 1;
+
+    const int gm = a.gm, gn = a.gn;
+    const int tl = xcd_tile(blockIdx.x, gridDim.x);
+    const int ct = tl % gn, rt = (tl / gn) % gm, split = tl / (gn * gm);
+
+    int row0, rows_t, s0 = 0;
+    if (EPI == HYPER_EPI_GCN) {
+        s0 = rt * a.S_t;
+        const int ns = a.B - s0 < a.S_t ? a.B - s0 : a.S_t;
+        row0 = s0 * a.P;
+        rows_t = ns * a.P;
+    } else {
+        row0 = rt * TM;
+        rows_t = a.rows - row0 < TM ? a.rows - row0 : TM;
+    }
+    const int col0 = ct * TN;
+    const int K = a.K, K1 = a.K1;
+    // k-steps of this split: [t_begin, t_end) of the full steps, plus the tail step in the last
+    const int KF = K / 16;                          // full 16-wide steps
+    const int per = (KF + a.splits - 1) / a.splits;
+    const int t_begin = split * per;
+    const int t_end = t_begin + per < KF ? t_begin + per : KF;
+    const bool tail = (K & 15) != 0 && split == a.splits - 1;
+
+    // operand rows (clamped into range)
+    size_t oa[WR], ob[WR];
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+        int r = 16 * (wr * WR + i) + j;
+        r = r < rows_t ? r : rows_t - 1;
+        oa[i] = (size_t)(row0 + r) * a.ld1 + 4 * h;
+        ob[i] = (size_t)(row0 + r) * a.ld2 + 4 * h;
+    }
+    size_t ow[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        int n = col0 + 16 * (2 * wcol + c) + j;
+        n = n < a.N ? n : a.N - 1;
+        ow[c] = (size_t)n * K + 4 * h;
+    }
+
+    const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 acc[WR][2];
+#pragma unroll
+    for (int i = 0; i < WR; ++i) acc[i][0] = acc[i][1] = zero;
+
+    auto mma = [&](const f32x4 (&av)[WR], const f32x4 (&bv)[2]) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < WR; ++i)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) acc[i][c] = mfma4(av[i][r], bv[c][r], acc[i][c]);
+    };
+    // steps [tb, te) of one input segment: X columns 16 t - koff at x + o[i]. The steady-state
+    // loop is straight-line (no conditional loads), so the compiler's vmcnt waits count exactly
+    // the D - 1 younger steps in flight instead of draining the queue every step.
+    auto segment = [&](const float* __restrict__ x, const size_t (&o)[WR], int koff, int tb, int te) {
+        f32x4 ar[D][WR], br[D][2];
+        auto load = [&](int u, int t) {
+#pragma unroll
+            for (int i = 0; i < WR; ++i) ar[u][i] = HYPER_ABL_A(*(const f32x4*)(x + o[i] + (16 * t - koff)));
+#pragma unroll
+            for (int c = 0; c < 2; ++c) br[u][c] = HYPER_ABL_W(*(const f32x4*)(a.W + ow[c] + 16 * t));
+        };
+        if (te - tb < D) {   // short segment: no ring
+            for (int t = tb; t < te; ++t) {
+                load(0, t);
+                mma(ar[0], br[0]);
+            }
+            return;
+        }
+#pragma unroll
+        for (int u = 0; u < D; ++u) load(u, tb + u);
+        // one group: D steps, each followed by the loads of the step D ahead (pinned there)
+        auto group = [&](int t0) {
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+                mma(ar[u], br[u]);
+                load(u, t0 + u + D);
+                mem_fence();
+            }
+        };
+        // two groups per trip: the compiler's waits at the loop head are conservative (they
+        // drain the queue), so a longer body exposes that latency less often
+        int t0 = tb;
+        for (; t0 + 3 * D <= te; t0 += 2 * D) {
+            group(t0);
+            group(t0 + D);
+        }
+        if (t0 + 2 * D <= te) {
+            group(t0);
+            t0 += D;
+        }
+        // te - t0 in [D, 2D): one group with its remaining prefetches, then the last steps
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+            mma(ar[u], br[u]);
+            if (t0 + u + D < te) load(u, t0 + u + D);
+        }
+        t0 += D;
+#pragma unroll
+        for (int u = 0; u < D; ++u)
+            if (t0 + u < te) mma(ar[u], br[u]);
+    };
+    if (SPLIT) {   // cat(x1, x2): K1 is a multiple of 16 (checked by the launcher)
+        const int t1 = K1 / 16;
+        segment(a.x1, oa, 0, t_begin, t_end < t1 ? t_end : t1);
+        segment(a.x2, ob, K1, t_begin > t1 ? t_begin : t1, t_end);
+    } else {
+        segment(a.x1, oa, 0, t_begin, t_end);
+    }
+    if (tail) {   // the last (K mod 16) columns: lanes past K load zeros
+        const int t = KF, k = 16 * t + 4 * h;
+        const bool kin = k < K;
+        f32x4 av[WR], bv[2];
+#pragma unroll
+        for (int i = 0; i < WR; ++i) {
+            const float* src = (SPLIT && k >= K1) ? a.x2 + ob[i] + (16 * t - K1)
+                                                  : a.x1 + oa[i] + 16 * t;
+            av[i] = kin ? *(const f32x4*)src : zero;
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) bv[c] = kin ? *(const f32x4*)(a.W + ow[c] + 16 * t) : zero;
+        mma(av, bv);
+    }
+
+    // lane (j, h) holds rows 16 (wr WR + i) + 4 h + r of column col0 + 16 (2 wcol + c) + j
+    if constexpr (EPI != HYPER_EPI_GCN) {
+        float* y = a.y + (size_t)split * a.split_stride;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int col = col0 + 16 * (2 * wcol + c) + j;
+            if (col >= a.N) continue;
+            float bv = 0.0f, mx = 1.0f;
+            int ch = 0;
+            if (EPI == HYPER_EPI_BIAS && a.bias != nullptr) bv = a.bias[col];
+            if (EPI == HYPER_EPI_HEAD) {
+                bv = a.bias[col];
+                ch = col / a.H;                         // view(B, 4, H): channel of fc output col
+                mx = a.maxv[ch];
+            }
+#pragma unroll
+            for (int i = 0; i < WR; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rr = 16 * (wr * WR + i) + 4 * h + r;
+                    if (rr >= rows_t) continue;
+                    float v = acc[i][c][r] + bv;
+                    if (EPI == HYPER_EPI_HEAD) {
+                        v = 1.0f / (1.0f + expf(-v));                  // torch.sigmoid  (:170)
+                        v = fminf(fmaxf(v, 1e-4f), 0.9999f);          // clamp          (:171)
+                        v = v * mx;                                   // * *_max        (:180-189)
+                        if (ch > 0) v = fminf(v, 0.9999f);            // tau/rho/eta    (:194-196)
+                    }
+                    y[(size_t)(row0 + rr) * a.ldy + col] = v;
+                }
+        }
+    } else {
+        // GCN epilogue. LDS: Z tile [TM][ZS] (ZS = 68: float4 rows), the tile's normalised
+        // adjacency blocks [S_t][P][P], per-column (bias, BN mean, BN scale, BN shift) [4][64].
+        // Output (node p of sample s, columns c..c+3):
+        //   BN(leaky(sum_q A_hat[s][p][q] Z[s, q][c] + bias[c])), BatchNorm on running statistics
+        const int P = a.P;
+        float* ahs = zt + TM * ZS;
+        float* colp = ahs + a.S_t * P * P;
+#pragma unroll
+        for (int i = 0; i < WR; ++i)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    zt[(16 * (wr * WR + i) + 4 * h + r) * ZS + 16 * (2 * wcol + c) + j] = acc[i][c][r];
+        const int nah = rows_t * P;                    // the tile's samples' A_hat rows
+        const float* agl = a.ahat + (a.ahat_per_sample ? (size_t)s0 * P * P : 0);
+        for (int i = threadIdx.x; i < nah; i += THREADS) ahs[i] = a.ahat_per_sample ? agl[i] : agl[i % (P * P)];
+        if (threadIdx.x < TN) {
+            const int col = col0 + threadIdx.x < a.N ? col0 + threadIdx.x : a.N - 1;
+            const float sc = (1.0f / sqrtf(a.bn_var[col] + a.bn_eps)) * a.bn_w[col];
+            colp[threadIdx.x] = a.bias[col];
+            colp[TN + threadIdx.x] = a.bn_mean[col];
+            colp[2 * TN + threadIdx.x] = sc;
+            colp[3 * TN + threadIdx.x] = a.bn_b[col];
+        }
+        __syncthreads();
+        const int cols = a.N - col0 < TN ? a.N - col0 : TN;
+        for (int task = threadIdx.x; task < rows_t * (TN / 4); task += THREADS) {
+            const int r = task / (TN / 4), c = 4 * (task - r * (TN / 4));
+            if (c >= cols) continue;
+            const int sl = r / P;
+            const float* ah = ahs + r * P;             // row p of sample sl's block
+            const float* zc = zt + sl * P * ZS + c;
+            f32x4 v = zero;
+            for (int q = 0; q < P; ++q) {
+                const float w = ah[q];
+                const f32x4 z = *(const f32x4*)(zc + q * ZS);
+                v = v + w * z;
+            }
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float t = v[e] + colp[c + e];
+                t = t > 0.0f ? t : t * a.slope;
+                o[e] = (t - colp[TN + c + e]) * colp[2 * TN + c + e] + colp[3 * TN + c + e];
+            }
+            float* dst = a.y + (size_t)(row0 + r) * a.ldy + col0 + c;
+            if (c + 4 <= cols) {
+                *(f32x4*)dst = o;
+            } else {
+                for (int e = 0; e < cols - c; ++e) dst[e] = o[e];
+            }
+        }
+    }
+}
+
+// LayerNorm over the C columns of every row (biased variance, like torch), then optionally
+// LeakyReLU(slope); one wave per row, the row held in registers (C <= 64 * 4 * CH).
+constexpr int CH = 8;
+__global__ __launch_bounds__(THREADS) void rownorm_kernel(RowNormArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+    if (row >= a.rows) return;
+    const float* x = a.x + (size_t)row * a.C;
+    const int C4 = a.C / 4;
+    f32x4 v[CH];
+    float s = 0.0f;
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        const int c4 = lane + 64 * u;
+        v[u] = c4 < C4 ? *(const f32x4*)(x + 4 * c4) : (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        if (c4 < C4) {
+            // split-K partial sums of the producing linear, added in split order, then its bias
+            for (int q = 1; q < a.nsum; ++q) v[u] += *(const f32x4*)(x + (size_t)q * a.sum_stride + 4 * c4);
+            if (a.pre_bias != nullptr) v[u] += *(const f32x4*)(a.pre_bias + 4 * c4);
+        }
+        s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / (float)a.C;
+    float q = 0.0f;
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        const int c4 = lane + 64 * u;
+        if (c4 < C4) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float d = v[u][e] - mean;
+                q += d * d;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+    const float rstd = 1.0f / sqrtf(q / (float)a.C + a.eps);
+    float* y = a.y + (size_t)row * a.C;
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        const int c4 = lane + 64 * u;
+        if (c4 >= C4) continue;
+        const f32x4 wv = *(const f32x4*)(a.weight + 4 * c4);
+        const f32x4 bv = *(const f32x4*)(a.bias + 4 * c4);
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float t = (v[u][e] - mean) * rstd * wv[e] + bv[e];
+            if (a.act) t = t > 0.0f ? t : t * a.slope;
+            o[e] = t;
+        }
+        *(f32x4*)(y + 4 * c4) = o;
+    }
+}
+
+template <int WR, int EPI, bool SPLIT>
+hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
+    size_t lds = 0;
+    if (EPI == HYPER_EPI_GCN) {
+        lds = 4 * ((size_t)32 * WR * ZS + (size_t)a.S_t * a.P * a.P + 4 * TN);
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void*)linear_kernel<WR, EPI, SPLIT>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+    }
+    hipLaunchKernelGGL((linear_kernel<WR, EPI, SPLIT>), dim3(grid), dim3(THREADS), lds, st, a);
+    return hipGetLastError();
+}
+
+template <int EPI, bool SPLIT>
+hipError_t launch_wr(int wr, int grid, const HyperArgs& a, hipStream_t st) {
+    switch (wr) {
+        case 1: return launch_one<1, EPI, SPLIT>(grid, a, st);
+        case 2: return launch_one<2, EPI, SPLIT>(grid, a, st);
+        case 4: return launch_one<4, EPI, SPLIT>(grid, a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int EPI>
+hipError_t launch_epi(int wr, int grid, const HyperArgs& a, hipStream_t st) {
+    if (a.K1 < a.K) return launch_wr<EPI, true>(wr, grid, a, st);
+    return launch_wr<EPI, false>(wr, grid, a, st);
+}
+
+}  // namespace hyper
+
+// Row tiling: the largest tile (32 WR rows; whole samples of P rows for the GCN epilogue) that
+// still gives ~two workgroups per CU; smaller tiles for small batches.
+static int pick_tiles(HyperArgs& a, int epi) {
+    const int unit = epi == HYPER_EPI_GCN ? a.P : 1;          // rows per tiling unit
+    const int units = epi == HYPER_EPI_GCN ? a.B : a.rows;
+    a.gn = (a.N + hyper::TN - 1) / hyper::TN;
+    int wr = 0;
+    for (int cand = 4; cand >= 1; cand >>= 1) {
+        const int su = 32 * cand / unit;
+        if (su < 1) break;
+        wr = cand;
+        a.S_t = su;
+        a.gm = (units + su - 1) / su;
+        if ((long)a.gm * a.gn >= 480) break;   // ~2 workgroups per CU: balance + latency hiding
+    }
+    return wr;
+}
+
+hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st) {
+    const int units = epi == HYPER_EPI_GCN ? a.B : a.rows;
+    if (units <= 0 || a.N <= 0) return hipSuccess;
+    if (a.K1 < a.K && (a.K1 & 15)) return hipErrorInvalidValue;
+    const int wr = pick_tiles(a, epi);
+    if (wr == 0) return hipErrorInvalidValue;
+    if (a.splits < 1) a.splits = 1;
+    const int grid = a.gm * a.gn * a.splits;
+    switch (epi) {
+        case HYPER_EPI_BIAS: return hyper::launch_epi<HYPER_EPI_BIAS>(wr, grid, a, st);
+        case HYPER_EPI_GCN: return hyper::launch_epi<HYPER_EPI_GCN>(wr, grid, a, st);
+        case HYPER_EPI_HEAD: return hyper::launch_epi<HYPER_EPI_HEAD>(wr, grid, a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+int hyper_linear_splits(int rows, int K, int N) {
+    HyperArgs a{};
+    a.rows = rows;
+    a.N = N;
+    const int wr = pick_tiles(a, HYPER_EPI_BIAS);
+    if (wr == 0) return 1;
+    const long tiles = (long)a.gm * a.gn;
+    int s = 1;
+    // split K while the grid is under ~2 workgroups per CU and every split keeps >= 16 k-steps
+    while (tiles * s * 2 <= 512 && K / 16 / (s * 2) >= 16 && s < 32) s *= 2;
+    return s;
+}
+
+hipError_t launch_rownorm(const RowNormArgs& a, hipStream_t st) {
+    if (a.rows <= 0) return hipSuccess;
+    const int per = hyper::THREADS / 64;
+    hipLaunchKernelGGL(hyper::rownorm_kernel, dim3((a.rows + per - 1) / per), dim3(hyper::THREADS),
+                       0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace dadmm

@@ -147,6 +147,48 @@ size_t loss_scratch_floats(int K, int64_t rows, int n);
 hipError_t launch_loss(const LossArgs& a, hipStream_t st);
 hipError_t launch_loss_grad(const LossArgs& a, const float* gout, float* dY, hipStream_t st);
 
+// ---- GNN hypernetwork, inference mode (dadmm_hyper.hip) ------------------------------------------
+#define HYPER_EPI_BIAS 0   // y = x W^T + bias
+#define HYPER_EPI_GCN 1    // y = BN(leaky(A_hat (x W^T) + bias)) per sample of P rows
+#define HYPER_EPI_HEAD 2   // y = min(clamp(sigmoid(x W^T + bias), 1e-4, 0.9999) * max_c, ...)
+struct HyperArgs {
+    const float* x1;        // input columns [0, K1): row r at x1 + r * ld1
+    const float* x2;        // input columns [K1, K): row r at x2 + r * ld2 (nullable if K1 == K)
+    int ld1, ld2, K1;
+    const float* W;         // [N][K] (nn.Linear.weight)
+    const float* bias;      // [N] (nullable for EPI_BIAS)
+    float* y;               // [rows][ldy]
+    int ldy;
+    int rows, K, N;         // rows = B * P for EPI_GCN
+    int B, P, S_t;          // GCN: samples, rows per sample, samples per tile (set by the launcher)
+    const float* ahat;      // GCN: [B or 1][P][P] normalised adjacency
+    int ahat_per_sample;
+    const float* bn_mean;   // GCN: BatchNorm1d running statistics and affine parameters [N]
+    const float* bn_var;
+    const float* bn_w;
+    const float* bn_b;
+    float bn_eps, slope;    // GCN: BatchNorm eps, leaky_relu negative slope
+    int H;                  // HEAD: hyper-parameter rows (P or 1); N = 4 H
+    float maxv[4];          // HEAD: alpha_max, tau_max, rho_max, eta_max
+    int splits;             // BIAS: split-K factor; split q writes y + q * split_stride (no bias)
+    size_t split_stride;
+    int gm, gn;             // tile grid (set by the launcher)
+};
+hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st);
+int hyper_linear_splits(int rows, int K, int N);
+struct RowNormArgs {
+    const float* x;         // [nsum][rows][C] (row stride C, partial q at x + q * sum_stride)
+    const float* weight;
+    const float* bias;
+    float* y;
+    int rows, C, act;
+    float eps, slope;
+    int nsum;               // split-K partials summed (in order) before the LayerNorm
+    size_t sum_stride;
+    const float* pre_bias;  // nullable: the producing linear's bias, added after the sum
+};
+hipError_t launch_rownorm(const RowNormArgs& a, hipStream_t st);
+
 // ---- forward prologue (dadmm_rng.hip) -----------------------------------------------------------
 struct PrologueArgs {
     uint64_t seed, offset, offset_step;   // torch Philox state; per-tensor offset increment

@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -30,6 +30,12 @@ EXPORTED_SYMBOLS = (
     "dadmm_forward_stepwise",
     "dadmm_backward_scratch_bytes",
     "dadmm_backward",
+    "dadmm_hyper_gcn",
+    "dadmm_hyper_linear",
+    "dadmm_hyper_rownorm",
+    "dadmm_hyper_head",
+    "dadmm_hyper_linear_ln_scratch_bytes",
+    "dadmm_hyper_linear_ln",
     "dadmm_gnn_flag_bytes",
     "dadmm_gnn_begin",
     "dadmm_gnn_gram",
@@ -124,6 +130,18 @@ def load() -> ctypes.CDLL:
         f = getattr(L, name)
         f.restype = ctypes.c_int
         f.argtypes = args
+    for name, args in (("dadmm_hyper_gcn", [i32] * 4 + [vp, i32, i32, vp, i32] + [vp] * 3 + [i32]
+                        + [vp] * 4 + [f32, f32, vp, i32, vp]),
+                       ("dadmm_hyper_linear", [i32] * 3 + [vp, i32, i32, vp, i32, vp, vp, vp, i32, vp]),
+                       ("dadmm_hyper_rownorm", [i32, i32, vp, vp, vp, f32, i32, f32, vp, vp]),
+                       ("dadmm_hyper_head", [i32, i32, i32, vp, i32, vp, vp] + [f32] * 4 + [vp, vp]),
+                       ("dadmm_hyper_linear_ln", [i32, i32, i32, vp, i32, vp, vp, vp, vp, f32, i32,
+                                                  f32, vp, vp, vp])):
+        f = getattr(L, name)
+        f.restype = ctypes.c_int
+        f.argtypes = args
+    L.dadmm_hyper_linear_ln_scratch_bytes.restype = ctypes.c_size_t
+    L.dadmm_hyper_linear_ln_scratch_bytes.argtypes = [i32, i32, i32]
     v = L.dadmm_abi_version()
     if v != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {v}, expected {ABI_VERSION}")

@@ -10,9 +10,11 @@ self.K, :137), and PyG-compatible state_dict names (``encoder.conv{1..5}.lin.wei
 
 Execution: every D-ADMM operation of the K-step loop — A^T A y_k, A^T b, gradient assembly,
 clamps, primal / consensus / dual updates and the batch-global NaN/Inf guards — runs in the HIP
-library one iteration at a time (``dadmm_hip.gnn_ops``); the hypernetwork between iterations is
-batched torch: all B per-sample graphs at once (the reference loops over samples in Python,
-:37-40), its linears on hipBLASLt (MFMA) GEMMs.
+library one iteration at a time (``dadmm_hip.gnn_ops``). The hypernetwork between iterations
+runs over all B per-sample graphs at once (the reference loops over samples in Python, :37-40):
+in inference (model.eval() under no_grad) on the fused HIP kernels of ``dadmm_hip.hyper_ops``
+(f32 MFMA GEMMs with the adjacency mix, leaky_relu and BatchNorm in their epilogues); in training
+(autograd, Dropout, per-sample BatchNorm statistics) as batched torch with hipBLASLt GEMMs.
 
 GCNConv (torch_geometric; absent here, unpinned version) is restated from its
 published algorithm: out = D^-1/2 (Adj + I) D^-1/2 (X W^T) + bias, self-loops added where missing,
@@ -28,6 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from dadmm_hip import _lib
+from dadmm_hip import hyper_ops
 from dadmm_hip.gnn_ops import GnnRun, GramFn, StepFn
 from dadmm_hip.graph import ingest
 from dadmm_hip.ops import PreparedOperator, draw_inits
@@ -170,6 +173,11 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         self._op = None
         self._op_key = None
         self.last_status = None
+        # "auto": the fused HIP hypernetwork in inference (eval + no_grad), torch otherwise;
+        # "torch": always the torch composition (tests compare the two)
+        self.hyper_backend = "auto"
+        # optional observer, called every iteration with (AtAy_k, Atb, (alpha, tau, rho, eta))
+        self.on_hyp = None
 
     @property
     def AtA(self):
@@ -233,10 +241,25 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         Atb = run.Atb[..., :n]
         y, U, D = run.ys[0], run.U0, run.d0
         ys = []
+        # inference (model.eval() under no_grad): the hypernetwork runs on the fused HIP kernels
+        fused = self.hyper_backend == "auto" and not grad and hyper_ops.supported(self, n)
+        if fused:
+            enc = self.encoder
+            bufs = hyper_ops.HyperBuffers(batch_size, self.P, enc.conv5.lin.out_features,
+                                          [self.decoder[i].out_features for i in (0, 4, 8)], H,
+                                          device)
+            a_hat = a_hat.contiguous()
         for k in range(K):
             AtAy = GramFn.apply(y, run, k)
-            alpha_k, tau_k, rho_k, eta_k = self.hypernetwork(AtAy[..., :n], Atb, a_hat)
-            hyp_k = torch.stack([alpha_k, tau_k, rho_k, eta_k], dim=1).reshape(batch_size, 4, H)
+            if fused:
+                alpha_k, tau_k, rho_k, eta_k = hyper_ops.hypernetwork_eval(
+                    self, AtAy, run.Atb, n, a_hat, not graphs.shared, bufs)
+                hyp_k = bufs.hyp
+            else:
+                alpha_k, tau_k, rho_k, eta_k = self.hypernetwork(AtAy[..., :n], Atb, a_hat)
+                hyp_k = torch.stack([alpha_k, tau_k, rho_k, eta_k], dim=1).reshape(batch_size, 4, H)
+            if self.on_hyp is not None:
+                self.on_hyp(AtAy[..., :n], Atb, (alpha_k, tau_k, rho_k, eta_k))
             y, U, D = StepFn.apply(y, U, D, AtAy, hyp_k.contiguous(), run, k)
             ys.append(y)
         self.last_status = run.finish()

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 7
+#define DADMM_ABI_VERSION 8
 
 enum {
     DADMM_OK = 0,
@@ -272,6 +272,52 @@ int dadmm_loss(int32_t K, int32_t B, int32_t P, int32_t n, int32_t n_store, cons
 int dadmm_loss_grad(int32_t K, int32_t B, int32_t P, int32_t n, int32_t n_store, const float* Y,
                     const float* label, const int32_t* flags, const float* gout, float* dY,
                     void* stream);
+
+/* ---- GNN hypernetwork, inference mode ---------------------------------------------------------
+ * GNNHypernetwork3 + decoder + fc of DLASSO_GNNHyp3_Progressive (gnn_dlasso_models_progressive.py
+ * :9-72, :93-123, :165-196) for model.eval() (Dropout = identity, BatchNorm on running
+ * statistics), batched over all B samples: one launch per layer instead of the reference's
+ * per-sample torch_geometric loop (:37-40). All operands are device fp32, row-major:
+ *   x1 / x2: the input rows, columns [0, K1) from x1 (row stride ld1), [K1, K) from x2 (row stride
+ *            ld2) — the cat(AtAy, Atb) of :165 without materialising it; K1 == K: x1 only;
+ *   W [N][K], bias [N]: nn.Linear / GCNConv.lin parameters;  y: row stride ldy.
+ * K, K1, ld1, ld2 multiples of 4 (K1 a multiple of 16 when K1 < K); x1, x2, W 16-byte aligned. f32 MFMA (exact f32 products and
+ * sums, summed in a fixed order that differs from torch's GEMMs: results agree to f32 rounding).
+ *
+ * dadmm_hyper_gcn: GCNConv(K -> N) -> leaky_relu(slope) -> BatchNorm1d (eval) for B samples of P
+ *   nodes (rows b*P + p): y = BN(leaky(A_hat[b] (x W^T) + bias)); ahat [B or 1][P][P] is
+ *   D^-1/2 (Adj + I) D^-1/2 (ahat_per_sample = 0: one graph for every sample).
+ *   Replaces: GCNConv + F.leaky_relu + self.bn_i of graph_conv (:52-68), per sample.
+ * dadmm_hyper_linear: y = x W^T + bias (bias nullable). Replaces: the decoder's nn.Linear (:94-104).
+ * dadmm_hyper_rownorm: y = LayerNorm(x) over C columns (biased variance), then LeakyReLU(slope)
+ *   when act != 0. Replaces: self.norm (:69) and the decoder's LayerNorm + LeakyReLU pairs.
+ *   C % 4 == 0, C <= 2048.
+ * dadmm_hyper_head: hyp [B][4][H] = (sigmoid(x W^T + bias) clamped to [1e-4, 0.9999]) * max_c,
+ *   then clamped to <= 0.9999 for c = tau, rho, eta; W [4H][K]. Replaces: fc, sigmoid, clamp and
+ *   the alpha/tau/rho/eta scaling of :167-196 (hyp is the reference's h.view(B, 4, H)). */
+int dadmm_hyper_gcn(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1, int32_t ld1,
+                    int32_t K1, const float* x2, int32_t ld2, const float* W, const float* bias,
+                    const float* ahat, int32_t ahat_per_sample, const float* bn_mean,
+                    const float* bn_var, const float* bn_weight, const float* bn_bias, float bn_eps,
+                    float slope, float* y, int32_t ldy, void* stream);
+int dadmm_hyper_linear(int32_t rows, int32_t K, int32_t N, const float* x1, int32_t ld1,
+                       int32_t K1, const float* x2, int32_t ld2, const float* W, const float* bias,
+                       float* y, int32_t ldy, void* stream);
+int dadmm_hyper_rownorm(int32_t rows, int32_t C, const float* x, const float* weight,
+                        const float* bias, float eps, int32_t act, float slope, float* y,
+                        void* stream);
+int dadmm_hyper_head(int32_t B, int32_t K, int32_t H, const float* x, int32_t ldx, const float* W,
+                     const float* bias, float alpha_max, float tau_max, float rho_max,
+                     float eta_max, float* hyp, void* stream);
+/* dadmm_hyper_linear_ln: y [rows][N] = LeakyReLU?(LayerNorm(x W^T + bias)) — one decoder block
+ *   (Linear -> Dropout(eval) -> LayerNorm -> LeakyReLU, :94-105) as a split-K GEMM whose partial
+ *   sums (scratch: dadmm_hyper_linear_ln_scratch_bytes, 16-byte aligned) the LayerNorm launch adds
+ *   in a fixed order (deterministic). N % 4 == 0, N <= 2048. */
+size_t dadmm_hyper_linear_ln_scratch_bytes(int32_t rows, int32_t K, int32_t N);
+int dadmm_hyper_linear_ln(int32_t rows, int32_t K, int32_t N, const float* x, int32_t ldx,
+                          const float* W, const float* bias, const float* ln_weight,
+                          const float* ln_bias, float eps, int32_t act, float slope, float* y,
+                          void* scratch, void* stream);
 
 #ifdef __cplusplus
 }

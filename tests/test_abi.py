@@ -163,3 +163,59 @@ def test_stepwise_record_pointers_both_or_neither(L):
     assert L.dadmm_forward_stepwise(ctypes.byref(d), *args, ctypes.c_void_p(0xA0000), None,
                                     ctypes.c_void_p(0xC0000), 0, scratch, None) == -1
     assert "both" in L.dadmm_last_error().decode()
+
+
+def _fk(i):
+    return ctypes.c_void_p(0x10000 * (i + 1))
+
+
+@pytest.mark.parametrize("kw,code", [
+    (dict(K=6, K1=6), -2),      # K not a multiple of 4
+    (dict(K1=6, K=8), -2),      # split point not a multiple of 4
+    (dict(ld1=3), -2),          # row stride
+    (dict(ldy=2), -2),          # ldy < N
+    (dict(K=0), -1),
+    (dict(N=0), -1),
+    (dict(K1=12, K=8), -1),     # K1 > K
+])
+def test_hyper_linear_rejects_before_launch(L, kw, code):
+    a = dict(rows=32, K=8, N=4, ld1=8, K1=8, ld2=0, ldy=4)
+    a.update(kw)
+    x2 = _fk(1) if a["K1"] < a["K"] else None
+    rc = L.dadmm_hyper_linear(a["rows"], a["K"], a["N"], _fk(0), a["ld1"], a["K1"], x2, a["ld2"],
+                              _fk(2), _fk(3), _fk(4), a["ldy"], None)
+    assert rc == code, L.dadmm_last_error()
+
+
+def test_hyper_null_and_misaligned(L):
+    assert L.dadmm_hyper_linear(8, 8, 4, None, 8, 8, None, 0, _fk(2), None, _fk(4), 4, None) == -1
+    assert L.dadmm_hyper_linear(8, 8, 4, ctypes.c_void_p(0x10004), 8, 8, None, 0, _fk(2), None,
+                                _fk(4), 4, None) == -1
+    # split input without its second pointer
+    assert L.dadmm_hyper_linear(8, 8, 4, _fk(0), 4, 4, None, 4, _fk(2), None, _fk(4), 4, None) == -1
+    # GCN: P outside 1..64, missing BatchNorm statistics
+    args = lambda P, bn: (4, P, 8, 4, _fk(0), 8, 8, None, 0, _fk(1), _fk(2), _fk(3), 1, bn,
+                          _fk(5), _fk(6), _fk(7), 1e-5, 0.01, _fk(8), 4, None)
+    assert L.dadmm_hyper_gcn(*args(65, _fk(4))) == -1
+    assert L.dadmm_hyper_gcn(*args(5, None)) == -1
+    assert L.dadmm_hyper_head(8, 8, 0, _fk(0), 8, _fk(1), _fk(2), 0.1, 0.99, 0.99, 0.99, _fk(3),
+                              None) == -1
+    assert L.dadmm_hyper_rownorm(8, 2052, _fk(0), _fk(1), _fk(2), 1e-5, 0, 0.0, _fk(3), None) == -2
+    assert L.dadmm_hyper_rownorm(8, 6, _fk(0), _fk(1), _fk(2), 1e-5, 0, 0.0, _fk(3), None) == -2
+    assert L.dadmm_hyper_rownorm(8, 8, _fk(0), None, _fk(2), 1e-5, 0, 0.0, _fk(3), None) == -1
+
+
+def test_hyper_empty_batch_is_ok(L):
+    assert L.dadmm_hyper_linear(0, 8, 4, _fk(0), 8, 8, None, 0, _fk(2), None, _fk(4), 4, None) == 0
+    assert L.dadmm_hyper_rownorm(0, 8, _fk(0), _fk(1), _fk(2), 1e-5, 1, 0.01, _fk(3), None) == 0
+
+
+def test_hyper_linear_ln_validation(L):
+    assert L.dadmm_hyper_linear_ln_scratch_bytes(1024, 2000, 400) >= 4 * 1024 * 400
+    assert L.dadmm_hyper_linear_ln_scratch_bytes(0, 8, 4) == 0
+    args = lambda N, scratch: (32, 8, N, _fk(0), 8, _fk(1), _fk(2), _fk(3), _fk(4), 1e-5, 1, 0.01,
+                               _fk(5), scratch, None)
+    assert L.dadmm_hyper_linear_ln(*args(6, _fk(6))) == -2          # LayerNorm width % 4
+    assert L.dadmm_hyper_linear_ln(*args(4, None)) == -1            # no scratch
+    # a split input whose split point is not a multiple of 16
+    assert L.dadmm_hyper_linear(8, 16, 4, _fk(0), 8, 8, _fk(1), 8, _fk(2), None, _fk(4), 4, None) == -2

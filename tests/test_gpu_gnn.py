@@ -48,16 +48,14 @@ def _setup(dev, P, m, n, B, K, mode, per_sample, seed=0, hidden=16):
 
 
 def _recording(model):
-    """Wrap model.hypernetwork to record (features, hyp) of every iteration."""
+    """Record (features, hyp) of every iteration through the model's on_hyp observer (either
+    hypernetwork backend)."""
     rec = []
-    orig = model.hypernetwork
 
-    def hook(AtAy, Atb, a_hat):
-        out = orig(AtAy, Atb, a_hat)
+    def hook(AtAy, Atb, out):
         rec.append((AtAy.detach().clone(), Atb.detach().clone(), [o.detach().clone() for o in out]))
-        return out
 
-    model.hypernetwork = hook
+    model.on_hyp = hook
     return rec
 
 
