@@ -226,7 +226,25 @@ def _batch_vectorized(graph_list, P: int, device) -> GraphBatch:
     return GraphBatch(t_[0], t_[1], False, t_[4] if ordered else None, t_[2], t_[3], fused_ok)
 
 
+def n_graphs(graph_list, batch_size: int) -> int:
+    """len(graph_list) as the reference's forward sees it; an already ingested GraphBatch counts
+    as one graph per sample."""
+    return batch_size if isinstance(graph_list, GraphBatch) else len(graph_list)
+
+
 def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
+    """The device layouts of ``graph_list`` (B networkx graphs, or one object repeated). A
+    ``GraphBatch`` from an earlier ingest() is passed through: callers that reuse the same graphs
+    across forwards (validation loops, benchmarks) ingest once — the tensor fast path."""
+    if isinstance(graph_list, GraphBatch):
+        gb = graph_list
+        if gb.deg.shape[-1] != P or (not gb.shared and gb.deg.shape[0] != batch_size):
+            raise ValueError(f"GraphBatch is for P={gb.deg.shape[-1]}"
+                             f"{'' if gb.shared else f', B={gb.deg.shape[0]}'}; "
+                             f"the forward needs P={P}, B={batch_size}")
+        if gb.deg.device != torch.device(device):
+            raise ValueError(f"GraphBatch lives on {gb.deg.device}, the forward runs on {device}")
+        return gb
     if P > 64:
         raise ValueError(f"P={P} > 64 agents does not fit the uint64 neighbour mask")
     G = len(graph_list)

@@ -32,7 +32,7 @@ import torch.nn.functional as F
 from dadmm_hip import _lib
 from dadmm_hip import hyper_ops
 from dadmm_hip.gnn_ops import GnnRun, GramFn, StepFn
-from dadmm_hip.graph import ingest
+from dadmm_hip.graph import ingest, n_graphs
 from dadmm_hip.ops import PreparedOperator, draw_inits
 
 
@@ -212,11 +212,11 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         return alpha_k, tau_k, rho_k, eta_k
 
     def forward(self, b, graph_list, training_iterations=None, *, inits=None):
-        batch_size = max(len(b), len(graph_list))
+        batch_size = max(len(b), n_graphs(graph_list, len(b)))
         K = training_iterations if training_iterations is not None else self.K
         if K <= 0:
             raise RuntimeError(f"forward needs at least one iteration, got K={K}")
-        if len(graph_list) != batch_size:
+        if n_graphs(graph_list, batch_size) != batch_size:
             # the reference's encoder indexes graph_list[i] for every sample (:39)
             raise IndexError("list index out of range")
         if b.dim() != 4 or b.shape[1] != self.P or b.shape[2] != self.m:

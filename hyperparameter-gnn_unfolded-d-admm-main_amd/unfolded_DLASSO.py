@@ -13,7 +13,7 @@ import torch.nn as nn
 from dadmm_hip import _lib
 from dadmm_hip.autograd import check_status, dadmm_unfolded_apply
 from dadmm_hip.ops import describe_status
-from dadmm_hip.graph import ingest
+from dadmm_hip.graph import ingest, n_graphs
 from dadmm_hip.ops import PreparedOperator
 
 
@@ -74,12 +74,13 @@ class DLASSO_unfolded(nn.Module):
         return self._table
 
     def forward(self, b, graph_list, K=None, *, inits=None):
-        """b [B,P,m,1]; graph_list: B networkx graphs on agents 0..P-1 (may repeat one object).
+        """b [B,P,m,1]; graph_list: B networkx graphs on agents 0..P-1 (may repeat one object),
+        or a ``dadmm_hip.graph.GraphBatch`` from an earlier ``ingest`` of them.
 
         ``inits`` (keyword-only, optional): (y0, U0, d0) each [B,P,n,1] or [B,P,n]; by default
         they are drawn like the reference (:49-51): randn * 1e-2 on b.device, in that order.
         """
-        batch_size = max(len(b), len(graph_list))
+        batch_size = max(len(b), n_graphs(graph_list, len(b)))
         device = b.device
         if K is None:
             K = self.K

@@ -81,6 +81,23 @@ def test_ingest_errors():
         ingest([G], 65, 1, "cpu")
 
 
+def test_ingest_passes_an_ingested_batch_through():
+    """The tensor fast path: a GraphBatch from ingest() is reused as is (validated for P, B and
+    device); n_graphs counts it as one graph per sample."""
+    from dadmm_hip.graph import GraphBatch, ingest, n_graphs
+    P, B = 5, 6
+    graphs = [O.connected_er_graph(P, 0.4, seed=s) for s in range(B)]
+    gb = ingest(graphs, P, B, "cpu")
+    assert ingest(gb, P, B, "cpu") is gb and isinstance(gb, GraphBatch)
+    assert n_graphs(gb, B) == B and n_graphs(graphs, 99) == B
+    with pytest.raises(ValueError):
+        ingest(gb, P + 1, B, "cpu")
+    with pytest.raises(ValueError):
+        ingest(gb, P, B + 1, "cpu")
+    shared = ingest([O.er_graph(P, 0.5, seed=7)] * B, P, B, "cpu")
+    assert shared.shared and ingest(shared, P, 3 * B, "cpu") is shared   # any batch size
+
+
 # ---- hyper-parameter table --------------------------------------------------------------------
 @pytest.mark.parametrize("mode", ["diff", "same"])
 def test_seq_hyp_table_matches_forward_k_and_oracle(mode):
