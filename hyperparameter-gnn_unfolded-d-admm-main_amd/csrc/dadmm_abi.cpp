@@ -464,6 +464,8 @@ int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
     if (d->m > dadmm::M_PAD)
         return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m, dadmm::M_PAD);
     if ((d->n & 3) != 0) return fail(DADMM_EUNSUPPORTED, "n=%d: needs n %% 4 == 0 (zero-pad n)", d->n);
+    if ((size_t)d->B * d->P * d->n * 4 >= ((size_t)1 << 31))
+        return fail(DADMM_EUNSUPPORTED, "B*P*n*4 >= 2^31 bytes per iterate (split the batch)");
     const int np = n_pad_of(d);
     if (dadmm::tiled_lds_bytes(np) > 160 * 1024)
         return fail(DADMM_EUNSUPPORTED, "n=%d: the y tile does not fit the LDS", d->n);

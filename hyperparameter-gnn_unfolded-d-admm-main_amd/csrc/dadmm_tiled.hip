@@ -30,6 +30,14 @@ namespace dadmm {
 namespace tiled {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(rsrc_t r, uint32_t voff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
 
 constexpr int THREADS = 256;   // 4 waves: GEMM1 = one 16-row m-block per wave
 constexpr int WAVES = 4;
@@ -83,16 +91,16 @@ __global__ __launch_bounds__(THREADS) void iter_kernel(TiledArgs a, int k) {
     const int hp = H == 1 ? 0 : p;
     uint32_t status = 0;
 
-    // visit lists of the workgroup's samples for agent p -> LDS
+    // visit lists of the workgroup's samples for agent p -> LDS: 8 threads per sample, the list
+    // pointers loaded once per thread, the entries' loads independent of each other
     if (k > 0) {
-        for (int i = threadIdx.x; i < ST * VMAX; i += THREADS) {
-            const int sl = i / VMAX, t = i % VMAX;
-            const int s2 = tile * ST + sl;
-            if (s2 < B) {
-                const int g0 = a.graph_shared ? 0 : s2 * P;
-                const int v0 = a.vptr[g0 + p], len = a.vptr[g0 + p + 1] - v0;
-                if (t < len) Vlds[i] = a.vq[v0 + t];
-            }
+        constexpr int TPS = THREADS / ST;             // threads per sample
+        const int sl = threadIdx.x / TPS, sub = threadIdx.x % TPS;
+        const int s2 = tile * ST + sl;
+        if (s2 < B) {
+            const int g0 = a.graph_shared ? 0 : s2 * P;
+            const int v0 = a.vptr[g0 + p], len = a.vptr[g0 + p + 1] - v0;
+            for (int t = sub; t < len; t += TPS) Vlds[sl * VMAX + t] = a.vq[v0 + t];
         }
     }
     if (!final_only) {
@@ -121,47 +129,60 @@ __global__ __launch_bounds__(THREADS) void iter_kernel(TiledArgs a, int k) {
             }
         }
         if (16 * w < m) {
-            // the B operand (y_k, 16 columns per half) straight from L2/HBM; columns past n and
-            // samples past B read as 0 (the padded operator columns are 0 too)
+            // the B operand (y_k, 16 columns per half) straight from L2/HBM through a buffer
+            // descriptor: columns past n and samples past B get an offset past the range, which
+            // the hardware returns as 0 (the padded operator columns are 0 too) - no branches
             const float* arow = a.A + ((size_t)p * M_PAD + 16 * w + j) * NP + 4 * h;
-            const float* brow[HALVES];
-            bool bok[HALVES];
+            const rsrc_t ry = make_rsrc(yk, (uint32_t)(S * 4));
+            uint32_t yoff[HALVES];
 #pragma unroll
             for (int hh = 0; hh < HALVES; ++hh) {
                 const int s = tile * ST + hh * BT + j;
-                bok[hh] = s < B;
-                brow[hh] = yk + ((size_t)(bok[hh] ? s : 0) * P + p) * n + 4 * h;
+                yoff[hh] = s < B ? (uint32_t)((((size_t)s * P + p) * n + 4 * h) * 4) : 0x80000000u;
             }
             auto ldb = [&](int hh, int t) -> f32x4 {
-                return (bok[hh] && 16 * t + 4 * h < n) ? *(const f32x4*)(brow[hh] + 16 * t)
-                                                       : (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+                return bload4(ry, 16 * t + 4 * h < n ? yoff[hh] + 64u * t : 0x80000000u);
             };
-            // operand ring of depth D: the loads of step t + D are issued after step t's MFMAs
-            // (NP / 16 is a multiple of 4)
+            // operand ring of depth D: the loads of step t + D are issued right after step t's
+            // MFMAs (pinned there by a scheduling barrier); T = NP / 16 is a multiple of D. The
+            // steady loop is straight-line, two groups per trip (the compiler's waits at a loop
+            // head drain the queue), so the waits count the D - 1 younger steps in flight.
             constexpr int D = 4;
             const int T = NP / 16;
             f32x4 ar[D], br[D][HALVES];
+            auto load = [&](int u, int t) {
+                ar[u] = *(const f32x4*)(arow + 16 * t);
 #pragma unroll
-            for (int u = 0; u < D; ++u) {
-                ar[u] = *(const f32x4*)(arow + 16 * u);
+                for (int hh = 0; hh < HALVES; ++hh) br[u][hh] = ldb(hh, t);
+            };
+            auto step = [&](int u) {
 #pragma unroll
-                for (int hh = 0; hh < HALVES; ++hh) br[u][hh] = ldb(hh, u);
-            }
-            for (int t0 = 0; t0 < T; t0 += D) {
+                for (int hh = 0; hh < HALVES; ++hh)
 #pragma unroll
-                for (int u = 0; u < D; ++u) {
+                    for (int r = 0; r < 4; ++r) acc[hh] = mfma4(ar[u][r], br[u][hh][r], acc[hh]);
+            };
 #pragma unroll
-                    for (int hh = 0; hh < HALVES; ++hh)
+            for (int u = 0; u < D; ++u) load(u, u);
+            int t0 = 0;
+            for (; t0 + 3 * D <= T; t0 += 2 * D) {
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) acc[hh] = mfma4(ar[u][r], br[u][hh][r], acc[hh]);
-                    const int tn = t0 + u + D;
-                    if (tn < T) {
-                        ar[u] = *(const f32x4*)(arow + 16 * tn);
-#pragma unroll
-                        for (int hh = 0; hh < HALVES; ++hh) br[u][hh] = ldb(hh, tn);
-                    }
+                for (int u = 0; u < 2 * D; ++u) {
+                    step(u % D);
+                    load(u % D, t0 + u + D);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             }
+            if (t0 + 2 * D <= T) {
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    step(u);
+                    load(u, t0 + u + D);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                t0 += D;
+            }
+#pragma unroll
+            for (int u = 0; u < D; ++u) step(u);   // the last D steps (T % D == 0)
         }
 #pragma unroll
         for (int hh = 0; hh < HALVES; ++hh)
