@@ -259,7 +259,7 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                         const float zb = inside(z, -vclip, vclip) ? yb[p][e] : 0.0f;
                         part[p][0] -= zb * g;
                         const float grb = inside(gr, -gclip, gclip) ? -al[p] * zb : 0.0f;
-                        const float sg = yk > 0.0f ? 1.0f : (yk < 0.0f ? -1.0f : 0.0f);
+                        const float sg = sign_times(yk, 1.0f);
                         part[p][1] += grb * sg;
                         part[p][2] += grb * t2[p][r];
                         Ub[p][e] = Ub[p][e] + grb * dg[p];

@@ -187,7 +187,7 @@ __global__ __launch_bounds__(THREADS) void grad_kernel(GnnArgs a, int k) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float y = yv[r];
-            const float st = y > 0.0f ? ta : (y < 0.0f ? -ta : 0.0f);   // sign(y) * tau
+            const float st = sign_times(y, ta);   // sign(y) * tau
             float g = aty[r] - atb[r];
             g = g + st;
             g = g + uv[r] * dg;
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
                 const size_t off = base + (size_t)p * n;
                 const float y = ys[off];
                 const float ta = hyp_at(a, s, 1, p);
-                const float st = y > 0.0f ? ta : (y < 0.0f ? -ta : 0.0f);
+                const float st = sign_times(y, ta);
                 float gr = a.AtAy[off] - a.Atb[off];
                 gr = gr + st;
                 gr = gr + a.U[off] * a.deg[g0 + p];
@@ -405,8 +405,8 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
                 const size_t off = base + (size_t)p * n;
                 const float al = hyp_at(a, s, 0, p), ta = hyp_at(a, s, 1, p), rh = hyp_at(a, s, 2, p);
                 const float y = ys[off];
-                const float sg = y > 0.0f ? 1.0f : (y < 0.0f ? -1.0f : 0.0f);
-                const float st = y > 0.0f ? ta : (y < 0.0f ? -ta : 0.0f);
+                const float sg = sign_times(y, 1.0f);
+                const float st = sign_times(y, ta);
                 float gr = a.AtAy[off] - a.Atb[off];
                 gr = gr + st;
                 gr = gr + a.U[off] * a.deg[g0 + p];

@@ -6,6 +6,15 @@
 
 namespace dadmm {
 
+// sign(y) * t exactly as torch's eager ops give it (sign(+-0) = sign(NaN) = 0, so +0 there, else
+// +-t), without branches: the sign bit of y moved onto t, then one select. (The nested-ternary
+// form compiles to divergent branches, ~11 instructions per element in the middle of the MFMA
+// chains.)
+__device__ __forceinline__ float sign_times(float y, float t) {
+    const float st = __uint_as_float(__float_as_uint(t) ^ (__float_as_uint(y) & 0x80000000u));
+    return __builtin_fabsf(y) > 0.0f ? st : 0.0f;
+}
+
 constexpr int BT = 16;       // samples per workgroup of the fused kernel (MFMA N dimension)
 constexpr int M_PAD = 64;    // padded rows per agent (4 m-blocks of 16 rows)
 #ifndef DADMM_FUSED_WAVES

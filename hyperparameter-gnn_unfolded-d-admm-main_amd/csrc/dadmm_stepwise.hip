@@ -186,7 +186,7 @@ __device__ void phase_grad(const StepArgs& a, int k, int item, float* lds) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float y = yv[r];
-                const float st = y > 0.0f ? ta : (y < 0.0f ? -ta : 0.0f);   // sign(y) * tau
+                const float st = sign_times(y, ta);   // sign(y) * tau
                 float g = gc[r] + st;
                 g = g + uv[r] * dg;
                 g = g + dv[r] * rh;

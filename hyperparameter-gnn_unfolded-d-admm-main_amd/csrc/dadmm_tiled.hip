@@ -327,7 +327,7 @@ __global__ __launch_bounds__(THREADS) void iter_kernel(TiledArgs a, int k) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float y = yp[g][r];
-                    const float st = y > 0.0f ? ta : (y < 0.0f ? -ta : 0.0f);   // sign(y) * tau
+                    const float st = sign_times(y, ta);   // sign(y) * tau
                     float gr = gc[r] + st;
                     gr = gr + uv[g][r] * dg[hh];
                     gr = gr + dv[g][r] * rh;
