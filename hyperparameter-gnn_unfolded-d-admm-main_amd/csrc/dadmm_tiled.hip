@@ -72,17 +72,29 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int G) {
     return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
 }
 
+typedef __attribute__((address_space(3))) void lds_void;
+
+// STAGE (n_pad <= STAGE_NP_MAX): the workgroup's y_k tile [ST][n_pad] is copied HBM -> LDS by
+// buffer_load ... lds (no VGPRs, the whole 64 KB in flight at once) at the start of the
+// iteration; GEMM1's B operand and the update phase's own rows are then read from LDS. The
+// image is lane-linear (the DMA's constraint), so the bank swizzle is applied on the source:
+// 16-byte chunk c of row sl is stored at chunk c ^ (sl & 15) of that row, and the 16 lanes of an
+// MFMA column block (16 samples, one chunk each) hit 16 distinct chunks of an aligned 256 B run.
+constexpr int STAGE_NP_MAX = 512;
+
 // k >= 0: one iteration (see header). k == K: the final dual update only (U_K into U_out).
 // Workgroup = (32-sample tile, agent p).
 // amdgpu_waves_per_eu(2): keeps VGPRs + AGPRs <= 256 (two workgroups per CU); without it the
 // allocator lands at 249 + 8 and the kernel runs at one wave per SIMD (0.40 -> 0.53 ms/iteration)
+template <bool STAGE>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) void iter_kernel(TiledArgs a, int k) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad;
     const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
     const int tile = wg / P, p = wg % P;
     const int RS = M_PAD + 4;
-    float* Rlds = lds;                               // [ST][RS]
+    float* Ylds = lds;                               // [ST][NP] swizzled y_k tile (STAGE)
+    float* Rlds = lds + (STAGE ? ST * NP : 0);       // [ST][RS]
     uint8_t* Vlds = (uint8_t*)(Rlds + ST * RS);      // [ST][VMAX] visit lists of agent p
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int j = lane & 15, h = lane >> 4;
@@ -92,6 +104,23 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int H = a.hyp_rows;
     const int hp = H == 1 ? 0 : p;
     uint32_t status = 0;
+
+    if constexpr (STAGE) {
+        if (!final_only) {
+            const rsrc_t ry = make_rsrc(yk, (uint32_t)(S * 4));
+            const int CPR = NP / 4;                   // 16-byte chunks per row (a multiple of 16)
+            for (int base = w * 64; base < ST * CPR; base += WAVES * 64) {
+                const int lc = base + lane;
+                const int sl = lc / CPR, c = (lc % CPR) ^ (sl & 15);
+                const int s = tile * ST + sl;
+                const uint32_t off = (s < B && 4 * c < n)
+                                         ? (uint32_t)((((size_t)s * P + p) * n + 4 * c) * 4)
+                                         : 0x80000000u;   // past the range: the DMA writes zeros
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (lds_void*)(Ylds + 4 * base), 16, off,
+                                                         0, 0, 0);
+            }
+        }
+    }
 
     // visit lists of the workgroup's samples for agent p -> LDS: 8 threads per sample, the list
     // pointers loaded once per thread, the entries' loads independent of each other
@@ -130,8 +159,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
                 acc[hh][r] = (s < B && mi < m) ? -a.b[((size_t)s * P + p) * m + mi] : 0.0f;
             }
         }
+        if constexpr (STAGE) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA has landed
+            __syncthreads();                                     // ... and every other wave's
+        }
         if (16 * w < m) {
-            // the B operand (y_k, 16 columns per half) straight from L2/HBM through a buffer
+            // the B operand (y_k, 16 columns per half) from the staged LDS tile (STAGE), else
+            // straight from L2/HBM through a buffer
             // descriptor: columns past n and samples past B get an offset past the range, which
             // the hardware returns as 0 (the padded operator columns are 0 too) - no branches
             const float* arow = a.A + ((size_t)p * M_PAD + 16 * w + j) * NP + 4 * h;
@@ -143,7 +177,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
                 yoff[hh] = s < B ? (uint32_t)((((size_t)s * P + p) * n + 4 * h) * 4) : 0x80000000u;
             }
             auto ldb = [&](int hh, int t) -> f32x4 {
-                return bload4(ry, 16 * t + 4 * h < n ? yoff[hh] + 64u * t : 0x80000000u);
+                if constexpr (STAGE)
+                    return *(const f32x4*)(Ylds + (hh * BT + j) * NP + 4 * ((4 * t + h) ^ j));
+                else
+                    return bload4(ry, 16 * t + 4 * h < n ? yoff[hh] + 64u * t : 0x80000000u);
             };
             // operand ring of depth D: the loads of step t + D are issued right after step t's
             // MFMAs (pinned there by a scheduling barrier); T = NP / 16 is a multiple of D. The
@@ -267,7 +304,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
                 off[g] = (srow[hh] + p) * n + n0[i];
                 yp[g] = up[g] = dv[g] = (f32x4){0, 0, 0, 0};
                 if (okr[g]) {
-                    yp[g] = *(const f32x4*)(yk + off[g]);
+                    if (STAGE && !final_only)   // (the final dual update stages nothing)
+                        yp[g] = *(const f32x4*)(Ylds + (hh * BT + j) * NP + 4 * ((n0[i] >> 2) ^ j));
+                    else
+                        yp[g] = *(const f32x4*)(yk + off[g]);
                     up[g] = *(const f32x4*)((k == 0 ? a.U0 : Uprev) + off[g]);
                     if (k == 0) dv[g] = *(const f32x4*)(a.d0 + off[g]);
                 }
@@ -355,23 +395,25 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
 }  // namespace tiled
 
 size_t tiled_lds_bytes(int n_pad) {
-    (void)n_pad;
-    return 4 * (size_t)(tiled::ST * (M_PAD + 4)) + tiled::ST * tiled::VMAX;
+    const size_t stage = n_pad <= tiled::STAGE_NP_MAX ? 4 * (size_t)tiled::ST * n_pad : 0;
+    return stage + 4 * (size_t)(tiled::ST * (M_PAD + 4)) + tiled::ST * tiled::VMAX;
 }
 
 hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream) {
     const size_t lds = tiled_lds_bytes(a.n_pad);
     if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+    if (a.n_pad % 64 != 0) return hipErrorInvalidValue;   // the swizzle and GEMM ring assume it
+    auto kern = a.n_pad <= tiled::STAGE_NP_MAX ? tiled::iter_kernel<true> : tiled::iter_kernel<false>;
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)tiled::iter_kernel,
+        hipError_t e = hipFuncSetAttribute((const void*)kern,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
     const int items = ((a.B + tiled::ST - 1) / tiled::ST) * a.P;
     for (int k = 0; k < a.K; ++k)
-        hipLaunchKernelGGL(tiled::iter_kernel, dim3(items), dim3(tiled::THREADS), lds, stream, a, k);
+        hipLaunchKernelGGL(kern, dim3(items), dim3(tiled::THREADS), lds, stream, a, k);
     if (a.U_out != nullptr)
-        hipLaunchKernelGGL(tiled::iter_kernel, dim3(items), dim3(tiled::THREADS), lds, stream, a, a.K);
+        hipLaunchKernelGGL(kern, dim3(items), dim3(tiled::THREADS), lds, stream, a, a.K);
     return hipGetLastError();
 }
 

@@ -9,7 +9,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdadmm.so")
+# DADMM_LIB_VARIANT: an alternative build of the same library (timing experiments,
+# scripts/time_variants.sh); it is still the HIP library, there is no other path
+LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
 ABI_VERSION = 8
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
