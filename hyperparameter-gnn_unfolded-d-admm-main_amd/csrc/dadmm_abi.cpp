@@ -445,7 +445,7 @@ int dadmm_prologue(uint64_t seed, uint64_t offset, int64_t numel, int32_t n, int
 
 size_t dadmm_tiled_scratch_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;
-    return 2 * align256(sizeof(float) * (size_t)d->B * d->P * d->n);
+    return 3 * align256(sizeof(float) * (size_t)d->B * d->P * d->n);   // U ping-pong, delta
 }
 
 int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
@@ -484,6 +484,7 @@ int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
     a.Y = Y;
     a.Ubuf[0] = (float*)scratch;
     a.Ubuf[1] = (float*)((char*)scratch + state);
+    a.delta = (float*)((char*)scratch + 2 * state);
     a.U_out = U_out;
     a.status = status;
     a.B = d->B;

@@ -134,6 +134,7 @@ struct TiledArgs {
     const float* d0;
     float* Y;               // [K][B][P][n]
     float* Ubuf[2];         // ping-pong U_k buffers [B][P][n] (scratch)
+    float* delta;           // delta_k [B][P][n] (scratch, consensus_kernel)
     float* U_out;           // [B][P][n] or nullptr
     int32_t* status;        // or nullptr (OR-ed DADMM_STATUS_* bits)
     int B, P, m, n, n_pad, K, hyp_rows, variant, graph_shared;

@@ -5,9 +5,9 @@
 //
 // Reference semantics: unfolded_DLASSO.py:53-107 / :127-140 (and the GNN variant's clamps,
 // gnn_dlasso_models_progressive.py:205-232). Iteration k of workgroup (tile, p):
-//   delta_k[p] = sum over p's visit list of (y_p - y_q), from y_k of the neighbours (their tiles
-//                are read by the sibling workgroups of the same tile at the same time: L2 hits)
-//                (k = 0: the caller's d0);
+//   delta_k[p] = sum over p's visit list of (y_p - y_q), from y_k of the neighbours: formed for
+//                every agent of a sample at once by consensus_kernel (one pass over y_k, the
+//                sample's rows staged in LDS) and read here as one more stream (k = 0: d0);
 //   U_k[p]     = clamp(U_{k-1}[p] + delta_k[p] eta_{k-1}, +-vclip_{k-1})   (the dual update of
 //                iteration k-1, deferred to here as in the fused kernel; k = 0: U0);
 //   R          = A_p y_k - b_p;  G = A_p^T R                (f32 MFMA fma chains, the fused
@@ -61,7 +61,6 @@ __device__ __forceinline__ void clips(int variant, int k, float& gclip, float& v
 constexpr int HALVES = 2;            // 16-sample MFMA column blocks per workgroup (32 samples):
                                      // every A / A^T operand load feeds two fma chains
 constexpr int ST = HALVES * BT;      // samples per workgroup
-constexpr int VMAX = 128;            // visit-list entries cached per sample (2P <= 128)
 
 // blockIdx -> (tile, agent) so that the P workgroups of one sample tile run on the same XCD
 // (dispatch is round-robin over the 8 XCDs, each with its own L2): the neighbour tiles a
@@ -95,7 +94,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int RS = M_PAD + 4;
     float* Ylds = lds;                               // [ST][NP] swizzled y_k tile (STAGE)
     float* Rlds = lds + (STAGE ? ST * NP : 0);       // [ST][RS]
-    uint8_t* Vlds = (uint8_t*)(Rlds + ST * RS);      // [ST][VMAX] visit lists of agent p
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int j = lane & 15, h = lane >> 4;
     const size_t S = (size_t)B * P * n;
@@ -122,18 +120,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
         }
     }
 
-    // visit lists of the workgroup's samples for agent p -> LDS: 8 threads per sample, the list
-    // pointers loaded once per thread, the entries' loads independent of each other
-    if (k > 0) {
-        constexpr int TPS = THREADS / ST;             // threads per sample
-        const int sl = threadIdx.x / TPS, sub = threadIdx.x % TPS;
-        const int s2 = tile * ST + sl;
-        if (s2 < B) {
-            const int g0 = a.graph_shared ? 0 : s2 * P;
-            const int v0 = a.vptr[g0 + p], len = a.vptr[g0 + p + 1] - v0;
-            for (int t = sub; t < len; t += TPS) Vlds[sl * VMAX + t] = a.vq[v0 + t];
-        }
-    }
     if (!final_only) {
         if (k == 0) {   // :55 guard on y0 (the only iteration where it can fire)
             const int nc4 = n / 4;
@@ -246,14 +232,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
 
     // per-lane data of the two samples this lane serves
     float dg[HALVES];
-    int vlen[HALVES];
     f32x4 rv[HALVES][M_PAD / 16];
 #pragma unroll
     for (int hh = 0; hh < HALVES; ++hh) {
         const int s = tile * ST + hh * BT + j;
         const int g0 = a.graph_shared ? 0 : s * P;
         dg[hh] = s < B ? a.deg[g0 + p] : 0.0f;
-        vlen[hh] = s < B ? a.vptr[g0 + p + 1] - a.vptr[g0 + p] : 0;
         if (!final_only) {
 #pragma unroll
             for (int t = 0; t < M_PAD / 16; ++t)
@@ -263,23 +247,20 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     bool bad_u0 = false, bad_g = false, bad_y = false;
     const float* atbase = a.At + ((size_t)p * NP + j) * M_PAD + 4 * h;
     // The wave's n-tiles nb = w, w + 4, ... are processed CH at a time; each chunk issues its
-    // loads together (y_k rows, U_{k-1} rows, A^T rows, and the neighbour rows of the consensus
-    // four visit-list entries at a time for all CH tiles x 2 samples): memory-level parallelism
-    // instead of one dependent round trip per tile.
-    constexpr int CH = 2;
+    // loads together (y_k rows, U_{k-1} rows, delta_k rows, A^T rows)
+#ifndef DADMM_TILED_CH
+#define DADMM_TILED_CH 2
+#endif
+    constexpr int CH = DADMM_TILED_CH;
     constexpr int RG = CH * HALVES;            // row groups per chunk
     const int ntw = (NP / 16 - w + WAVES - 1) / WAVES;   // tiles of this wave
+    const float* dsrc = k == 0 ? a.d0 : a.delta;   // delta_k
     size_t srow[HALVES];
-    const uint8_t* vl[HALVES];
-    int len[HALVES];
 #pragma unroll
     for (int hh = 0; hh < HALVES; ++hh) {
         const int s = tile * ST + hh * BT + j;
         srow[hh] = (size_t)(s < B ? s : 0) * P;
-        vl[hh] = Vlds + (hh * BT + j) * VMAX;
-        len[hh] = (s < B && k > 0) ? vlen[hh] : 0;
     }
-    const int L = len[0] > len[1] ? len[0] : len[1];
     for (int c0 = 0; c0 < ntw; c0 += CH) {
         int n0[CH];
         bool okr[RG];
@@ -309,31 +290,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
                     else
                         yp[g] = *(const f32x4*)(yk + off[g]);
                     up[g] = *(const f32x4*)((k == 0 ? a.U0 : Uprev) + off[g]);
-                    if (k == 0) dv[g] = *(const f32x4*)(a.d0 + off[g]);
+                    dv[g] = *(const f32x4*)(dsrc + off[g]);
                 }
             }
-        }
-        // delta_k: visit lists in order, 4 entries x RG row groups of loads in flight
-        for (int t = 0; t < L; t += 4) {
-            f32x4 yq[4][RG];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int g = 0; g < RG; ++g) {
-                    const int hh = g % HALVES, i = g / HALVES;
-                    if (okr[g] && t + u < len[hh])
-                        yq[u][g] = *(const f32x4*)(yk + (srow[hh] + vl[hh][t + u]) * n + n0[i]);
-                }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int g = 0; g < RG; ++g) {
-                    const int hh = g % HALVES;
-                    if (okr[g] && t + u < len[hh]) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) dv[g][r] = dv[g][r] + (yp[g][r] - yq[u][g][r]);
-                    }
-                }
         }
 #pragma unroll
         for (int g = 0; g < RG; ++g) {
@@ -392,11 +351,45 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
 }
 
+// delta_k = compute_delta(y_k) (unfolded_DLASSO.py:127-140) for every agent of one sample over a
+// block of CB columns: the sample's P rows are staged in LDS (one coalesced pass over y_k), then
+// wave w forms agent p = w, w + 4, ... by its visit list in the reference's order, one fp32 add
+// chain per column from 0 (bit-identical to the fused / stepwise consensus). The visit list is
+// wave-uniform (scalar loads).
+constexpr int CB = 256;
+__global__ __launch_bounds__(THREADS) void consensus_kernel(TiledArgs a, const float* __restrict__ y) {
+    extern __shared__ __attribute__((aligned(16))) float ys[];   // [P][CB]
+    const int P = a.P, n = a.n;
+    const int ncb = (n + CB - 1) / CB;
+    const int s = blockIdx.x / ncb, c0 = (blockIdx.x % ncb) * CB;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float* ys_g = y + (size_t)s * P * n;
+    for (int idx = threadIdx.x; idx < P * (CB / 4); idx += THREADS) {
+        const int p = idx / (CB / 4), c = c0 + 4 * (idx % (CB / 4));
+        if (c < n) *(f32x4*)(ys + p * CB + (c - c0)) = *(const f32x4*)(ys_g + (size_t)p * n + c);
+    }
+    __syncthreads();
+    const int c = c0 + 4 * lane;
+    if (c >= n) return;
+    const int g0 = a.graph_shared ? 0 : s * P;
+    for (int p = w; p < P; p += WAVES) {
+        const int v0 = a.vptr[g0 + p], v1 = a.vptr[g0 + p + 1];
+        const f32x4 yp = *(const f32x4*)(ys + p * CB + 4 * lane);
+        f32x4 dv = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int t = v0; t < v1; ++t) {
+            const f32x4 yq = *(const f32x4*)(ys + (int)a.vq[t] * CB + 4 * lane);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dv[r] = dv[r] + (yp[r] - yq[r]);
+        }
+        *(f32x4*)(a.delta + ((size_t)s * P + p) * n + c) = dv;
+    }
+}
+
 }  // namespace tiled
 
 size_t tiled_lds_bytes(int n_pad) {
     const size_t stage = n_pad <= tiled::STAGE_NP_MAX ? 4 * (size_t)tiled::ST * n_pad : 0;
-    return stage + 4 * (size_t)(tiled::ST * (M_PAD + 4)) + tiled::ST * tiled::VMAX;
+    return stage + 4 * (size_t)(tiled::ST * (M_PAD + 4));
 }
 
 hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream) {
@@ -410,10 +403,16 @@ hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream) {
         if (e != hipSuccess) return e;
     }
     const int items = ((a.B + tiled::ST - 1) / tiled::ST) * a.P;
-    for (int k = 0; k < a.K; ++k)
+    const size_t S = (size_t)a.B * a.P * a.n;
+    const int citems = a.B * ((a.n + tiled::CB - 1) / tiled::CB);
+    const size_t clds = 4 * (size_t)a.P * tiled::CB;
+    for (int k = 0; k <= a.K; ++k) {
+        if (k == a.K && a.U_out == nullptr) break;   // k == K: the final dual update (U_out)
+        if (k > 0)   // delta_k from y_k = Y[k-1]
+            hipLaunchKernelGGL(tiled::consensus_kernel, dim3(citems), dim3(tiled::THREADS), clds,
+                               stream, a, (const float*)(a.Y + (size_t)(k - 1) * S));
         hipLaunchKernelGGL(kern, dim3(items), dim3(tiled::THREADS), lds, stream, a, k);
-    if (a.U_out != nullptr)
-        hipLaunchKernelGGL(kern, dim3(items), dim3(tiled::THREADS), lds, stream, a, a.K);
+    }
     return hipGetLastError();
 }
 
