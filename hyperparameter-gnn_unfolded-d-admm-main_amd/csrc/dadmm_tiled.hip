@@ -352,14 +352,17 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
 }
 
 // delta_k = compute_delta(y_k) (unfolded_DLASSO.py:127-140) for every agent of one sample over a
-// block of CB columns: the sample's P rows are staged in LDS (one coalesced pass over y_k), then
-// wave w forms agent p = w, w + 4, ... by its visit list in the reference's order, one fp32 add
-// chain per column from 0 (bit-identical to the fused / stepwise consensus). The visit list is
-// wave-uniform (scalar loads).
+// block of CB columns: the sample's P rows and its visit lists are staged in LDS (one coalesced
+// pass over y_k), then wave w forms agent p = w, w + 4, ... by its visit list in the reference's
+// order, one fp32 add chain per column from 0 (bit-identical to the fused / stepwise consensus).
 constexpr int CB = 256;
+// visit entries per sample: every node lists each neighbour twice (both ends of an edge), <= 2 P^2
+size_t consensus_lds_bytes(int P) { return 4 * (size_t)P * CB + 4 * (size_t)(P + 1) + 2 * (size_t)P * P; }
 __global__ __launch_bounds__(THREADS) void consensus_kernel(TiledArgs a, const float* __restrict__ y) {
     extern __shared__ __attribute__((aligned(16))) float ys[];   // [P][CB]
     const int P = a.P, n = a.n;
+    int32_t* vp = (int32_t*)(ys + P * CB);                       // [P + 1] list starts (local)
+    uint8_t* vq = (uint8_t*)(vp + P + 1);                        // <= 2 P^2 entries
     const int ncb = (n + CB - 1) / CB;
     const int s = blockIdx.x / ncb, c0 = (blockIdx.x % ncb) * CB;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -368,16 +371,19 @@ __global__ __launch_bounds__(THREADS) void consensus_kernel(TiledArgs a, const f
         const int p = idx / (CB / 4), c = c0 + 4 * (idx % (CB / 4));
         if (c < n) *(f32x4*)(ys + p * CB + (c - c0)) = *(const f32x4*)(ys_g + (size_t)p * n + c);
     }
+    const int g0 = a.graph_shared ? 0 : s * P;
+    const int vbase = a.vptr[g0], vend = a.vptr[g0 + P];
+    for (int i = threadIdx.x; i <= P; i += THREADS) vp[i] = a.vptr[g0 + i] - vbase;
+    for (int i = threadIdx.x; i < vend - vbase; i += THREADS) vq[i] = a.vq[vbase + i];
     __syncthreads();
     const int c = c0 + 4 * lane;
     if (c >= n) return;
-    const int g0 = a.graph_shared ? 0 : s * P;
     for (int p = w; p < P; p += WAVES) {
-        const int v0 = a.vptr[g0 + p], v1 = a.vptr[g0 + p + 1];
+        const int v0 = vp[p], v1 = vp[p + 1];
         const f32x4 yp = *(const f32x4*)(ys + p * CB + 4 * lane);
         f32x4 dv = {0.0f, 0.0f, 0.0f, 0.0f};
         for (int t = v0; t < v1; ++t) {
-            const f32x4 yq = *(const f32x4*)(ys + (int)a.vq[t] * CB + 4 * lane);
+            const f32x4 yq = *(const f32x4*)(ys + (int)vq[t] * CB + 4 * lane);
 #pragma unroll
             for (int r = 0; r < 4; ++r) dv[r] = dv[r] + (yp[r] - yq[r]);
         }
@@ -405,7 +411,13 @@ hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream) {
     const int items = ((a.B + tiled::ST - 1) / tiled::ST) * a.P;
     const size_t S = (size_t)a.B * a.P * a.n;
     const int citems = a.B * ((a.n + tiled::CB - 1) / tiled::CB);
-    const size_t clds = 4 * (size_t)a.P * tiled::CB;
+    const size_t clds = tiled::consensus_lds_bytes(a.P);
+    if (clds > 160 * 1024) return hipErrorInvalidConfiguration;
+    if (clds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)tiled::consensus_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)clds);
+        if (e != hipSuccess) return e;
+    }
     for (int k = 0; k <= a.K; ++k) {
         if (k == a.K && a.U_out == nullptr) break;   // k == K: the final dual update (U_out)
         if (k > 0)   // delta_k from y_k = Y[k-1]

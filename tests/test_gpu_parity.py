@@ -156,7 +156,7 @@ def test_shapes_bit_exact(cuda, P, m, n, B, K, prob, per_sample, path):
     assert np.array_equal(U, Uo)
 
 
-@pytest.mark.parametrize("path", ["auto", "stepwise"])
+@pytest.mark.parametrize("path", ["auto", "stepwise", "tiled"])
 def test_same_mode_and_gnn_variant(cuda, path):
     """'same' hyper-parameters (H = 1) and the GNN variant's fixed clamps / delta clamp."""
     P, m, n, B, K = 5, 32, 128, 24, 12
