@@ -326,8 +326,9 @@ int dadmm_gnn_step(const dadmm_dims* d, int32_t k, const int32_t* visit_ptr, con
     if (!visit_ptr || !visit_q || !deg || !hyp_k || !yptr || !AtAy || !Atb || !U || !D || !U_next ||
         !D_next || !G || !flags)
         return fail(DADMM_EINVAL, "a required pointer is NULL");
-    if (!aligned16(AtAy) || !aligned16(Atb) || !aligned16(U) || !aligned16(D) || !aligned16(G))
-        return fail(DADMM_EINVAL, "AtAy, Atb, U, D and G must be 16-byte aligned");
+    if (!aligned16(AtAy) || !aligned16(Atb) || !aligned16(U) || !aligned16(D) || !aligned16(G) ||
+        !aligned16(U_next) || !aligned16(D_next))
+        return fail(DADMM_EINVAL, "AtAy, Atb, U, D, U_next, D_next and G must be 16-byte aligned");
     a.vptr = visit_ptr;
     a.vq = visit_q;
     a.deg = deg;

@@ -201,23 +201,29 @@ __global__ __launch_bounds__(THREADS) void grad_kernel(GnnArgs a, int k) {
     flag_or(a.flags + GNN_F_GBAD(k), bad);
 }
 
-// ---- update: primal update, consensus and dual update of (sample, 64 columns) (:221-232) -------
-// One wave per (sample, 64 columns); the item is wave-uniform, so the visit lists and the
-// hyper-parameters are scalar loads. The per-agent global loads are issued UP_CH agents at a time
-// (memory-level parallelism for large P: P = 50 at BASELINE configs[4]); the sample's visit lists
-// are staged in LDS next to y_{k+1}.
-constexpr int UP_CH = 8;
-// LDS words for one sample's visit lists: at most 2 P entries per agent (each incident edge is
+// ---- update: primal update, consensus and dual update of (sample, 128 columns) (:221-232) ------
+// One workgroup per (sample, UCB = 128 columns). A lane owns 4 columns of one agent row; a wave
+// instruction covers two agent rows (lanes 0-31 and 32-63), so every global access is a 16-byte
+// vector and a wave keeps UP_CH row pairs of loads in flight. y_{k+1} of all P agents is staged in
+// LDS ([P][UCB], 25.6 KB at P = 50) next to the sample's visit lists, and the consensus reads its
+// neighbours from there in the reference's visit order (one fp32 add chain per column from 0).
+constexpr int UP_CH = 4;
+constexpr int UCB = 128;
+// LDS bytes for one sample's visit lists: at most 2 P entries per agent (each incident edge is
 // visited from both of its ends; a self-loop twice), one byte each
 __host__ __device__ constexpr int update_visit_words(int P) { return (2 * P * P + 3) / 4; }
+__host__ __device__ constexpr size_t update_lds_bytes(int P) {
+    return 4 * ((size_t)P * UCB + (size_t)(P + 1) + update_visit_words(P));
+}
 __global__ __launch_bounds__(THREADS) void update_kernel(GnnArgs a, int k, int items) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + (threadIdx.x >> 6));
-    if (item >= items) return;
     const int P = a.P, n = a.n;
-    const int nch = (n + 63) / 64;
-    const int s = item / nch, lane = threadIdx.x & 63;
-    const int c = (item % nch) * 64 + lane;
+    const int ncb = (n + UCB - 1) / UCB;
+    const int s = blockIdx.x / ncb;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int half = lane >> 5;
+    const int c = (blockIdx.x % ncb) * UCB + 4 * (lane & 31);
+    const int cl = 4 * (lane & 31);                  // column within the block
     const bool cv = c < n;
     const size_t base = (size_t)s * P * n + (cv ? c : 0);
     bool yzero = false;
@@ -226,76 +232,80 @@ __global__ __launch_bounds__(THREADS) void update_kernel(GnnArgs a, int k, int i
     const bool uzero = flag_ld(a.flags + GNN_F_UBAD(k)) != 0;
     float gclip, vclip;
     clips(a, k, gclip, vclip);
-    // per-wave LDS: y_{k+1} rows [P][64], then the sample's visit lists
-    float* yl = lds + (threadIdx.x >> 6) * (P * 64 + update_visit_words(P));
-    uint8_t* vl = (uint8_t*)(yl + P * 64);
+    float* yl = lds;                                  // [P][UCB] y_{k+1}
+    int32_t* vpl = (int32_t*)(yl + P * UCB);          // [P + 1] list starts (sample-local)
+    uint8_t* vl = (uint8_t*)(vpl + P + 1);            // the sample's visit lists
     const int g0 = a.graph_shared ? 0 : s * P;
     const int vb = a.vptr[g0], vlen = a.vptr[g0 + P] - vb;
-    for (int i = lane; i < vlen; i += 64) vl[i] = a.vq[vb + i];
+    for (int i = threadIdx.x; i <= P; i += THREADS) vpl[i] = a.vptr[g0 + i] - vb;
+    for (int i = threadIdx.x; i < vlen; i += THREADS) vl[i] = a.vq[vb + i];
     const float* __restrict__ G = a.G;
     const float* __restrict__ U = a.U;
     float* __restrict__ Yk = a.yptr[k + 1];
+    const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+    // row pairs: wave w handles pairs w, w + 4, ...; lane half selects the row of the pair
     bool bad_y = false;
-    for (int p0 = 0; p0 < P; p0 += UP_CH) {
-        float gv[UP_CH], yv[UP_CH];
+    for (int q0 = w; 2 * q0 < P; q0 += WAVES * UP_CH) {
+        f32x4 gv[UP_CH], yv[UP_CH];
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
-            const int p = p0 + u;
-            gv[u] = 0.0f;
-            yv[u] = 0.0f;
+            const int p = 2 * (q0 + WAVES * u) + half;
+            gv[u] = yv[u] = z4;
             if (p < P && cv) {
-                if (!gzero) gv[u] = G[base + (size_t)p * n];                 // :216-218
-                if (!yzero) yv[u] = ys[base + (size_t)p * n];
+                if (!gzero) gv[u] = *(const f32x4*)(G + base + (size_t)p * n);       // :216-218
+                if (!yzero) yv[u] = *(const f32x4*)(ys + base + (size_t)p * n);
             }
         }
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
-            const int p = p0 + u;
-            if (p >= P) break;
-            float v = 0.0f;
-            if (cv) {
-                v = clamp_t(yv[u] - hyp_at(a, s, 0, p) * gv[u], -vclip, vclip);   // :221-225
-                Yk[base + (size_t)p * n] = v;
-                bad_y |= !finitef(v);
+            const int p = 2 * (q0 + WAVES * u) + half;
+            if (p < P) {
+                f32x4 v = z4;
+                if (cv) {
+                    const float al = hyp_at(a, s, 0, p);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] = clamp_t(yv[u][r] - al * gv[u][r], -vclip, vclip);   // :221-225
+                        bad_y |= !finitef(v[r]);
+                    }
+                    *(f32x4*)(Yk + base + (size_t)p * n) = v;
+                }
+                *(f32x4*)(yl + p * UCB + cl) = v;
             }
-            yl[p * 64 + lane] = v;
         }
     }
+    __syncthreads();
     bool bad_u = false;
-    for (int p0 = 0; p0 < P; p0 += UP_CH) {
-        float uv[UP_CH];
+    for (int q0 = w; 2 * q0 < P; q0 += WAVES * UP_CH) {
+        f32x4 uv[UP_CH];
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
-            const int p = p0 + u;
-            uv[u] = (p < P && cv && !uzero) ? U[base + (size_t)p * n] : 0.0f;
+            const int p = 2 * (q0 + WAVES * u) + half;
+            uv[u] = (p < P && cv && !uzero) ? *(const f32x4*)(U + base + (size_t)p * n) : z4;
         }
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
-            const int p = p0 + u;
-            if (p >= P) break;
-            const float yp = yl[p * 64 + lane];
-            float acc = 0.0f;
-            // the agent's visit list from LDS, four entries' y reads in flight, summed in order
-            const uint8_t* vp = vl + (a.vptr[g0 + p] - vb);
-            const int len = a.vptr[g0 + p + 1] - a.vptr[g0 + p];
-            int t = 0;
-            for (; t + 4 <= len; t += 4) {
-                const float y0 = yl[(int)vp[t] * 64 + lane], y1 = yl[(int)vp[t + 1] * 64 + lane];
-                const float y2 = yl[(int)vp[t + 2] * 64 + lane], y3 = yl[(int)vp[t + 3] * 64 + lane];
-                acc = acc + (yp - y0);
-                acc = acc + (yp - y1);
-                acc = acc + (yp - y2);
-                acc = acc + (yp - y3);
+            const int p = 2 * (q0 + WAVES * u) + half;
+            if (p >= P || !cv) continue;
+            const f32x4 yp = *(const f32x4*)(yl + p * UCB + cl);
+            f32x4 acc = z4;
+            const int v0 = vpl[p], v1 = vpl[p + 1];
+            for (int t = v0; t < v1; ++t) {
+                const f32x4 yq = *(const f32x4*)(yl + (int)vl[t] * UCB + cl);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[r] = acc[r] + (yp[r] - yq[r]);
             }
-            for (; t < len; ++t) acc = acc + (yp - yl[(int)vp[t] * 64 + lane]);
-            if (a.variant != 0) acc = clamp_t(acc, -20.0f, 20.0f);             // :229
-            if (cv) {
-                const size_t off = base + (size_t)p * n;
-                const float un = clamp_t(uv[u] + acc * hyp_at(a, s, 3, p), -vclip, vclip);   // :231-232
-                a.U_next[off] = un;
-                a.D_next[off] = acc;
-                bad_u |= !finitef(un);
+            const float et = hyp_at(a, s, 3, p);
+            f32x4 un;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (a.variant != 0) acc[r] = clamp_t(acc[r], -20.0f, 20.0f);          // :229
+                un[r] = clamp_t(uv[u][r] + acc[r] * et, -vclip, vclip);              // :231-232
+                bad_u |= !finitef(un[r]);
             }
+            const size_t off = base + (size_t)p * n;
+            *(f32x4*)(a.U_next + off) = un;
+            *(f32x4*)(a.D_next + off) = acc;
         }
     }
     flag_or(a.flags + GNN_F_YNB(k), bad_y);
@@ -466,16 +476,15 @@ hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* o
 hipError_t gnn_launch_step(const GnnArgs& a, int k, hipStream_t st) {
     const int g = grid_for((size_t)a.B * a.P * a.n / 4, gnn::THREADS, 4096);
     hipLaunchKernelGGL(gnn::grad_kernel, dim3(g), dim3(gnn::THREADS), 0, st, a, k);
-    const int items = a.B * ((a.n + 63) / 64);
-    const size_t lds = 4 * (size_t)gnn::WAVES * (a.P * 64 + gnn::update_visit_words(a.P));
+    const int items = a.B * ((a.n + gnn::UCB - 1) / gnn::UCB);
+    const size_t lds = gnn::update_lds_bytes(a.P);
     auto kern = gnn::update_kernel;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, dim3((items + gnn::WAVES - 1) / gnn::WAVES), dim3(gnn::THREADS), lds, st,
-                       a, k, items);
+    hipLaunchKernelGGL(kern, dim3(items), dim3(gnn::THREADS), lds, st, a, k, items);
     return hipGetLastError();
 }
 
