@@ -182,9 +182,11 @@ def main():
                 traffic = None
 
         parity = check_parity(O, model, A, b, G, dev, P, n, m, K)
-        cpu = None if a.no_cpu_baseline else cpu_baseline(O, A, b, G, model, P, n, m, K,
-                                                          a.cpu_baseline_seconds)
-        extras = None if a.no_extras else secondary(O, dev, A, b, x, G, model, P, n, m, K, B)
+        # the CPU baseline and the single-GPU secondary measurements belong to the N = 1 run
+        cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(
+            O, A, b, G, model, P, n, m, K, a.cpu_baseline_seconds)
+        extras = None if (a.no_extras or world > 1) else secondary(O, dev, A, b, x, G, model, P, n,
+                                                                   m, K, B)
         out = {
             "metric": "ADMM-iters/sec (node), batch=4096 P=5 n=256 K=25; final-iter MSE vs ref",
             "value": value,
