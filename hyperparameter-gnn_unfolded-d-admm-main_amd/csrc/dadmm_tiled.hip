@@ -61,6 +61,12 @@ __device__ __forceinline__ void clips(int variant, int k, float& gclip, float& v
 constexpr int HALVES = 2;            // 16-sample MFMA column blocks per workgroup (32 samples):
                                      // every A / A^T operand load feeds two fma chains
 constexpr int ST = HALVES * BT;      // samples per workgroup
+constexpr int CH = 2;                // n-tiles per chunk of the update phase
+constexpr int RG = CH * HALVES;      // row groups per chunk
+struct Chunk {                       // one chunk's operands
+    f32x4 yp[RG], up[RG], dv[RG];
+    f32x4 atv[CH][M_PAD / 16];
+};
 
 // blockIdx -> (tile, agent) so that the P workgroups of one sample tile run on the same XCD
 // (dispatch is round-robin over the 8 XCDs, each with its own L2): the neighbour tiles a
@@ -102,6 +108,47 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int H = a.hyp_rows;
     const int hp = H == 1 ? 0 : p;
     uint32_t status = 0;
+
+    // update-phase operands; chunk 0 is issued now, so that it lands with the y tile
+    const float* Uprev = a.Ubuf[(k + 1) & 1];     // U_{k-1}   (k = 0: unused)
+    const float* usrc = k == 0 ? a.U0 : Uprev;
+    const float* dsrc = k == 0 ? a.d0 : a.delta;  // delta_k
+    const int ntw = (NP / 16 - w + WAVES - 1) / WAVES;   // n-tiles of this wave: w, w + 4, ...
+    const float* atbase = a.At + ((size_t)p * NP + j) * M_PAD + 4 * h;
+    const bool ylds = STAGE && !final_only;       // own rows from the staged tile
+    size_t srow[HALVES];
+#pragma unroll
+    for (int hh = 0; hh < HALVES; ++hh) {
+        const int s = tile * ST + hh * BT + j;
+        srow[hh] = (size_t)(s < B ? s : 0) * P;
+    }
+    auto load_chunk = [&](int c0, Chunk& c) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int nb = w + WAVES * (c0 + i);
+            const int n0 = 16 * nb + 4 * h;
+            const bool tile_ok = c0 + i < ntw;
+            if (!final_only && tile_ok) {
+#pragma unroll
+                for (int t = 0; t < M_PAD / 16; ++t)
+                    c.atv[i][t] = *(const f32x4*)(atbase + (size_t)16 * nb * M_PAD + 16 * t);
+            }
+#pragma unroll
+            for (int hh = 0; hh < HALVES; ++hh) {
+                const int g = i * HALVES + hh;
+                const int s = tile * ST + hh * BT + j;
+                const size_t off = (srow[hh] + p) * n + n0;
+                c.yp[g] = c.up[g] = c.dv[g] = (f32x4){0, 0, 0, 0};
+                if (tile_ok && s < B && n0 < n) {
+                    if (!ylds) c.yp[g] = *(const f32x4*)(yk + off);
+                    c.up[g] = *(const f32x4*)(usrc + off);
+                    c.dv[g] = *(const f32x4*)(dsrc + off);
+                }
+            }
+        }
+    };
+    Chunk cA;
+    if (ntw > 0) load_chunk(0, cA);
 
     if constexpr (STAGE) {
         if (!final_only) {
@@ -227,7 +274,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
         float gtmp;
         clips(a.variant, k - 1, gtmp, vclip_prev);
     }
-    const float* Uprev = a.Ubuf[(k + 1) & 1];     // U_{k-1}   (k = 0: unused)
     float* Ucur = final_only ? a.U_out : a.Ubuf[k & 1];   // U_k
 
     // per-lane data of the two samples this lane serves
@@ -245,74 +291,43 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
         }
     }
     bool bad_u0 = false, bad_g = false, bad_y = false;
-    const float* atbase = a.At + ((size_t)p * NP + j) * M_PAD + 4 * h;
-    // The wave's n-tiles nb = w, w + 4, ... are processed CH at a time; each chunk issues its
-    // loads together (y_k rows, U_{k-1} rows, delta_k rows, A^T rows)
-#ifndef DADMM_TILED_CH
-#define DADMM_TILED_CH 2
-#endif
-    constexpr int CH = DADMM_TILED_CH;
-    constexpr int RG = CH * HALVES;            // row groups per chunk
-    const int ntw = (NP / 16 - w + WAVES - 1) / WAVES;   // tiles of this wave
-    const float* dsrc = k == 0 ? a.d0 : a.delta;   // delta_k
-    size_t srow[HALVES];
-#pragma unroll
-    for (int hh = 0; hh < HALVES; ++hh) {
-        const int s = tile * ST + hh * BT + j;
-        srow[hh] = (size_t)(s < B ? s : 0) * P;
-    }
-    for (int c0 = 0; c0 < ntw; c0 += CH) {
+    auto compute_chunk = [&](int c0, Chunk& c) {
         int n0[CH];
         bool okr[RG];
         size_t off[RG];
-        f32x4 yp[RG], up[RG], dv[RG], uv[RG];
-        f32x4 atv[CH][M_PAD / 16];
+        f32x4 uv[RG];
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
-            const int nb = w + WAVES * (c0 + i);
-            n0[i] = 16 * nb + 4 * h;
-            const bool tile_ok = c0 + i < ntw;
-            if (!final_only && tile_ok) {
-#pragma unroll
-                for (int t = 0; t < M_PAD / 16; ++t)
-                    atv[i][t] = *(const f32x4*)(atbase + (size_t)16 * nb * M_PAD + 16 * t);
-            }
+            n0[i] = 16 * (w + WAVES * (c0 + i)) + 4 * h;
 #pragma unroll
             for (int hh = 0; hh < HALVES; ++hh) {
                 const int g = i * HALVES + hh;
                 const int s = tile * ST + hh * BT + j;
-                okr[g] = tile_ok && s < B && n0[i] < n;
+                okr[g] = c0 + i < ntw && s < B && n0[i] < n;
                 off[g] = (srow[hh] + p) * n + n0[i];
-                yp[g] = up[g] = dv[g] = (f32x4){0, 0, 0, 0};
-                if (okr[g]) {
-                    if (STAGE && !final_only)   // (the final dual update stages nothing)
-                        yp[g] = *(const f32x4*)(Ylds + (hh * BT + j) * NP + 4 * ((n0[i] >> 2) ^ j));
-                    else
-                        yp[g] = *(const f32x4*)(yk + off[g]);
-                    up[g] = *(const f32x4*)((k == 0 ? a.U0 : Uprev) + off[g]);
-                    dv[g] = *(const f32x4*)(dsrc + off[g]);
-                }
+                if (ylds && okr[g])
+                    c.yp[g] = *(const f32x4*)(Ylds + (hh * BT + j) * NP + 4 * ((n0[i] >> 2) ^ j));
             }
         }
 #pragma unroll
         for (int g = 0; g < RG; ++g) {
             if (!okr[g]) continue;
             if (k == 0) {
-                uv[g] = up[g];
+                uv[g] = c.up[g];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) bad_u0 |= !finitef(uv[g][r]);
             } else {
                 if (a.variant != 0) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) dv[g][r] = tclamp(dv[g][r], -20.0f, 20.0f);   // :229
+                    for (int r = 0; r < 4; ++r) c.dv[g][r] = tclamp(c.dv[g][r], -20.0f, 20.0f);   // :229
                 }
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    uv[g][r] = tclamp(up[g][r] + dv[g][r] * et_prev, -vclip_prev, vclip_prev);
+                    uv[g][r] = tclamp(c.up[g][r] + c.dv[g][r] * et_prev, -vclip_prev, vclip_prev);
             }
             *(f32x4*)(Ucur + off[g]) = uv[g];          // U_k (the ping-pong buffer / U_out)
         }
-        if (final_only) continue;
+        if (final_only) return;
         // GEMM2 rows of these tiles + gradient assembly + primal update (:69-93)
 #pragma unroll
         for (int g = 0; g < RG; ++g) {
@@ -322,16 +337,16 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
             for (int t = 0; t < M_PAD / 16; ++t)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) gc = mfma4(atv[i][t][r], rv[hh][t][r], gc);
+                for (int r = 0; r < 4; ++r) gc = mfma4(c.atv[i][t][r], rv[hh][t][r], gc);
             if (okr[g]) {
                 f32x4 yn;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float y = yp[g][r];
+                    const float y = c.yp[g][r];
                     const float st = sign_times(y, ta);   // sign(y) * tau
                     float gr = gc[r] + st;
                     gr = gr + uv[g][r] * dg[hh];
-                    gr = gr + dv[g][r] * rh;
+                    gr = gr + c.dv[g][r] * rh;
                     bad_g |= gr != gr;
                     gr = tclamp(gr, -gclip, gclip);
                     const float v = tclamp(y - al * gr, -vclip, vclip);
@@ -341,6 +356,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
                 *(f32x4*)(a.Y + (size_t)k * S + off[g]) = yn;
             }
         }
+    };
+    for (int c0 = 0; c0 < ntw; c0 += CH) {
+        if (c0 > 0) load_chunk(c0, cA);
+        compute_chunk(c0, cA);
     }
     status |= (bad_u0 ? 2u : 0u) | (bad_g ? 4u : 0u) | (bad_y ? 8u : 0u);
     if (a.status != nullptr) {
