@@ -402,11 +402,41 @@ static int pick_tiles(HyperArgs& a, int epi) {
     return wr;
 }
 
+// Split-K linears (the decoder's, HYPER_EPI_BIAS): the largest row tile whose grid, times the
+// K splits that the deep K then allows, still gives ~two workgroups per CU. Big tiles cut the
+// operand re-reads (x is read once per column tile, W once per row tile: configs[4]'s
+// 1024 x 20000 x 400 decoder input moved 1.6 GB at 32-row tiles).
+static int split_k(long tiles, int K) {
+    int s = 1;
+    // split K while the grid is under ~8 workgroups per CU and every split keeps >= 16 k-steps
+    while (tiles * s * 2 <= 2048 && K / 16 / (s * 2) >= 16 && s < 32) s *= 2;
+    return s;
+}
+static int pick_split_tiles(HyperArgs& a, int K, int& splits) {
+    a.gn = (a.N + hyper::TN - 1) / hyper::TN;
+    int wr = 0;
+    for (int cand = 4; cand >= 1; cand >>= 1) {
+        wr = cand;
+        a.S_t = 32 * cand;
+        a.gm = (a.rows + a.S_t - 1) / a.S_t;
+        splits = split_k((long)a.gm * a.gn, K);
+        if ((long)a.gm * a.gn * splits >= 480) break;
+    }
+    return wr;
+}
+
 hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st) {
     const int units = epi == HYPER_EPI_GCN ? a.B : a.rows;
     if (units <= 0 || a.N <= 0) return hipSuccess;
     if (a.K1 < a.K && (a.K1 & 15)) return hipErrorInvalidValue;
-    const int wr = pick_tiles(a, epi);
+    int wr = 0;
+    if (epi == HYPER_EPI_BIAS && a.splits > 1) {
+        int sp = 0;
+        wr = pick_split_tiles(a, a.K, sp);
+        if (sp != a.splits) wr = pick_tiles(a, epi);   // caller's own split count: plain tiling
+    } else {
+        wr = pick_tiles(a, epi);
+    }
     if (wr == 0) return hipErrorInvalidValue;
     if (a.splits < 1) a.splits = 1;
     const int grid = a.gm * a.gn * a.splits;
@@ -422,12 +452,9 @@ int hyper_linear_splits(int rows, int K, int N) {
     HyperArgs a{};
     a.rows = rows;
     a.N = N;
-    const int wr = pick_tiles(a, HYPER_EPI_BIAS);
-    if (wr == 0) return 1;
-    const long tiles = (long)a.gm * a.gn;
+    if (rows <= 0 || N <= 0) return 1;
     int s = 1;
-    // split K while the grid is under ~2 workgroups per CU and every split keeps >= 16 k-steps
-    while (tiles * s * 2 <= 512 && K / 16 / (s * 2) >= 16 && s < 32) s *= 2;
+    pick_split_tiles(a, K, s);
     return s;
 }
 
