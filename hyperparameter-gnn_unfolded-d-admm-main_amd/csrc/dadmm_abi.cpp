@@ -245,6 +245,8 @@ int gnn_common(const dadmm_dims* d, dadmm::GnnArgs* a) {
         return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
                     dadmm::M_PAD);
     if ((d->n & 3) != 0) return fail(DADMM_EUNSUPPORTED, "n=%d: needs n %% 4 == 0 (zero-pad n)", d->n);
+    if ((size_t)d->B * d->P * d->n * 4 >= ((size_t)1 << 31))   // 32-bit buffer offsets (gram)
+        return fail(DADMM_EUNSUPPORTED, "B*P*n*4 >= 2^31 bytes per iterate (split the batch)");
     *a = dadmm::GnnArgs{};
     a->B = d->B;
     a->P = d->P;

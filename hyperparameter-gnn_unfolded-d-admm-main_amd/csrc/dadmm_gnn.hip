@@ -101,9 +101,8 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad;
     const int tile = blockIdx.x / P, p = blockIdx.x % P;
-    const int YS = NP + 4, RS = M_PAD + 4;
-    float* Xlds = lds;               // [16][YS]
-    float* Rlds = lds + BT * YS;     // [16][RS]
+    const int RS = M_PAD + 4;
+    float* Rlds = lds;               // [16][RS]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int j = lane & 15, h = lane >> 4;
     const int s = tile * BT + j;
@@ -112,25 +111,40 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
     if (mode == 0) {
         bool zero = false;
         const float* xs = x_raw != nullptr ? x_raw : y_source(a, k, zero);
-        const int nc4 = NP / 4;
-        for (int idx = threadIdx.x; idx < BT * nc4; idx += THREADS) {
-            const int jj = idx / nc4, c = 4 * (idx % nc4);
-            const int s2 = tile * BT + jj;
-            f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (s2 < B && c < n && !zero) v = *(const f32x4*)(xs + ((size_t)s2 * P + p) * n + c);
-            *(f32x4*)(Xlds + jj * YS + c) = v;
-        }
-        __syncthreads();
-        // GEMM1: R = A_p x (chain from +0); wave w = m-block w
+        // GEMM1: R = A_p x (chain from +0); wave w = m-block w. Both operands stream through a
+        // ring of GD steps (the loads of step t + GD issue after step t's MFMAs): A rows from L2,
+        // the x columns (16 samples) from L2/HBM through a buffer descriptor whose range check
+        // returns 0 for columns past n, samples past B and a guard-zeroed x. NP / 16 is a
+        // multiple of GD.
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
         if (16 * w < m) {
             const float* arow = a.A + ((size_t)p * M_PAD + 16 * w + j) * NP + 4 * h;
-            const float* brow = Xlds + j * YS + 4 * h;
-            for (int t = 0; t < NP / 16; ++t) {
-                const f32x4 av = *(const f32x4*)(arow + 16 * t);
-                const f32x4 bv = *(const f32x4*)(brow + 16 * t);
+            const uint32_t xbytes = zero ? 0u : (uint32_t)((size_t)B * P * n * 4);
+            const __amdgpu_buffer_rsrc_t rx =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), 0, (int)xbytes, 0x00020000);
+            const uint32_t xoff = sv ? (uint32_t)((((size_t)s * P + p) * n + 4 * h) * 4) : 0x80000000u;
+            auto ldx = [&](int t) -> f32x4 {
+                return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                    rx, 16 * t + 4 * h < n && sv ? xoff + 64u * t : 0x80000000u, 0, 0));
+            };
+            constexpr int GD = 4;
+            const int T = NP / 16;
+            f32x4 ar[GD], xr[GD];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc = mfma4(av[r], bv[r], acc);
+            for (int u = 0; u < GD; ++u) {
+                ar[u] = *(const f32x4*)(arow + 16 * u);
+                xr[u] = ldx(u);
+            }
+            for (int t0 = 0; t0 < T; t0 += GD) {
+#pragma unroll
+                for (int u = 0; u < GD; ++u) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc = mfma4(ar[u][r], xr[u][r], acc);
+                    if (t0 + GD + u < T) {
+                        ar[u] = *(const f32x4*)(arow + 16 * (t0 + GD + u));
+                        xr[u] = ldx(t0 + GD + u);
+                    }
+                }
             }
         }
         *(f32x4*)(Rlds + j * RS + 16 * w + 4 * h) = acc;
@@ -145,21 +159,35 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
         *(f32x4*)(Rlds + j * RS + 16 * w + 4 * h) = v;
     }
     __syncthreads();
-    // GEMM2: out = A_p^T R (chain from +0); wave w takes n-tiles w, w + 4, ...
+    // GEMM2: out = A_p^T R (chain from +0); wave w takes n-tiles w, w + 4, ...; the m-blocks
+    // past m (zero rows of R and of the padded operator) are skipped, and the A^T rows of the
+    // next tile load under the current tile's MFMAs
     f32x4 rv[M_PAD / 16];
 #pragma unroll
     for (int t = 0; t < M_PAD / 16; ++t) rv[t] = *(const f32x4*)(Rlds + j * RS + 16 * t + 4 * h);
+    const int mbk = (m + 15) / 16;
+    const float* atb = a.At + ((size_t)p * NP + j) * M_PAD + 4 * h;
+    f32x4 at_cur[M_PAD / 16], at_nxt[M_PAD / 16];
+    auto load_at = [&](f32x4 (&dst)[M_PAD / 16], int nb) {
+#pragma unroll
+        for (int t = 0; t < M_PAD / 16; ++t)
+            if (t < mbk) dst[t] = *(const f32x4*)(atb + (size_t)16 * nb * M_PAD + 16 * t);
+    };
+    if (w < NP / 16) load_at(at_cur, w);
     for (int nb = w; nb < NP / 16; nb += WAVES) {
-        const float* atrow = a.At + ((size_t)p * NP + 16 * nb + j) * M_PAD + 4 * h;
+        if (nb + WAVES < NP / 16) load_at(at_nxt, nb + WAVES);
         f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int t = 0; t < M_PAD / 16; ++t) {
-            const f32x4 av = *(const f32x4*)(atrow + 16 * t);
+            if (t < mbk) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) gc = mfma4(av[r], rv[t][r], gc);
+                for (int r = 0; r < 4; ++r) gc = mfma4(at_cur[t][r], rv[t][r], gc);
+            }
         }
         const int n0 = 16 * nb + 4 * h;
         if (sv && n0 < n) *(f32x4*)(out + ((size_t)s * P + p) * n + n0) = gc;
+#pragma unroll
+        for (int t = 0; t < M_PAD / 16; ++t) at_cur[t] = at_nxt[t];
     }
 }
 
@@ -457,7 +485,7 @@ hipError_t gnn_launch_check0(const GnnArgs& a, const float* y0, hipStream_t st) 
     return hipGetLastError();
 }
 
-size_t gnn_gram_lds(int n_pad) { return 4 * (size_t)(BT * (n_pad + 4) + BT * (M_PAD + 4)); }
+size_t gnn_gram_lds(int n_pad) { (void)n_pad; return 4 * (size_t)(BT * (M_PAD + 4)); }
 
 hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* out, int mode,
                            hipStream_t st) {
