@@ -159,11 +159,12 @@ int dadmm_prologue(uint64_t seed, uint64_t offset, int64_t numel, int32_t n, int
 /* Bytes of device scratch dadmm_forward_tiled needs for `d` (256-byte aligned pointer). */
 size_t dadmm_tiled_scratch_bytes(const dadmm_dims* d);
 
-/* The K-step forward, one launch per iteration with the state in HBM — the path for shapes the fused
- * kernel cannot hold on chip (P > 6 or n > 256; e.g. P = 16, n = 512). Each (16-sample tile, agent)
- * workgroup forms delta_k from its neighbours' y_k (visit lists, the reference's order), applies
- * the deferred dual update, the factored gradient GEMM pair and the primal update; Y is
- * bit-identical to dadmm_forward_stepwise's on guard-free inputs.
+/* The K-step forward, two launches per iteration with the state in HBM — the path for shapes the
+ * fused kernel cannot hold on chip (P > 6 or n > 256; e.g. P = 16, n = 512). A consensus launch forms
+ * delta_k for every agent of a sample from y_k (visit lists, the reference's order; scratch), then
+ * each (32-sample tile, agent) workgroup applies the deferred dual update, the factored gradient
+ * GEMM pair and the primal update; Y is bit-identical to dadmm_forward_stepwise's on guard-free
+ * inputs. Scratch: the U_k ping-pong pair and delta_k (dadmm_tiled_scratch_bytes).
  * Replaces: the same loop as dadmm_forward (unfolded_DLASSO.py:45, 53-109).
  * Like dadmm_forward it only FLAGS the reference's guards in `status` (OR-ed; caller zeroes it):
  * enqueue dadmm_forward_stepwise with DADMM_GATE_ON behind it for the exact guarded result.
