@@ -82,6 +82,25 @@ def test_recurrence_bit_exact_given_hypernetwork_outputs(cuda, mode, per_sample)
     assert np.array_equal(Y[..., 0].cpu().numpy(), Yo), np.abs(Y[..., 0].cpu().numpy() - Yo).max()
 
 
+@pytest.mark.parametrize("P,m,n,B,K", [
+    (13, 40, 200, 9, 3),    # n past one 128-column update block, m = 40: a partial gram m-block
+    (50, 32, 1024, 2, 2),   # BASELINE configs[4]'s agent count and signal length
+])
+def test_recurrence_bit_exact_larger_shapes(cuda, P, m, n, B, K):
+    """The update kernel's column blocks / agent-row pairs and the gram kernel's operand ring and
+    m-block skip at shapes beyond the small cases above."""
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", True, seed=3)
+    model.eval()
+    rec = _recording(model)
+    with torch.no_grad():
+        Y, _ = model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in inits))
+    assert int(model.last_status.item()) == 0
+    table = _hyp_table(rec, B, P)
+    Yo, _, st = O.forward_f32_gram(A, b, graphs, table, *inits, variant=1, hyp_mode=1)
+    assert st == 0
+    assert np.array_equal(Y[..., 0].cpu().numpy(), Yo), np.abs(Y[..., 0].cpu().numpy() - Yo).max()
+
+
 def test_hypernetwork_matches_numpy_restatement(cuda):
     P, m, n, B, K = 5, 32, 64, 12, 2
     model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", True)
