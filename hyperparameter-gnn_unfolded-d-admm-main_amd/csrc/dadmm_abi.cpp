@@ -48,6 +48,13 @@ int check_dims(const dadmm_dims* d) {
 }
 
 int n_pad_of(const dadmm_dims* d) { return 64 * dadmm::fused_nt(d->n); }
+int m_pad_of(const dadmm_dims* d) { return dadmm::m_pad_of(d->m); }
+
+int check_m(const dadmm_dims* d) {
+    if (d->m > dadmm::M_MAX)
+        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent", d->m, dadmm::M_MAX);
+    return DADMM_OK;
+}
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -61,7 +68,8 @@ const char* dadmm_last_error(void) { return g_err; }
 
 size_t dadmm_operator_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;
-    return 2 * sizeof(float) * (size_t)d->P * dadmm::M_PAD * (size_t)n_pad_of(d);
+    if (check_m(d) != DADMM_OK) return 0;
+    return 2 * sizeof(float) * (size_t)d->P * m_pad_of(d) * (size_t)n_pad_of(d);
 }
 
 int dadmm_prepare_operator(const dadmm_dims* d, const float* A, void* op, void* stream) {
@@ -69,12 +77,10 @@ int dadmm_prepare_operator(const dadmm_dims* d, const float* A, void* op, void* 
     if (rc) return rc;
     if (A == nullptr || op == nullptr) return fail(DADMM_EINVAL, "A/op is NULL");
     if (!aligned16(op)) return fail(DADMM_EINVAL, "op workspace must be 16-byte aligned");
-    if (d->m > dadmm::M_PAD)
-        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
-                    dadmm::M_PAD);
+    if ((rc = check_m(d)) != DADMM_OK) return rc;
     const int np = n_pad_of(d);
     float* Apad = (float*)op;
-    float* Atpad = Apad + (size_t)d->P * dadmm::M_PAD * np;
+    float* Atpad = Apad + (size_t)d->P * m_pad_of(d) * np;
     hipError_t e = dadmm::launch_prepare(A, Apad, Atpad, d->P, d->m, d->n, np, (hipStream_t)stream);
     if (e != hipSuccess) return fail(DADMM_EHIP, "prepare launch: %s", hipGetErrorString(e));
     return ok();
@@ -87,8 +93,8 @@ namespace {
 // shape checks shared by the fused forward (plain / recording) and the fused adjoint; on success
 // *graph and *nt select the compiled configuration
 int check_fused_shape(const dadmm_dims* d, const uint32_t* nbr_order, int* graph, int* nt) {
-    if (d->m > dadmm::M_PAD)
-        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
+    if (d->m > dadmm::M_PAD)   // the fused kernels hold one m-group of R on chip
+        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent: not a fused shape", d->m,
                     dadmm::M_PAD);
     if ((d->n & 3) != 0)
         return fail(DADMM_EUNSUPPORTED, "n=%d: the fused kernel needs n %% 4 == 0 (zero-pad n)", d->n);
@@ -129,7 +135,7 @@ int forward_impl(const dadmm_dims* d, const void* op, const float* b, const uint
     const int np = 64 * nt;
     dadmm::FusedArgs a;
     a.A = (const float*)op;
-    a.At = a.A + (size_t)d->P * dadmm::M_PAD * np;
+    a.At = a.A + (size_t)d->P * m_pad_of(d) * np;
     a.b = b;
     a.nbr = nbr;
     a.nbr_order = nbr_order;
@@ -209,7 +215,7 @@ int dadmm_backward(const dadmm_dims* d, const void* op, const uint64_t* nbr,
     const int np = 64 * nt;
     dadmm::BackwardArgs a;
     a.A = (const float*)op;
-    a.At = a.A + (size_t)d->P * dadmm::M_PAD * np;
+    a.At = a.A + (size_t)d->P * m_pad_of(d) * np;
     a.nbr = nbr;
     a.nbr_order = nbr_order;
     a.deg = deg;
@@ -236,14 +242,81 @@ int dadmm_backward(const dadmm_dims* d, const void* op, const uint64_t* nbr,
     return ok();
 }
 
+size_t dadmm_adjoint_scratch_bytes(const dadmm_dims* d) {
+    if (check_dims(d) != DADMM_OK) return 0;
+    const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);
+    const size_t part = sizeof(float) * (size_t)dadmm::adjoint_workgroups(d->B, d->n) * d->K * d->P * 4;
+    return 3 * state + align256(part > 0 ? part : 16);
+}
+
+int dadmm_adjoint(const dadmm_dims* d, const void* op, const int32_t* visit_ptr,
+                  const uint8_t* visit_q, const float* deg, const float* hyp, const float* y0,
+                  const float* d0, const float* Y, const float* Grec, const float* Urec,
+                  const float* gY, float* dhyp, void* scratch, void* stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (d->K == 0) return ok();
+    if (!dhyp) return fail(DADMM_EINVAL, "dhyp is NULL");
+    if (d->B == 0) {
+        hipError_t e = hipMemsetAsync(dhyp, 0, sizeof(float) * (size_t)d->K * d->hyp_rows * 4,
+                                      (hipStream_t)stream);
+        if (e != hipSuccess) return fail(DADMM_EHIP, "memset: %s", hipGetErrorString(e));
+        return ok();
+    }
+    if (!op || !visit_ptr || !visit_q || !deg || !hyp || !y0 || !d0 || !Y || !Grec || !Urec || !gY ||
+        !scratch)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(op) || !aligned16(Y) || !aligned16(y0) || !aligned16(d0) || !aligned16(Grec) ||
+        !aligned16(Urec) || !aligned16(gY))
+        return fail(DADMM_EINVAL, "op, Y, y0, d0, Grec, Urec and gY must be 16-byte aligned");
+    if (((uintptr_t)scratch & 255u) != 0) return fail(DADMM_EINVAL, "scratch must be 256-byte aligned");
+    if ((rc = check_m(d)) != DADMM_OK) return rc;
+    if ((d->n & 3) != 0) return fail(DADMM_EUNSUPPORTED, "n=%d: needs n %% 4 == 0 (zero-pad n)", d->n);
+    if ((size_t)d->B * d->P * d->n * 4 >= ((size_t)1 << 31))   // 32-bit buffer offsets (gram)
+        return fail(DADMM_EUNSUPPORTED, "B*P*n*4 >= 2^31 bytes per iterate (split the batch)");
+    if (dadmm::adjoint_lds_bytes(d->P) > 160 * 1024 || dadmm::gnn_gram_lds(m_pad_of(d)) > 160 * 1024)
+        return fail(DADMM_EUNSUPPORTED, "P=%d / m=%d: the adjoint's LDS tiles do not fit", d->P, d->m);
+    const int np = n_pad_of(d);
+    const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);
+    char* base = (char*)scratch;
+    dadmm::AdjArgs a{};
+    a.A = (const float*)op;
+    a.At = a.A + (size_t)d->P * m_pad_of(d) * np;
+    a.vptr = visit_ptr;
+    a.vq = visit_q;
+    a.deg = deg;
+    a.hyp = hyp;
+    a.y0 = y0;
+    a.d0 = d0;
+    a.Y = Y;
+    a.Grec = Grec;
+    a.Urec = Urec;
+    a.gY = gY;
+    a.yb = (float*)base;
+    a.Ub = (float*)(base + state);
+    a.Gb = (float*)(base + 2 * state);
+    a.partial = (float*)(base + 3 * state);
+    a.B = d->B;
+    a.P = d->P;
+    a.m = d->m;
+    a.m_pad = m_pad_of(d);
+    a.n = d->n;
+    a.n_pad = np;
+    a.K = d->K;
+    a.hyp_rows = d->hyp_rows;
+    a.variant = d->variant;
+    a.graph_shared = d->graph_shared;
+    hipError_t e = dadmm::launch_adjoint(a, dhyp, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "adjoint launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 namespace {
 
 int gnn_common(const dadmm_dims* d, dadmm::GnnArgs* a) {
     int rc = check_dims(d);
     if (rc) return rc;
-    if (d->m > dadmm::M_PAD)
-        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
-                    dadmm::M_PAD);
+    if ((rc = check_m(d)) != DADMM_OK) return rc;
     if ((d->n & 3) != 0) return fail(DADMM_EUNSUPPORTED, "n=%d: needs n %% 4 == 0 (zero-pad n)", d->n);
     if ((size_t)d->B * d->P * d->n * 4 >= ((size_t)1 << 31))   // 32-bit buffer offsets (gram)
         return fail(DADMM_EUNSUPPORTED, "B*P*n*4 >= 2^31 bytes per iterate (split the batch)");
@@ -251,6 +324,7 @@ int gnn_common(const dadmm_dims* d, dadmm::GnnArgs* a) {
     a->B = d->B;
     a->P = d->P;
     a->m = d->m;
+    a->m_pad = m_pad_of(d);
     a->n = d->n;
     a->n_pad = n_pad_of(d);
     a->K = d->K;
@@ -262,7 +336,7 @@ int gnn_common(const dadmm_dims* d, dadmm::GnnArgs* a) {
 
 void set_op(dadmm::GnnArgs* a, const void* op) {
     a->A = (const float*)op;
-    a->At = a->A + (size_t)a->P * dadmm::M_PAD * a->n_pad;
+    a->At = a->A + (size_t)a->P * a->m_pad * a->n_pad;
 }
 
 int hip_rc(hipError_t e, const char* what) {
@@ -308,8 +382,8 @@ int dadmm_gnn_gram(const dadmm_dims* d, const void* op, int32_t k, float* const*
     if (x == nullptr && (k < 0 || k >= d->K)) return fail(DADMM_EINVAL, "k=%d outside [0, K)", k);
     if (!aligned16(op) || !aligned16(out) || (x && !aligned16(x)))
         return fail(DADMM_EINVAL, "op, x and out must be 16-byte aligned");
-    if (dadmm::gnn_gram_lds(a.n_pad) > 160 * 1024)
-        return fail(DADMM_EUNSUPPORTED, "n=%d too large for the gram tile", d->n);
+    if (dadmm::gnn_gram_lds(a.m_pad) > 160 * 1024)
+        return fail(DADMM_EUNSUPPORTED, "m=%d too large for the gram tile", d->m);
     set_op(&a, op);
     a.yptr = yptr;
     a.flags = const_cast<int32_t*>(flags);
@@ -464,18 +538,19 @@ int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
         (U_out != nullptr && !aligned16(U_out)))
         return fail(DADMM_EINVAL, "op, Y, y0, U0, d0 and U_out must be 16-byte aligned");
     if (((uintptr_t)scratch & 255u) != 0) return fail(DADMM_EINVAL, "scratch must be 256-byte aligned");
-    if (d->m > dadmm::M_PAD)
-        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m, dadmm::M_PAD);
+    if (m_pad_of(d) > 2 * dadmm::M_PAD)   // iter_kernel<MB>: MB in {1, 2}
+        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent: not a tiled shape", d->m,
+                    2 * dadmm::M_PAD);
     if ((d->n & 3) != 0) return fail(DADMM_EUNSUPPORTED, "n=%d: needs n %% 4 == 0 (zero-pad n)", d->n);
     if ((size_t)d->B * d->P * d->n * 4 >= ((size_t)1 << 31))
         return fail(DADMM_EUNSUPPORTED, "B*P*n*4 >= 2^31 bytes per iterate (split the batch)");
     const int np = n_pad_of(d);
-    if (dadmm::tiled_lds_bytes(np) > 160 * 1024)
+    if (dadmm::tiled_lds_bytes(np, m_pad_of(d)) > 160 * 1024)
         return fail(DADMM_EUNSUPPORTED, "n=%d: the y tile does not fit the LDS", d->n);
     const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);
     dadmm::TiledArgs a{};
     a.A = (const float*)op;
-    a.At = a.A + (size_t)d->P * dadmm::M_PAD * np;
+    a.At = a.A + (size_t)d->P * m_pad_of(d) * np;
     a.b = b;
     a.vptr = visit_ptr;
     a.vq = visit_q;
@@ -493,6 +568,7 @@ int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
     a.B = d->B;
     a.P = d->P;
     a.m = d->m;
+    a.m_pad = m_pad_of(d);
     a.n = d->n;
     a.n_pad = np;
     a.K = d->K;
@@ -725,9 +801,7 @@ int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
         return fail(DADMM_EINVAL, "Grec and Urec: both or neither");
     if (Grec != nullptr && (!aligned16(Grec) || !aligned16(Urec)))
         return fail(DADMM_EINVAL, "Grec and Urec must be 16-byte aligned");
-    if (d->m > dadmm::M_PAD)
-        return fail(DADMM_EUNSUPPORTED, "m=%d > %d rows per agent is not compiled", d->m,
-                    dadmm::M_PAD);
+    if ((rc = check_m(d)) != DADMM_OK) return rc;
     if ((d->n & 3) != 0)
         return fail(DADMM_EUNSUPPORTED, "n=%d: needs n %% 4 == 0 (zero-pad n)", d->n);
     const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);
@@ -735,7 +809,7 @@ int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
     const int np = n_pad_of(d);
     dadmm::StepArgs a;
     a.A = (const float*)op;
-    a.At = a.A + (size_t)d->P * dadmm::M_PAD * np;
+    a.At = a.A + (size_t)d->P * m_pad_of(d) * np;
     a.b = b;
     a.vptr = visit_ptr;
     a.vq = visit_q;
@@ -755,6 +829,7 @@ int dadmm_forward_stepwise(const dadmm_dims* d, const void* op, const float* b,
     a.B = d->B;
     a.P = d->P;
     a.m = d->m;
+    a.m_pad = m_pad_of(d);
     a.n = d->n;
     a.n_pad = np;
     a.K = d->K;

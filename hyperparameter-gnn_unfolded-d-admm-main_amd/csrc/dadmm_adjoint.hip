@@ -1,0 +1,195 @@
+// dadmm_adjoint.hip — the adjoint of the unfolded D-ADMM forward for EVERY shape (P <= 64, any m,
+// n % 4 == 0): the shapes the fused adjoint (dadmm_backward.hip: P <= 6, n <= 256, m <= 64) does
+// not hold on chip, e.g. the reference's defaults m = 100, n = 500 (configurations.py:6-9) and
+// BASELINE configs[2] (P = 16, n = 512).
+//
+// Same mathematics as dadmm_backward.hip (see its header): dL/dhyp [K][H][4] for
+// L = sum_k <gY[k], Y[k]>, differentiating the reference's eager ops the way torch autograd does
+// (unfolded_train_new.py:74-80 through unfolded_DLASSO.py:53-107): sign() has zero derivative,
+// clamp passes the gradient where lo <= x <= hi, delta_{k+1} = compute_delta(y_{k+1}) = 2 L y_{k+1}
+// (self-adjoint), delta_0 is a leaf. Masks are re-evaluated with the forward's own float ops.
+//
+// State in HBM (scratch): y_bar, U_bar and gr_bar_{k+1} ([B][P][n] each). Per reverse iteration k:
+//   adj_update_kernel  one wave per (sample, 64 columns), all P agents: delta_{k+1} from Y[k] and
+//                      delta_k from y_k in the reference's visit order (rows staged in LDS), the
+//                      dual-update adjoint, 2 L d_bar, the primal-update / gradient-clamp adjoint;
+//                      dhyp partial sums (wave shuffles, then the workgroup's 4 waves in order);
+//   gram (mode 2)      y_bar += A_p^T (A_p gr_bar), the forward's MFMA GEMM pair
+//                      (dadmm_gnn.hip gram_kernel).
+// A fixed-order reduce (dadmm_backward.hip's) sums the workgroup partials: deterministic.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dadmm_internal.h"
+
+namespace dadmm {
+namespace adj {
+
+constexpr int THREADS = 256;   // 4 waves, one (sample, 64-column) item each
+constexpr int WAVES = 4;
+
+__device__ __forceinline__ float tclamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+__device__ __forceinline__ bool inside(float x, float lo, float hi) { return x >= lo && x <= hi; }
+
+__device__ __forceinline__ void clips(int variant, int k, float& gclip, float& vclip) {
+    if (variant == 0) {
+        gclip = fmaxf(1.0f, 30.0f - (float)k);          // unfolded_DLASSO.py:80
+        vclip = fmaxf(10.0f, 200.0f - (float)(k * 3));  // unfolded_DLASSO.py:92
+    } else {
+        gclip = 10.0f;                                   // gnn_dlasso_models_progressive.py:212
+        vclip = 100.0f;                                  // :224, :232
+    }
+}
+
+// sum over p's visit list of (x_p - x_q): compute_delta's accumulation order (:127-140)
+__device__ __forceinline__ float visit_sum(const float* __restrict__ x, const int32_t* __restrict__ vp,
+                                           const uint8_t* __restrict__ vq, int g0, int p, int lane) {
+    const float xp = x[p * 64 + lane];
+    float acc = 0.0f;
+    const int t1 = vp[g0 + p + 1];
+    for (int t = vp[g0 + p]; t < t1; ++t) acc = acc + (xp - x[(int)vq[t] * 64 + lane]);
+    return acc;
+}
+
+// wave-sum of v into red[p][c] (lane 0 accumulates; one wave owns its red slice)
+__device__ __forceinline__ void wave_accum(float* red, int p, int c, float v, int lane) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) red[p * 4 + c] += v;
+}
+
+__global__ __launch_bounds__(THREADS) void adj_update_kernel(AdjArgs a, int k, int items) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int P = a.P, n = a.n, K = a.K, H = a.hyp_rows;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float* xs = lds + w * (2 * P * 64);        // [P][64] rows of y_{k+1}, then of y_k
+    float* ds = xs + P * 64;                   // [P][64] d_bar (w.r.t. delta_{k+1})
+    float* red = lds + WAVES * 2 * P * 64;     // [WAVES][P][4] partial sums
+    float* rw = red + w * P * 4;
+    for (int i = lane; i < P * 4; i += 64) rw[i] = 0.0f;
+    const int item = blockIdx.x * WAVES + w;
+    const size_t S = (size_t)a.B * P * n;
+    if (item < items) {
+        const int nch = (n + 63) / 64;
+        const int s = item / nch, c = (item % nch) * 64 + lane;
+        const bool cv = c < n;
+        const size_t base = (size_t)s * P * n + (cv ? c : 0);
+        const int g0 = a.graph_shared ? 0 : s * P;
+        float gclip, vclip;
+        clips(a.variant, k, gclip, vclip);
+        auto hyp = [&](int kk, int p, int comp) {
+            return a.hyp[((size_t)kk * H + (H == 1 ? 0 : p)) * 4 + comp];
+        };
+        const float* __restrict__ y1 = a.Y + (size_t)k * S;                    // y_{k+1}
+        const float* __restrict__ yk = k > 0 ? a.Y + (size_t)(k - 1) * S : a.y0;
+        for (int p = 0; p < P; ++p) xs[p * 64 + lane] = cv ? y1[base + (size_t)p * n] : 0.0f;
+        __builtin_amdgcn_wave_barrier();
+        // dual-update adjoint of iteration k (:95-99): w = U_k + delta_{k+1} eta_k
+        for (int p = 0; p < P; ++p) {
+            const float d1 = visit_sum(xs, a.vptr, a.vq, g0, p, lane);
+            const bool md = a.variant == 0 || inside(d1, -20.0f, 20.0f);   // GNN clamp :229
+            const float dcl = a.variant == 0 ? d1 : tclamp(d1, -20.0f, 20.0f);
+            float pe = 0.0f, db = 0.0f;
+            if (cv) {
+                const size_t off = base + (size_t)p * n;
+                const float et = hyp(k, p, 3);
+                const float rh1 = k + 1 < K ? hyp(k + 1, p, 2) : 0.0f;
+                a.yb[off] = a.yb[off] + a.gY[(size_t)k * S + off];            // + gY[k]
+                const float wv = a.Urec[(size_t)k * S + off] + dcl * et;
+                const float wb = inside(wv, -vclip, vclip) ? a.Ub[off] : 0.0f;
+                pe = wb * dcl;
+                db = md ? a.Gb[off] * rh1 + wb * et : 0.0f;
+                a.Ub[off] = wb;
+            }
+            ds[p * 64 + lane] = db;
+            wave_accum(rw, p, 3, pe, lane);
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int p = 0; p < P; ++p) xs[p * 64 + lane] = cv ? yk[base + (size_t)p * n] : 0.0f;
+        __builtin_amdgcn_wave_barrier();
+        // y_bar += 2 L d_bar; primal-update and gradient-clamp adjoint (:73-93)
+        for (int p = 0; p < P; ++p) {
+            const float t = visit_sum(ds, a.vptr, a.vq, g0, p, lane);
+            float dk = 0.0f;
+            if (k > 0) {
+                dk = visit_sum(xs, a.vptr, a.vq, g0, p, lane);
+                if (a.variant != 0) dk = tclamp(dk, -20.0f, 20.0f);
+            }
+            float pa = 0.0f, pt = 0.0f, pr = 0.0f;
+            if (cv) {
+                const size_t off = base + (size_t)p * n;
+                if (k == 0) dk = a.d0[off];
+                const float al = hyp(k, p, 0);
+                const float y = xs[p * 64 + lane];
+                const float gr = a.Grec[(size_t)k * S + off];
+                const float g = tclamp(gr, -gclip, gclip);
+                const float z = y - al * g;
+                const float ybv = a.yb[off] + t;
+                const float zb = inside(z, -vclip, vclip) ? ybv : 0.0f;
+                pa = -zb * g;
+                const float grb = inside(gr, -gclip, gclip) ? -al * zb : 0.0f;
+                pt = grb * sign_times(y, 1.0f);
+                pr = grb * dk;
+                const float dg = a.deg[g0 + p];
+                a.Ub[off] = a.Ub[off] + grb * dg;
+                a.yb[off] = zb;
+                a.Gb[off] = grb;
+            }
+            wave_accum(rw, p, 0, pa, lane);
+            wave_accum(rw, p, 1, pt, lane);
+            wave_accum(rw, p, 2, pr, lane);
+        }
+    }
+    __syncthreads();
+    // workgroup partial: the 4 waves in order -> partial[wg][k][p][c]
+    for (int i = threadIdx.x; i < P * 4; i += THREADS) {
+        float v = 0.0f;
+#pragma unroll
+        for (int ww = 0; ww < WAVES; ++ww) v += red[ww * P * 4 + i];
+        a.partial[((size_t)blockIdx.x * K + k) * P * 4 + i] = v;
+    }
+}
+
+}  // namespace adj
+
+size_t adjoint_lds_bytes(int P) { return 4 * ((size_t)adj::WAVES * 2 * P * 64 + (size_t)adj::WAVES * P * 4); }
+int adjoint_workgroups(int B, int n) {
+    const long items = (long)B * ((n + 63) / 64);
+    return (int)((items + adj::WAVES - 1) / adj::WAVES);
+}
+
+hipError_t launch_adjoint(const AdjArgs& a, float* dhyp, hipStream_t st) {
+    const size_t S = (size_t)a.B * a.P * a.n;
+    hipError_t e;
+    // y_bar = U_bar = gr_bar_K = 0
+    if ((e = hipMemsetAsync(a.yb, 0, 4 * S, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.Ub, 0, 4 * S, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.Gb, 0, 4 * S, st)) != hipSuccess) return e;
+    const size_t lds = adjoint_lds_bytes(a.P);
+    if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+    if (lds > 64 * 1024 &&
+        (e = hipFuncSetAttribute((const void*)adj::adj_update_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
+        return e;
+    const int items = a.B * ((a.n + 63) / 64);
+    const int nwg = adjoint_workgroups(a.B, a.n);
+    GnnArgs g{};
+    g.A = a.A;
+    g.At = a.At;
+    g.B = a.B;
+    g.P = a.P;
+    g.m = a.m;
+    g.m_pad = a.m_pad;
+    g.n = a.n;
+    g.n_pad = a.n_pad;
+    g.K = a.K;
+    for (int k = a.K - 1; k >= 0; --k) {
+        hipLaunchKernelGGL(adj::adj_update_kernel, dim3(nwg), dim3(adj::THREADS), lds, st, a, k, items);
+        if ((e = gnn_launch_gram(g, k, a.Gb, a.yb, 2, st)) != hipSuccess) return e;
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return launch_backward_reduce(a.partial, dhyp, nwg, a.K, a.P, a.hyp_rows, st);
+}
+
+}  // namespace dadmm

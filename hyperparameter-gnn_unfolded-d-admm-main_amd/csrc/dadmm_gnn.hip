@@ -11,7 +11,8 @@
 // with the reference's batch-global NaN/Inf guards (:150-156, :216-218, :235-237) decided through
 // device flag words between launches (no host synchronisation), exactly as dadmm_stepwise.hip
 // does for the unfolded model. Y[k] stores y_{k+1}; a y_next guard that fired is resolved by
-// every later reader (y_source) and by dadmm_gnn_finish for Y[K-1].
+// every later reader (y_source), Y[k] itself is rewritten by the next iteration's grad launch,
+// and Y[K-1] by dadmm_gnn_finish.
 //
 // Operation order (restated bit-for-bit by oracle_forward_f32 with gram_mode = 1): AtAy is one
 // fma chain per row through R = A y (from +0) and A^T R (from +0), each in the fused kernel's
@@ -93,101 +94,125 @@ __global__ __launch_bounds__(THREADS) void check0_kernel(GnnArgs a, const float*
     flag_or(a.flags + GNN_F_UBAD(0), bu);
 }
 
-// ---- gram: out = A^T (A x) per agent (mode 0), or out = A^T b (mode 1) --------------------------
+// ---- gram: out = A^T (A x) per agent (mode 0), out = A^T b (mode 1), out += A^T (A x) (mode 2) --
 // item = (16-sample tile, agent p); x is y_k resolved through the guard flags (x_raw == nullptr)
-// or the raw operand x_raw (the adjoint's AtAy gradient).
+// or the raw operand x_raw (the adjoints' gradient operands).
 __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const float* x_raw,
                                                        float* out, int mode) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad;
+    const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad, MP = a.m_pad;
     const int tile = blockIdx.x / P, p = blockIdx.x % P;
-    const int RS = M_PAD + 4;
+    const int RS = MP + 4;
     float* Rlds = lds;               // [16][RS]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int j = lane & 15, h = lane >> 4;
     const int s = tile * BT + j;
     const bool sv = s < B;
 
-    if (mode == 0) {
+    if (mode != 1) {
         bool zero = false;
         const float* xs = x_raw != nullptr ? x_raw : y_source(a, k, zero);
-        // GEMM1: R = A_p x (chain from +0); wave w = m-block w. Both operands stream through a
-        // ring of GD steps (the loads of step t + GD issue after step t's MFMAs): A rows from L2,
-        // the x columns (16 samples) from L2/HBM through a buffer descriptor whose range check
-        // returns 0 for columns past n, samples past B and a guard-zeroed x. NP / 16 is a
+        // GEMM1: R = A_p x (chain from +0); wave w = m-blocks w, w + 4, .... Both operands stream
+        // through a ring of GD steps (the loads of step t + GD issue after step t's MFMAs): A rows
+        // from L2, the x columns (16 samples) from L2/HBM through a buffer descriptor whose range
+        // check returns 0 for columns past n, samples past B and a guard-zeroed x. NP / 16 is a
         // multiple of GD.
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (16 * w < m) {
-            const float* arow = a.A + ((size_t)p * M_PAD + 16 * w + j) * NP + 4 * h;
-            const uint32_t xbytes = zero ? 0u : (uint32_t)((size_t)B * P * n * 4);
-            const __amdgpu_buffer_rsrc_t rx =
-                __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), 0, (int)xbytes, 0x00020000);
-            const uint32_t xoff = sv ? (uint32_t)((((size_t)s * P + p) * n + 4 * h) * 4) : 0x80000000u;
-            auto ldx = [&](int t) -> f32x4 {
-                return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                    rx, 16 * t + 4 * h < n && sv ? xoff + 64u * t : 0x80000000u, 0, 0));
-            };
-            constexpr int GD = 4;
-            const int T = NP / 16;
-            f32x4 ar[GD], xr[GD];
-#pragma unroll
-            for (int u = 0; u < GD; ++u) {
-                ar[u] = *(const f32x4*)(arow + 16 * u);
-                xr[u] = ldx(u);
-            }
-            for (int t0 = 0; t0 < T; t0 += GD) {
+        for (int mq = w; mq < MP / 16; mq += WAVES) {
+            f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (16 * mq < m) {
+                const float* arow = a.A + ((size_t)p * MP + 16 * mq + j) * NP + 4 * h;
+                const uint32_t xbytes = zero ? 0u : (uint32_t)((size_t)B * P * n * 4);
+                const __amdgpu_buffer_rsrc_t rx =
+                    __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), 0, (int)xbytes, 0x00020000);
+                const uint32_t xoff = sv ? (uint32_t)((((size_t)s * P + p) * n + 4 * h) * 4) : 0x80000000u;
+                auto ldx = [&](int t) -> f32x4 {
+                    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                        rx, 16 * t + 4 * h < n && sv ? xoff + 64u * t : 0x80000000u, 0, 0));
+                };
+                constexpr int GD = 4;
+                const int T = NP / 16;
+                f32x4 ar[GD], xr[GD];
 #pragma unroll
                 for (int u = 0; u < GD; ++u) {
+                    ar[u] = *(const f32x4*)(arow + 16 * u);
+                    xr[u] = ldx(u);
+                }
+                for (int t0 = 0; t0 < T; t0 += GD) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) acc = mfma4(ar[u][r], xr[u][r], acc);
-                    if (t0 + GD + u < T) {
-                        ar[u] = *(const f32x4*)(arow + 16 * (t0 + GD + u));
-                        xr[u] = ldx(t0 + GD + u);
+                    for (int u = 0; u < GD; ++u) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc = mfma4(ar[u][r], xr[u][r], acc);
+                        if (t0 + GD + u < T) {
+                            ar[u] = *(const f32x4*)(arow + 16 * (t0 + GD + u));
+                            xr[u] = ldx(t0 + GD + u);
+                        }
                     }
                 }
             }
+            *(f32x4*)(Rlds + j * RS + 16 * mq + 4 * h) = acc;
         }
-        *(f32x4*)(Rlds + j * RS + 16 * w + 4 * h) = acc;
     } else {
         // R = b_p (rows past m are zero)
-        f32x4 v;
+        for (int mq = w; mq < MP / 16; mq += WAVES) {
+            f32x4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int mi = 16 * w + 4 * h + r;
-            v[r] = (sv && mi < m) ? a.b[((size_t)s * P + p) * m + mi] : 0.0f;
+            for (int r = 0; r < 4; ++r) {
+                const int mi = 16 * mq + 4 * h + r;
+                v[r] = (sv && mi < m) ? a.b[((size_t)s * P + p) * m + mi] : 0.0f;
+            }
+            *(f32x4*)(Rlds + j * RS + 16 * mq + 4 * h) = v;
         }
-        *(f32x4*)(Rlds + j * RS + 16 * w + 4 * h) = v;
     }
     __syncthreads();
-    // GEMM2: out = A_p^T R (chain from +0); wave w takes n-tiles w, w + 4, ...; the m-blocks
-    // past m (zero rows of R and of the padded operator) are skipped, and the A^T rows of the
-    // next tile load under the current tile's MFMAs
-    f32x4 rv[M_PAD / 16];
+    // GEMM2: out = A_p^T R, one chain from +0 over the m-blocks in ascending order; wave w takes
+    // n-tiles w, w + 4, ...; the m-blocks past m (zero rows of R and of the padded operator) are
+    // skipped. Work unit u = (n-tile, m-group of 4 blocks); the A^T rows of unit u + 1 load under
+    // unit u's MFMAs. R of m-group 0 is held in registers, later groups are read from LDS.
+    const int mbk = (m + 15) / 16;                 // m-blocks holding rows
+    const int MG = (mbk + 3) / 4;                  // m-groups holding rows
+    f32x4 rv0[4];
 #pragma unroll
-    for (int t = 0; t < M_PAD / 16; ++t) rv[t] = *(const f32x4*)(Rlds + j * RS + 16 * t + 4 * h);
-    const int mbk = (m + 15) / 16;
-    const float* atb = a.At + ((size_t)p * NP + j) * M_PAD + 4 * h;
-    f32x4 at_cur[M_PAD / 16], at_nxt[M_PAD / 16];
-    auto load_at = [&](f32x4 (&dst)[M_PAD / 16], int nb) {
+    for (int t = 0; t < 4; ++t) rv0[t] = *(const f32x4*)(Rlds + j * RS + 16 * t + 4 * h);
+    const float* atb = a.At + ((size_t)p * NP + j) * MP + 4 * h;
+    f32x4 at_cur[4], at_nxt[4];
+    auto load_at = [&](f32x4 (&dst)[4], int u) {
+        const int nb = w + WAVES * (u / MG), mg = u % MG;
 #pragma unroll
-        for (int t = 0; t < M_PAD / 16; ++t)
-            if (t < mbk) dst[t] = *(const f32x4*)(atb + (size_t)16 * nb * M_PAD + 16 * t);
+        for (int t = 0; t < 4; ++t)
+            if (4 * mg + t < mbk) dst[t] = *(const f32x4*)(atb + (size_t)16 * nb * MP + 64 * mg + 16 * t);
     };
-    if (w < NP / 16) load_at(at_cur, w);
-    for (int nb = w; nb < NP / 16; nb += WAVES) {
-        if (nb + WAVES < NP / 16) load_at(at_nxt, nb + WAVES);
-        f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const int units = (NP / 16 - w + WAVES - 1) / WAVES * MG;
+    if (units > 0) load_at(at_cur, 0);
+    f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int u = 0; u < units; ++u) {
+        const int nb = w + WAVES * (u / MG), mg = u % MG;
+        if (u + 1 < units) load_at(at_nxt, u + 1);
+        if (mg == 0) {
+            gc = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int t = 0; t < M_PAD / 16; ++t) {
-            if (t < mbk) {
+            for (int t = 0; t < 4; ++t) {
+                if (t < mbk) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) gc = mfma4(at_cur[t][r], rv[t][r], gc);
+                    for (int r = 0; r < 4; ++r) gc = mfma4(at_cur[t][r], rv0[t][r], gc);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (4 * mg + t < mbk) {
+                    const f32x4 rt = *(const f32x4*)(Rlds + j * RS + 64 * mg + 16 * t + 4 * h);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) gc = mfma4(at_cur[t][r], rt[r], gc);
+                }
             }
         }
         const int n0 = 16 * nb + 4 * h;
-        if (sv && n0 < n) *(f32x4*)(out + ((size_t)s * P + p) * n + n0) = gc;
+        if (mg == MG - 1 && sv && n0 < n) {
+            f32x4* o = (f32x4*)(out + ((size_t)s * P + p) * n + n0);
+            *o = mode == 2 ? *o + gc : gc;
+        }
 #pragma unroll
-        for (int t = 0; t < M_PAD / 16; ++t) at_cur[t] = at_nxt[t];
+        for (int t = 0; t < 4; ++t) at_cur[t] = at_nxt[t];
     }
 }
 
@@ -198,6 +223,9 @@ __global__ __launch_bounds__(THREADS) void grad_kernel(GnnArgs a, int k) {
     bool yzero = false;
     const float* ys = y_source(a, k, yzero);
     const bool uzero = flag_ld(a.flags + GNN_F_UBAD(k)) != 0;
+    // the y_next guard of iteration k - 1 fired (:235-237): the reference keeps y_k = y_{k-1}
+    // and appends it, so Y[k-1] (= yptr[k], which holds the rejected y_next) is rewritten with it
+    float* const fix = (k > 0 && flag_ld(a.flags + GNN_F_YNB(k - 1)) != 0) ? a.yptr[k] : nullptr;
     float gclip, vclip;
     clips(a, k, gclip, vclip);
     bool bad = false;
@@ -209,6 +237,7 @@ __global__ __launch_bounds__(THREADS) void grad_kernel(GnnArgs a, int k) {
         const f32x4 aty = ((const f32x4*)a.AtAy)[i];
         const f32x4 atb = ((const f32x4*)a.Atb)[i];
         const f32x4 yv = yzero ? (f32x4){0, 0, 0, 0} : ((const f32x4*)ys)[i];
+        if (fix != nullptr) ((f32x4*)fix)[i] = yv;
         const f32x4 uv = uzero ? (f32x4){0, 0, 0, 0} : ((const f32x4*)a.U)[i];
         const f32x4 dv = ((const f32x4*)a.D)[i];
         f32x4 gv;
@@ -485,11 +514,11 @@ hipError_t gnn_launch_check0(const GnnArgs& a, const float* y0, hipStream_t st) 
     return hipGetLastError();
 }
 
-size_t gnn_gram_lds(int n_pad) { (void)n_pad; return 4 * (size_t)(BT * (M_PAD + 4)); }
+size_t gnn_gram_lds(int m_pad) { return 4 * (size_t)(BT * (m_pad + 4)); }
 
 hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* out, int mode,
                            hipStream_t st) {
-    const size_t lds = gnn_gram_lds(a.n_pad);
+    const size_t lds = gnn_gram_lds(a.m_pad);
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)gnn::gram_kernel,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

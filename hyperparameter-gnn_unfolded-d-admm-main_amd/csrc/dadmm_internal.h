@@ -16,7 +16,10 @@ __device__ __forceinline__ float sign_times(float y, float t) {
 }
 
 constexpr int BT = 16;       // samples per workgroup of the fused kernel (MFMA N dimension)
-constexpr int M_PAD = 64;    // padded rows per agent (4 m-blocks of 16 rows)
+constexpr int M_PAD = 64;    // rows per m-group (4 m-blocks of 16 rows); the fused kernels hold one
+constexpr int M_MAX = 1024;  // rows per agent accepted by the ABI (the stepwise path: any m-group count)
+// padded rows per agent of the prepared operator: whole m-groups of 64 rows
+__host__ __device__ constexpr int m_pad_of(int m) { return (m + M_PAD - 1) / M_PAD * M_PAD; }
 #ifndef DADMM_FUSED_WAVES
 #define DADMM_FUSED_WAVES 8
 #endif
@@ -72,6 +75,30 @@ backward_fn_ptr find_backward(int P, int nt, int graph);
 hipError_t launch_backward_reduce(const float* partial, float* dhyp, int nwg, int K, int P, int H,
                                   hipStream_t stream);
 
+// ---- adjoint for every shape (dadmm_adjoint.hip) ------------------------------------------------
+struct AdjArgs {
+    const float* A;         // prepared operator [P][m_pad][n_pad]
+    const float* At;        // [P][n_pad][m_pad]
+    const int32_t* vptr;    // visit lists (as StepArgs)
+    const uint8_t* vq;
+    const float* deg;       // [G][P]
+    const float* hyp;       // [K][hyp_rows][4]
+    const float* y0;        // [B][P][n]
+    const float* d0;        // [B][P][n]
+    const float* Y;         // [K][B][P][n] recorded trajectory
+    const float* Grec;      // [K][B][P][n]
+    const float* Urec;      // [K][B][P][n]
+    const float* gY;        // [K][B][P][n] dL/dY
+    float* yb;              // scratch [B][P][n]: dL/dy
+    float* Ub;              // scratch [B][P][n]: dL/dU
+    float* Gb;              // scratch [B][P][n]: dL/d(pre-clamp gradient) of the later iteration
+    float* partial;         // scratch [adjoint_workgroups(B, n)][K][P][4]
+    int B, P, m, m_pad, n, n_pad, K, hyp_rows, variant, graph_shared;
+};
+size_t adjoint_lds_bytes(int P);
+int adjoint_workgroups(int B, int n);
+hipError_t launch_adjoint(const AdjArgs& a, float* dhyp, hipStream_t st);
+
 // ---- GNN-model per-iteration path (dadmm_gnn.hip) -----------------------------------------------
 // flag words (int32, zeroed by dadmm_gnn_begin): y0 guard, then U_k non-finite (k = 0..K),
 // gradient NaN and y_next non-finite (k = 0..K-1)
@@ -82,8 +109,8 @@ hipError_t launch_backward_reduce(const float* partial, float* dhyp, int nwg, in
 #define GNN_FLAG_WORDS(K) (3 * (K) + 4)
 
 struct GnnArgs {
-    const float* A;         // prepared operator [P][M_PAD][n_pad]
-    const float* At;        // [P][n_pad][M_PAD]
+    const float* A;         // prepared operator [P][m_pad][n_pad]
+    const float* At;        // [P][n_pad][m_pad]
     const float* b;         // [B][P][m]
     const int32_t* vptr;    // visit lists (as StepArgs)
     const uint8_t* vq;
@@ -100,7 +127,7 @@ struct GnnArgs {
     float* G;               // scratch [B][P][n]: clamped gradient of the iteration
     int32_t* flags;         // [GNN_FLAG_WORDS(K)]
     int32_t* status;        // nullable
-    int B, P, m, n, n_pad, K, hyp_rows, variant, graph_shared;
+    int B, P, m, m_pad, n, n_pad, K, hyp_rows, variant, graph_shared;
 };
 struct GnnGrads {
     const float* gy1;       // dL/dy_{k+1} (nullable = 0)
@@ -118,12 +145,12 @@ hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* o
 hipError_t gnn_launch_step(const GnnArgs& a, int k, hipStream_t st);
 hipError_t gnn_launch_finish(const GnnArgs& a, hipStream_t st);
 hipError_t gnn_launch_step_backward(const GnnArgs& a, int k, const GnnGrads& gg, hipStream_t st);
-size_t gnn_gram_lds(int n_pad);
+size_t gnn_gram_lds(int m_pad);
 
 // ---- one launch per iteration, state in HBM (dadmm_tiled.hip) ---------------------------------
 struct TiledArgs {
-    const float* A;         // prepared operator [P][M_PAD][n_pad]
-    const float* At;        // [P][n_pad][M_PAD]
+    const float* A;         // prepared operator [P][m_pad][n_pad]
+    const float* At;        // [P][n_pad][m_pad]
     const float* b;         // [B][P][m]
     const int32_t* vptr;    // visit lists (as StepArgs)
     const uint8_t* vq;
@@ -137,9 +164,9 @@ struct TiledArgs {
     float* delta;           // delta_k [B][P][n] (scratch, consensus_kernel)
     float* U_out;           // [B][P][n] or nullptr
     int32_t* status;        // or nullptr (OR-ed DADMM_STATUS_* bits)
-    int B, P, m, n, n_pad, K, hyp_rows, variant, graph_shared;
+    int B, P, m, m_pad, n, n_pad, K, hyp_rows, variant, graph_shared;
 };
-size_t tiled_lds_bytes(int n_pad);
+size_t tiled_lds_bytes(int n_pad, int m_pad);
 hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream);
 
 // ---- fused loss (dadmm_loss.hip) ----------------------------------------------------------------
@@ -220,18 +247,19 @@ hipError_t launch_prepare(const float* A, float* Apad, float* Atpad, int P, int 
 
 // ---- stepwise path (dadmm_stepwise.hip) --------------------------------------------------------
 // flag words (int32, zeroed before every forward): barrier counter, barrier timeout, y0 guard,
-// then per iteration k: U_k non-finite, gradient NaN, y_next non-finite (U_K is index K).
+// exit counter, then per iteration k: U_k non-finite, gradient NaN, y_next non-finite (U_K is index K).
 #define SW_F_BARRIER 0
 #define SW_F_TIMEOUT 1
 #define SW_F_Y0 2
+#define SW_F_EXIT 3    // persistent form: workgroups past their last write (the last one finishes)
 #define SW_F_UBAD(k) (4 + 4 * (k))
 #define SW_F_GBAD(k) (5 + 4 * (k))
 #define SW_F_YNB(k) (6 + 4 * (k))
 #define SW_FLAG_WORDS(K) (4 + 4 * ((K) + 1))
 
 struct StepArgs {
-    const float* A;         // prepared operator [P][M_PAD][n_pad]
-    const float* At;        // [P][n_pad][M_PAD]
+    const float* A;         // prepared operator [P][m_pad][n_pad]
+    const float* At;        // [P][n_pad][m_pad]
     const float* b;         // [B][P][m]
     const int32_t* vptr;    // visit lists: [G*P + 1] offsets into vq (G = 1 shared, B otherwise)
     const uint8_t* vq;      // neighbour ids in the reference's accumulation order
@@ -248,7 +276,7 @@ struct StepArgs {
     int32_t* status;        // [1]
     float* Grec;            // nullable [K][B][P][n]: pre-clamp gradient of iteration k
     float* Urec;            // nullable [K][B][P][n]: U_k entering iteration k
-    int B, P, m, n, n_pad, K, hyp_rows, variant, graph_shared;
+    int B, P, m, m_pad, n, n_pad, K, hyp_rows, variant, graph_shared;
 };
 
 size_t stepwise_flag_bytes(int K);

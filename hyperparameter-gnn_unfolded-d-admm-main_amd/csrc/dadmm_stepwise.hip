@@ -1,5 +1,5 @@
 // dadmm_stepwise.hip — iteration-at-a-time unfolded D-ADMM forward with the reference's
-// batch-global NaN/Inf guards, for every shape (P <= 64, m <= 64, n % 4 == 0).
+// batch-global NaN/Inf guards, for every shape (P <= 64, any m up to M_MAX, n % 4 == 0).
 //
 // Reference semantics: unfolded_DLASSO.py:53-107 (DLASSO_unfolded.forward), :127-140
 // (compute_delta); the GNN variant's fixed clamps gnn_dlasso_models_progressive.py:205-232.
@@ -102,9 +102,9 @@ __device__ void phase_check0(const StepArgs& a, int wid, int nw) {
 
 // ---- phase G: gradient of (16-sample tile, agent p) -------------------------------------------
 __device__ void phase_grad(const StepArgs& a, int k, int item, float* lds) {
-    const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad;
+    const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad, MP = a.m_pad;
     const int tile = item / P, p = item % P;
-    const int YS = NP + 4, RS = M_PAD + 4;
+    const int YS = NP + 4, RS = MP + 4;
     float* Ylds = lds;                   // [16][YS]
     float* Rlds = lds + 16 * YS;         // [16][RS]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -135,16 +135,17 @@ __device__ void phase_grad(const StepArgs& a, int k, int item, float* lds) {
     }
     __syncthreads();
 
-    // GEMM1: wave w computes m-block w: R = A_p y - b_p, one fma chain per row from -b
-    {
+    // GEMM1: wave w computes m-blocks w, w + 4, ...: R = A_p y - b_p, one fma chain per row from
+    // -b (rows past m stay 0: the padded A^T rows they meet in GEMM2 are 0 too)
+    for (int mq = w; mq < MP / 16; mq += SW_WAVES) {
         f32x4 acc;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int mi = 16 * w + 4 * h + r;
+            const int mi = 16 * mq + 4 * h + r;
             acc[r] = (sv && mi < m) ? -a.b[((size_t)s * P + p) * m + mi] : 0.0f;
         }
-        if (16 * w < m) {
-            const float* arow = a.A + ((size_t)p * M_PAD + 16 * w + j) * NP + 4 * h;
+        if (16 * mq < m) {
+            const float* arow = a.A + ((size_t)p * MP + 16 * mq + j) * NP + 4 * h;
             const float* brow = Ylds + j * YS + 4 * h;
             for (int t = 0; t < NP / 16; ++t) {
                 const f32x4 av = *(const f32x4*)(arow + 16 * t);
@@ -153,7 +154,7 @@ __device__ void phase_grad(const StepArgs& a, int k, int item, float* lds) {
                 for (int r = 0; r < 4; ++r) acc = mfma4(av[r], bv[r], acc);
             }
         }
-        *(f32x4*)(Rlds + j * RS + 16 * w + 4 * h) = acc;
+        *(f32x4*)(Rlds + j * RS + 16 * mq + 4 * h) = acc;
     }
     __syncthreads();
 
@@ -162,18 +163,16 @@ __device__ void phase_grad(const StepArgs& a, int k, int item, float* lds) {
     hyp_row(a, k, p, al, ta, rh, et);
     clips(a, k, gclip, vclip);
     const float dg = sv ? a.deg[(a.graph_shared ? 0 : (size_t)s * P) + p] : 0.0f;
-    f32x4 rv[M_PAD / 16];
-#pragma unroll
-    for (int t = 0; t < M_PAD / 16; ++t) rv[t] = *(const f32x4*)(Rlds + j * RS + 16 * t + 4 * h);
     bool bad = false;
     for (int nb = w; nb < NP / 16; nb += SW_WAVES) {
-        const float* atrow = a.At + ((size_t)p * NP + 16 * nb + j) * M_PAD + 4 * h;
+        // one fma chain over every m-block in ascending order (m-blocks past m add exact zeros)
+        const float* atrow = a.At + ((size_t)p * NP + 16 * nb + j) * MP + 4 * h;
         f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int t = 0; t < M_PAD / 16; ++t) {
+        for (int t = 0; t < MP / 16; ++t) {
             const f32x4 av = *(const f32x4*)(atrow + 16 * t);
+            const f32x4 rv = *(const f32x4*)(Rlds + j * RS + 16 * t + 4 * h);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) gc = mfma4(av[r], rv[t][r], gc);
+            for (int r = 0; r < 4; ++r) gc = mfma4(av[r], rv[r], gc);
         }
         const int n0 = 16 * nb + 4 * h;
         if (sv && n0 < n) {
@@ -336,6 +335,9 @@ __device__ bool grid_barrier(const StepArgs& a, uint32_t target) {
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // a workgroup that gave up earlier has already poisoned (or is poisoning) Y: a late
+        // arrival that saw the counter reach the target must not go on writing over it
+        if (flag_ld(a.flags + SW_F_TIMEOUT)) to = 1;
         timed_out = to;
     }
     __syncthreads();
@@ -365,10 +367,26 @@ __global__ __launch_bounds__(SW_THREADS) void sw_persistent_kernel(StepArgs a) {
         }
     }
 out:
-    phase_final(a, blockIdx.x, G);
+    // The final pass (the Y[K-1] fix-up, or the NaN poison after a timeout) runs in the LAST
+    // workgroup to leave: every other workgroup is then past its last write to Y, so no late
+    // phase_update of a workgroup that missed the timeout can land over the poison.
+    {
+        __shared__ int last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            const uint32_t prev = __hip_atomic_fetch_add((uint32_t*)(a.flags + SW_F_EXIT), 1u,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            last = prev == (uint32_t)(G - 1);
+        }
+        __syncthreads();
+        if (last) phase_final(a, 0, 1);
+    }
 }
 
-size_t grad_lds_bytes(int n_pad) { return 4 * (size_t)(BT * (n_pad + 4) + BT * (M_PAD + 4)); }
+size_t grad_lds_bytes(int n_pad, int m_pad) { return 4 * (size_t)(BT * (n_pad + 4) + BT * (m_pad + 4)); }
 size_t update_lds_bytes(int P) { return 4 * (size_t)SW_WAVES * P * 64; }
 
 }  // namespace
@@ -379,7 +397,7 @@ hipError_t launch_stepwise(const StepArgs& a, int gate, bool flags_zeroed, hipSt
     hipError_t e = hipSuccess;
     if (!flags_zeroed && (e = hipMemsetAsync(a.flags, 0, stepwise_flag_bytes(a.K), stream)) != hipSuccess)
         return e;
-    const size_t lds_g = grad_lds_bytes(a.n_pad), lds_u = update_lds_bytes(a.P);
+    const size_t lds_g = grad_lds_bytes(a.n_pad, a.m_pad), lds_u = update_lds_bytes(a.P);
     const size_t lds = lds_g > lds_u ? lds_g : lds_u;
     if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
     const void* fns[3] = {(const void*)sw_persistent_kernel, (const void*)sw_grad_kernel,

@@ -61,11 +61,15 @@ __device__ __forceinline__ void clips(int variant, int k, float& gclip, float& v
 constexpr int HALVES = 2;            // 16-sample MFMA column blocks per workgroup (32 samples):
                                      // every A / A^T operand load feeds two fma chains
 constexpr int ST = HALVES * BT;      // samples per workgroup
-constexpr int CH = 2;                // n-tiles per chunk of the update phase
-constexpr int RG = CH * HALVES;      // row groups per chunk
+// MB = m-groups of 64 rows per agent (m_pad = 64 MB; MB in {1, 2}). The update phase works in
+// chunks of CH = 2 / MB n-tiles, so that a chunk's A^T rows (CH x 4 MB vectors) take the same
+// registers for both; with MB = 2 the GEMM2 B operand (R) is read from LDS, not held.
+template <int MB>
 struct Chunk {                       // one chunk's operands
+    static constexpr int CH = 2 / MB;            // n-tiles per chunk of the update phase
+    static constexpr int RG = CH * HALVES;       // row groups per chunk
     f32x4 yp[RG], up[RG], dv[RG];
-    f32x4 atv[CH][M_PAD / 16];
+    f32x4 atv[CH][4 * MB];
 };
 
 // blockIdx -> (tile, agent) so that the P workgroups of one sample tile run on the same XCD
@@ -91,13 +95,15 @@ constexpr int STAGE_NP_MAX = 512;
 // Workgroup = (32-sample tile, agent p).
 // amdgpu_waves_per_eu(2): keeps VGPRs + AGPRs <= 256 (two workgroups per CU); without it the
 // allocator lands at 249 + 8 and the kernel runs at one wave per SIMD (0.40 -> 0.53 ms/iteration)
-template <bool STAGE>
+template <bool STAGE, int MB>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) void iter_kernel(TiledArgs a, int k) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int MP = 64 * MB;                      // padded rows per agent (a.m_pad)
+    constexpr int CH = Chunk<MB>::CH, RG = Chunk<MB>::RG;
     const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad;
     const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
     const int tile = wg / P, p = wg % P;
-    const int RS = M_PAD + 4;
+    const int RS = MP + 4;
     float* Ylds = lds;                               // [ST][NP] swizzled y_k tile (STAGE)
     float* Rlds = lds + (STAGE ? ST * NP : 0);       // [ST][RS]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -114,7 +120,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     const float* usrc = k == 0 ? a.U0 : Uprev;
     const float* dsrc = k == 0 ? a.d0 : a.delta;  // delta_k
     const int ntw = (NP / 16 - w + WAVES - 1) / WAVES;   // n-tiles of this wave: w, w + 4, ...
-    const float* atbase = a.At + ((size_t)p * NP + j) * M_PAD + 4 * h;
+    const float* atbase = a.At + ((size_t)p * NP + j) * MP + 4 * h;
     const bool ylds = STAGE && !final_only;       // own rows from the staged tile
     size_t srow[HALVES];
 #pragma unroll
@@ -122,7 +128,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
         const int s = tile * ST + hh * BT + j;
         srow[hh] = (size_t)(s < B ? s : 0) * P;
     }
-    auto load_chunk = [&](int c0, Chunk& c) {
+    auto load_chunk = [&](int c0, Chunk<MB>& c) {
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
             const int nb = w + WAVES * (c0 + i);
@@ -130,8 +136,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
             const bool tile_ok = c0 + i < ntw;
             if (!final_only && tile_ok) {
 #pragma unroll
-                for (int t = 0; t < M_PAD / 16; ++t)
-                    c.atv[i][t] = *(const f32x4*)(atbase + (size_t)16 * nb * M_PAD + 16 * t);
+                for (int t = 0; t < MP / 16; ++t)
+                    c.atv[i][t] = *(const f32x4*)(atbase + (size_t)16 * nb * MP + 16 * t);
             }
 #pragma unroll
             for (int hh = 0; hh < HALVES; ++hh) {
@@ -147,7 +153,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
             }
         }
     };
-    Chunk cA;
+    Chunk<MB> cA;
     if (ntw > 0) load_chunk(0, cA);
 
     if constexpr (STAGE) {
@@ -180,85 +186,89 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
             }
             status |= bad ? 1u : 0u;
         }
-        // GEMM1: R = A_p y - b_p, one fma chain per row from -b (wave w = m-block w), one chain
-        // per 16-sample half sharing every A load
-        f32x4 acc[HALVES];
-#pragma unroll
-        for (int hh = 0; hh < HALVES; ++hh) {
-            const int s = tile * ST + hh * BT + j;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int mi = 16 * w + 4 * h + r;
-                acc[hh][r] = (s < B && mi < m) ? -a.b[((size_t)s * P + p) * m + mi] : 0.0f;
-            }
-        }
+        // GEMM1: R = A_p y - b_p, one fma chain per row from -b (wave w = m-blocks w, w + 4, ...
+        // of the MB m-groups), one chain per 16-sample half sharing every A load
         if constexpr (STAGE) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA has landed
             __syncthreads();                                     // ... and every other wave's
         }
-        if (16 * w < m) {
-            // the B operand (y_k, 16 columns per half) from the staged LDS tile (STAGE), else
-            // straight from L2/HBM through a buffer
-            // descriptor: columns past n and samples past B get an offset past the range, which
-            // the hardware returns as 0 (the padded operator columns are 0 too) - no branches
-            const float* arow = a.A + ((size_t)p * M_PAD + 16 * w + j) * NP + 4 * h;
-            const rsrc_t ry = make_rsrc(yk, (uint32_t)(S * 4));
-            uint32_t yoff[HALVES];
+#pragma unroll
+        for (int mg = 0; mg < MB; ++mg) {
+            const int mq = w + WAVES * mg;                   // this pass's m-block
+            f32x4 acc[HALVES];
 #pragma unroll
             for (int hh = 0; hh < HALVES; ++hh) {
                 const int s = tile * ST + hh * BT + j;
-                yoff[hh] = s < B ? (uint32_t)((((size_t)s * P + p) * n + 4 * h) * 4) : 0x80000000u;
-            }
-            auto ldb = [&](int hh, int t) -> f32x4 {
-                if constexpr (STAGE)
-                    return *(const f32x4*)(Ylds + (hh * BT + j) * NP + 4 * ((4 * t + h) ^ j));
-                else
-                    return bload4(ry, 16 * t + 4 * h < n ? yoff[hh] + 64u * t : 0x80000000u);
-            };
-            // operand ring of depth D: the loads of step t + D are issued right after step t's
-            // MFMAs (pinned there by a scheduling barrier); T = NP / 16 is a multiple of D. The
-            // steady loop is straight-line, two groups per trip (the compiler's waits at a loop
-            // head drain the queue), so the waits count the D - 1 younger steps in flight.
-            constexpr int D = 4;
-            const int T = NP / 16;
-            f32x4 ar[D], br[D][HALVES];
-            auto load = [&](int u, int t) {
-                ar[u] = *(const f32x4*)(arow + 16 * t);
 #pragma unroll
-                for (int hh = 0; hh < HALVES; ++hh) br[u][hh] = ldb(hh, t);
-            };
-            auto step = [&](int u) {
-#pragma unroll
-                for (int hh = 0; hh < HALVES; ++hh)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[hh] = mfma4(ar[u][r], br[u][hh][r], acc[hh]);
-            };
-#pragma unroll
-            for (int u = 0; u < D; ++u) load(u, u);
-            int t0 = 0;
-            for (; t0 + 3 * D <= T; t0 += 2 * D) {
-#pragma unroll
-                for (int u = 0; u < 2 * D; ++u) {
-                    step(u % D);
-                    load(u % D, t0 + u + D);
-                    __builtin_amdgcn_sched_barrier(0);
+                for (int r = 0; r < 4; ++r) {
+                    const int mi = 16 * mq + 4 * h + r;
+                    acc[hh][r] = (s < B && mi < m) ? -a.b[((size_t)s * P + p) * m + mi] : 0.0f;
                 }
             }
-            if (t0 + 2 * D <= T) {
+            if (16 * mq < m) {
+                // the B operand (y_k, 16 columns per half) from the staged LDS tile (STAGE), else
+                // straight from L2/HBM through a buffer
+                // descriptor: columns past n and samples past B get an offset past the range, which
+                // the hardware returns as 0 (the padded operator columns are 0 too) - no branches
+                const float* arow = a.A + ((size_t)p * MP + 16 * mq + j) * NP + 4 * h;
+                const rsrc_t ry = make_rsrc(yk, (uint32_t)(S * 4));
+                uint32_t yoff[HALVES];
 #pragma unroll
-                for (int u = 0; u < D; ++u) {
-                    step(u);
-                    load(u, t0 + u + D);
-                    __builtin_amdgcn_sched_barrier(0);
+                for (int hh = 0; hh < HALVES; ++hh) {
+                    const int s = tile * ST + hh * BT + j;
+                    yoff[hh] = s < B ? (uint32_t)((((size_t)s * P + p) * n + 4 * h) * 4) : 0x80000000u;
                 }
-                t0 += D;
+                auto ldb = [&](int hh, int t) -> f32x4 {
+                    if constexpr (STAGE)
+                        return *(const f32x4*)(Ylds + (hh * BT + j) * NP + 4 * ((4 * t + h) ^ j));
+                    else
+                        return bload4(ry, 16 * t + 4 * h < n ? yoff[hh] + 64u * t : 0x80000000u);
+                };
+                // operand ring of depth D: the loads of step t + D are issued right after step t's
+                // MFMAs (pinned there by a scheduling barrier); T = NP / 16 is a multiple of D. The
+                // steady loop is straight-line, two groups per trip (the compiler's waits at a loop
+                // head drain the queue), so the waits count the D - 1 younger steps in flight.
+                constexpr int D = 4;
+                const int T = NP / 16;
+                f32x4 ar[D], br[D][HALVES];
+                auto load = [&](int u, int t) {
+                    ar[u] = *(const f32x4*)(arow + 16 * t);
+#pragma unroll
+                    for (int hh = 0; hh < HALVES; ++hh) br[u][hh] = ldb(hh, t);
+                };
+                auto step = [&](int u) {
+#pragma unroll
+                    for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc[hh] = mfma4(ar[u][r], br[u][hh][r], acc[hh]);
+                };
+#pragma unroll
+                for (int u = 0; u < D; ++u) load(u, u);
+                int t0 = 0;
+                for (; t0 + 3 * D <= T; t0 += 2 * D) {
+#pragma unroll
+                    for (int u = 0; u < 2 * D; ++u) {
+                        step(u % D);
+                        load(u % D, t0 + u + D);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+                if (t0 + 2 * D <= T) {
+#pragma unroll
+                    for (int u = 0; u < D; ++u) {
+                        step(u);
+                        load(u, t0 + u + D);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    t0 += D;
+                }
+#pragma unroll
+                for (int u = 0; u < D; ++u) step(u);   // the last D steps (T % D == 0)
             }
 #pragma unroll
-            for (int u = 0; u < D; ++u) step(u);   // the last D steps (T % D == 0)
+            for (int hh = 0; hh < HALVES; ++hh)
+                *(f32x4*)(Rlds + (hh * BT + j) * RS + 16 * mq + 4 * h) = acc[hh];
         }
-#pragma unroll
-        for (int hh = 0; hh < HALVES; ++hh)
-            *(f32x4*)(Rlds + (hh * BT + j) * RS + 16 * w + 4 * h) = acc[hh];
     }
     __syncthreads();
 
@@ -278,20 +288,20 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
 
     // per-lane data of the two samples this lane serves
     float dg[HALVES];
-    f32x4 rv[HALVES][M_PAD / 16];
+    f32x4 rv[HALVES][MB == 1 ? 4 : 1];   // MB = 1: GEMM2's B operand held; MB = 2: read from LDS
 #pragma unroll
     for (int hh = 0; hh < HALVES; ++hh) {
         const int s = tile * ST + hh * BT + j;
         const int g0 = a.graph_shared ? 0 : s * P;
         dg[hh] = s < B ? a.deg[g0 + p] : 0.0f;
-        if (!final_only) {
+        if (MB == 1 && !final_only) {
 #pragma unroll
-            for (int t = 0; t < M_PAD / 16; ++t)
+            for (int t = 0; t < 4; ++t)
                 rv[hh][t] = *(const f32x4*)(Rlds + (hh * BT + j) * RS + 16 * t + 4 * h);
         }
     }
     bool bad_u0 = false, bad_g = false, bad_y = false;
-    auto compute_chunk = [&](int c0, Chunk& c) {
+    auto compute_chunk = [&](int c0, Chunk<MB>& c) {
         int n0[CH];
         bool okr[RG];
         size_t off[RG];
@@ -335,9 +345,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
             if (c0 + i >= ntw) continue;
             f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-            for (int t = 0; t < M_PAD / 16; ++t)
+            for (int t = 0; t < MP / 16; ++t) {
+                const f32x4 rt = MB == 1 ? rv[hh][t & 3]
+                                         : *(const f32x4*)(Rlds + (hh * BT + j) * RS + 16 * t + 4 * h);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) gc = mfma4(c.atv[i][t][r], rv[hh][t][r], gc);
+                for (int r = 0; r < 4; ++r) gc = mfma4(c.atv[i][t][r], rt[r], gc);
+            }
             if (okr[g]) {
                 f32x4 yn;
 #pragma unroll
@@ -412,16 +425,19 @@ __global__ __launch_bounds__(THREADS) void consensus_kernel(TiledArgs a, const f
 
 }  // namespace tiled
 
-size_t tiled_lds_bytes(int n_pad) {
+size_t tiled_lds_bytes(int n_pad, int m_pad) {
     const size_t stage = n_pad <= tiled::STAGE_NP_MAX ? 4 * (size_t)tiled::ST * n_pad : 0;
-    return stage + 4 * (size_t)(tiled::ST * (M_PAD + 4));
+    return stage + 4 * (size_t)(tiled::ST * (m_pad + 4));
 }
 
 hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream) {
-    const size_t lds = tiled_lds_bytes(a.n_pad);
+    const size_t lds = tiled_lds_bytes(a.n_pad, a.m_pad);
     if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
     if (a.n_pad % 64 != 0) return hipErrorInvalidValue;   // the swizzle and GEMM ring assume it
-    auto kern = a.n_pad <= tiled::STAGE_NP_MAX ? tiled::iter_kernel<true> : tiled::iter_kernel<false>;
+    if (a.m_pad != 64 && a.m_pad != 128) return hipErrorInvalidValue;   // MB in {1, 2}
+    const bool stage = a.n_pad <= tiled::STAGE_NP_MAX;
+    auto kern = a.m_pad == 64 ? (stage ? tiled::iter_kernel<true, 1> : tiled::iter_kernel<false, 1>)
+                              : (stage ? tiled::iter_kernel<true, 2> : tiled::iter_kernel<false, 2>);
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kern,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -32,6 +32,8 @@ EXPORTED_SYMBOLS = (
     "dadmm_forward_stepwise",
     "dadmm_backward_scratch_bytes",
     "dadmm_backward",
+    "dadmm_adjoint_scratch_bytes",
+    "dadmm_adjoint",
     "dadmm_hyper_gcn",
     "dadmm_hyper_linear",
     "dadmm_hyper_rownorm",
@@ -106,6 +108,10 @@ def load() -> ctypes.CDLL:
     L.dadmm_backward_scratch_bytes.argtypes = [ctypes.POINTER(Dims)]
     L.dadmm_backward.restype = ctypes.c_int
     L.dadmm_backward.argtypes = [ctypes.POINTER(Dims)] + [vp] * 14
+    L.dadmm_adjoint_scratch_bytes.restype = ctypes.c_size_t
+    L.dadmm_adjoint_scratch_bytes.argtypes = [ctypes.POINTER(Dims)]
+    L.dadmm_adjoint.restype = ctypes.c_int
+    L.dadmm_adjoint.argtypes = [ctypes.POINTER(Dims)] + [vp] * 14
     D = ctypes.POINTER(Dims)
     u64, i64, f32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_float
     L.dadmm_normal_offset_step.restype = u64

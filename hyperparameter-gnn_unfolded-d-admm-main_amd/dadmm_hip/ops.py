@@ -199,7 +199,7 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
                 ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.vptr), _ptr(graphs.vq),
                 _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U),
                 _ptr(Grec), _ptr(Urec), _ptr(status), gate, _ptr(scratch), stream))
-    traj = Trajectory(Y, Grec, Urec, y0, d0, hyp, variant) if record else None
+    traj = Trajectory(Y, Grec, Urec, y0, d0, hyp, variant, fused) if record else None
     if ns != op.n:
         Y = Y[..., : op.n]
         U = U[..., : op.n] if U is not None else None
@@ -210,20 +210,28 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
 
 class Trajectory:
     """What the adjoint consumes: the n-padded iterates Y, pre-clamp gradients Grec and dual
-    states Urec ([K,B,P,n_store] each), the inits y0 / d0 and the hyper-parameter table."""
+    states Urec ([K,B,P,n_store] each), the inits y0 / d0 and the hyper-parameter table;
+    ``fused``: recorded by the fused kernel (its on-chip adjoint applies), else by the stepwise
+    path (the general adjoint)."""
 
-    __slots__ = ("Y", "Grec", "Urec", "y0", "d0", "hyp", "variant")
+    __slots__ = ("Y", "Grec", "Urec", "y0", "d0", "hyp", "variant", "fused")
 
-    def __init__(self, Y, Grec, Urec, y0, d0, hyp, variant):
+    def __init__(self, Y, Grec, Urec, y0, d0, hyp, variant, fused=False):
         self.Y, self.Grec, self.Urec = Y, Grec, Urec
-        self.y0, self.d0, self.hyp, self.variant = y0, d0, hyp, variant
+        self.y0, self.d0, self.hyp, self.variant, self.fused = y0, d0, hyp, variant, fused
 
 
 def backward_raw(op: PreparedOperator, graphs: GraphBatch, traj: Trajectory,
-                 gY: torch.Tensor) -> torch.Tensor:
-    """dL/dhyp [K,H,4] for L = sum_k <gY[k], Y[k]> along ``traj`` (dadmm_backward), enqueued on
-    the current stream. gY: [K,B,P,n] (n or n_store columns)."""
+                 gY: torch.Tensor, path: str = "auto") -> torch.Tensor:
+    """dL/dhyp [K,H,4] for L = sum_k <gY[k], Y[k]> along ``traj``, enqueued on the current
+    stream. gY: [K,B,P,n] (n or n_store columns).
+
+    path "auto": the fused adjoint (dadmm_backward: one launch, state on chip) for a fused
+    trajectory, otherwise the general adjoint (dadmm_adjoint: any P <= 64, any m, n); "fused" /
+    "general" force one."""
     _dev_check(gY)
+    if path not in ("auto", "fused", "general"):
+        raise ValueError(f"unknown path {path!r}")
     K, B, P, ns = traj.Y.shape
     H = int(traj.hyp.shape[1])
     gY = _pad_n(gY.float(), ns).contiguous()
@@ -232,22 +240,28 @@ def backward_raw(op: PreparedOperator, graphs: GraphBatch, traj: Trajectory,
     d = op.dims(B=B, K=K, variant=traj.variant, hyp_rows=H, graph_shared=graphs.shared)
     L = _lib.load()
     dhyp = torch.empty((K, H, 4), dtype=torch.float32, device=gY.device)
-    nbytes = L.dadmm_backward_scratch_bytes(ctypes.byref(d))
-    scratch = torch.empty(max(nbytes, 16) // 4 + 4, dtype=torch.float32, device=gY.device)
-    order = graphs.order
-    if not graphs.fused_ok:
-        raise NotImplementedError(
-            "the adjoint kernel follows non-ascending adjacency orders only for P <= 8")
+    use_fused = path == "fused" or (path == "auto" and traj.fused and graphs.fused_ok)
     with torch.cuda.device(gY.device):
-        rc = L.dadmm_backward(ctypes.byref(d), _ptr(op.workspace), _ptr(graphs.nbr), _ptr(order),
-                              _ptr(graphs.deg), _ptr(traj.hyp), _ptr(traj.y0), _ptr(traj.d0),
-                              _ptr(traj.Y), _ptr(traj.Grec), _ptr(traj.Urec), _ptr(gY),
-                              _ptr(dhyp), _ptr(scratch), _stream(gY.device))
-        if rc == _lib.DADMM_EUNSUPPORTED:
-            raise NotImplementedError(
-                "the adjoint kernel covers the fused kernel's shapes (P <= 6, n <= 256, m <= 64); "
-                + _lib.load().dadmm_last_error().decode(errors="replace"))
-        _lib.check("dadmm_backward", rc)
+        stream = _stream(gY.device)
+        if use_fused:
+            if not graphs.fused_ok:
+                raise ValueError("the fused adjoint follows non-ascending adjacency orders only "
+                                 "for P <= 8; use path='auto' or 'general'")
+            nbytes = L.dadmm_backward_scratch_bytes(ctypes.byref(d))
+            scratch = torch.empty(max(nbytes, 16) // 4 + 4, dtype=torch.float32, device=gY.device)
+            rc = L.dadmm_backward(ctypes.byref(d), _ptr(op.workspace), _ptr(graphs.nbr),
+                                  _ptr(graphs.order), _ptr(graphs.deg), _ptr(traj.hyp),
+                                  _ptr(traj.y0), _ptr(traj.d0), _ptr(traj.Y), _ptr(traj.Grec),
+                                  _ptr(traj.Urec), _ptr(gY), _ptr(dhyp), _ptr(scratch), stream)
+            if rc != _lib.DADMM_EUNSUPPORTED or path == "fused":
+                _lib.check("dadmm_backward", rc)
+                return dhyp
+        nbytes = L.dadmm_adjoint_scratch_bytes(ctypes.byref(d))
+        scratch = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=gY.device)
+        _lib.check("dadmm_adjoint", L.dadmm_adjoint(
+            ctypes.byref(d), _ptr(op.workspace), _ptr(graphs.vptr), _ptr(graphs.vq),
+            _ptr(graphs.deg), _ptr(traj.hyp), _ptr(traj.y0), _ptr(traj.d0), _ptr(traj.Y),
+            _ptr(traj.Grec), _ptr(traj.Urec), _ptr(gY), _ptr(dhyp), _ptr(scratch), stream))
     return dhyp
 
 

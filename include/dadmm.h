@@ -39,8 +39,9 @@
  *
  * Compiled configurations of dadmm_forward (fused): P <= 6 (P <= 5 at n > 128), m <= 64,
  * n <= 256, n % 4 == 0 (callers zero-pad n otherwise: zero columns of A are inert),
- * B*P*n*4 < 2^31. Anything else returns DADMM_EUNSUPPORTED; dadmm_forward_stepwise covers every
- * P <= 64, m <= 64, n % 4 == 0.
+ * B*P*n*4 < 2^31. Anything else returns DADMM_EUNSUPPORTED; dadmm_forward_tiled covers
+ * P <= 64, m <= 128, and dadmm_forward_stepwise every P <= 64, m <= 1024, n % 4 == 0
+ * (the reference's defaults m = 100, n = 500, configurations.py:6-9, run on the tiled path).
  */
 #ifndef DADMM_H_
 #define DADMM_H_
@@ -52,7 +53,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 8
+#define DADMM_ABI_VERSION 9
 
 enum {
     DADMM_OK = 0,
@@ -104,8 +105,8 @@ size_t dadmm_operator_bytes(const dadmm_dims* d);
 /* Prepare the per-agent operator once per A.
  * Replaces: DLASSO_unfolded.__init__'s `self.AtA = self.compute_Atx(self.A)`
  *           (unfolded_DLASSO.py:16, :120-124). The Gram matrix is never formed: the kernels use
- *           the factored gradient A_p^T (A_p y - b_p); this call lays A out padded (rows to 64,
- *           columns to a multiple of 64) together with its transpose in `op`
+ *           the factored gradient A_p^T (A_p y - b_p); this call lays A out padded (rows to a
+ *           multiple of 64, columns to a multiple of 64) together with its transpose in `op`
  *           (dadmm_operator_bytes(d) bytes, 16-byte aligned). */
 int dadmm_prepare_operator(const dadmm_dims* d, const float* A, void* op, void* stream);
 
@@ -168,7 +169,7 @@ size_t dadmm_tiled_scratch_bytes(const dadmm_dims* d);
  * Replaces: the same loop as dadmm_forward (unfolded_DLASSO.py:45, 53-109).
  * Like dadmm_forward it only FLAGS the reference's guards in `status` (OR-ed; caller zeroes it):
  * enqueue dadmm_forward_stepwise with DADMM_GATE_ON behind it for the exact guarded result.
- * Graph: visit_ptr / visit_q / deg as dadmm_forward_stepwise. P <= 64, m <= 64, n % 4 == 0. */
+ * Graph: visit_ptr / visit_q / deg as dadmm_forward_stepwise. P <= 64, m <= 128, n % 4 == 0. */
 int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
                         const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
                         const float* hyp, const float* y0, const float* U0, const float* d0,
@@ -213,6 +214,23 @@ int dadmm_backward(const dadmm_dims* d, const void* op, const uint64_t* nbr,
                    const float* d0, const float* Y, const float* Grec, const float* Urec,
                    const float* gY, float* dhyp, void* scratch, void* stream);
 
+/* Bytes of device scratch dadmm_adjoint needs for `d` (256-byte aligned pointer). */
+size_t dadmm_adjoint_scratch_bytes(const dadmm_dims* d);
+
+/* The same adjoint as dadmm_backward for EVERY shape (P <= 64, m <= 1024, n % 4 == 0): the state
+ * (dL/dy, dL/dU, the later iteration's gradient adjoint) lives in `scratch`, two launches per
+ * reverse iteration (elementwise + consensus adjoint per (sample, 64 columns); the forward's
+ * factored Gram pair for A^T A gr_bar). Takes the stepwise path's visit lists (the reference's
+ * compute_delta order, unfolded_DLASSO.py:127-140) instead of the neighbour masks, so it also
+ * covers the tiled / stepwise trajectories, e.g. the reference's defaults m = 100, n = 500
+ * (configurations.py:6-9) under unfolded_train_new.py:74-80's loss.backward().
+ * Replaces: the autograd backward of the reference's eager forward graph (as dadmm_backward).
+ * Valid only when the recorded forward's status was 0; deterministic (fixed reduction order). */
+int dadmm_adjoint(const dadmm_dims* d, const void* op, const int32_t* visit_ptr,
+                  const uint8_t* visit_q, const float* deg, const float* hyp, const float* y0,
+                  const float* d0, const float* Y, const float* Grec, const float* Urec,
+                  const float* gY, float* dhyp, void* scratch, void* stream);
+
 /* ---- GNN-hypernetwork model: per-iteration entry points --------------------------------------
  * DLASSO_GNNHyp3_Progressive.forward (gnn_dlasso_models_progressive.py:131-243) evaluates a GNN on
  * [A^T A y_k, A^T b] between iterations, so its loop runs one iteration per call, the caller
@@ -229,7 +247,7 @@ int dadmm_backward(const dadmm_dims* d, const void* op, const uint64_t* nbr,
  * on the device through `flags` (dadmm_gnn_flag_bytes(K) bytes): no host synchronisation.
  * Graph operands are the stepwise path's visit lists and degrees; H = dims.hyp_rows (P for
  * 'diff', 1 for 'same'); dims.variant selects the clamps (1 for this model). Shapes: P <= 64,
- * m <= 64, n % 4 == 0. */
+ * m <= 1024, n % 4 == 0. */
 size_t dadmm_gnn_flag_bytes(int32_t K);
 int dadmm_gnn_begin(const dadmm_dims* d, const void* op, const float* b, const float* y0,
                     const float* U0, float* Atb, int32_t* flags, void* stream);

@@ -14,6 +14,7 @@ REFERENCE = "/root/reference"  # read only as DATA (fixtures), never imported; a
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); run with -m gpu")
+    config.addinivalue_line("markers", "stepwise_only: a shape only the stepwise path covers")
 
 
 @pytest.fixture(scope="session")

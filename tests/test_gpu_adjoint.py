@@ -116,6 +116,86 @@ def test_adjoint_vs_oracle_on_own_trajectory(cuda, P, m, n, B, K, prob, per_samp
     _close(dh.cpu().numpy().astype(np.float64), want)
 
 
+# shapes only the general adjoint (dadmm_adjoint) covers: many agents, long signals, m > 64,
+# non-ascending adjacency at P > 8
+GENERAL_SHAPES = [
+    # P, m, n, B, K, prob, per_sample, H, variant
+    (5, 100, 500, 12, 10, 0.5, False, 5, 0),   # the reference's defaults m = 100, n = 500
+    (16, 64, 512, 9, 6, 0.3, True, 16, 0),     # BASELINE configs[2] agent count and size
+    (9, 40, 320, 14, 5, 0.4, False, 1, 1),     # 'same' mode, GNN variant
+    (50, 32, 1024, 3, 3, 0.5, True, 50, 0),    # configs[4] agent count and size
+    (12, 130, 96, 7, 4, 0.6, True, 12, 1),     # three m-groups
+]
+
+
+@pytest.mark.parametrize("P,m,n,B,K,prob,per_sample,H,variant", GENERAL_SHAPES + SHAPES[:3])
+def test_general_adjoint_vs_oracle_on_own_trajectory(cuda, P, m, n, B, K, prob, per_sample, H,
+                                                     variant):
+    """dadmm_adjoint (any shape) against the fp64 oracle adjoint along the recorded trajectory;
+    the fused shapes too (path 'general' on a fused trajectory)."""
+    from dadmm_hip.ops import backward_raw
+    A, b, _ = O.make_problem(P, m, n, B, seed=P * 10 + n)
+    graphs = _graphs(P, B, prob, per_sample)
+    y0, U0, d0 = _inits(B, P, n, seed=B)
+    rng = np.random.default_rng(K)
+    hyp = O.hyp_table((0.5 * rng.standard_normal((K, H, 4))).astype(np.float32), MAXP)
+    op, g, Y, _, st, traj = _record(cuda, A, b, graphs, hyp, y0, U0, d0, variant)
+    assert st == 0
+    Yo, _, _, Go, Uro = O.forward_f32_rec(A, b, graphs, hyp, y0, U0, d0, variant=variant)
+    assert np.array_equal(Y.cpu().numpy(), Yo)
+    assert np.array_equal(traj.Grec[..., :n].cpu().numpy(), Go)
+    rng = np.random.default_rng(7)
+    gY = rng.standard_normal((K, B, P, n)).astype(np.float32)
+    gY[: K // 2] *= 0.1
+    dh = backward_raw(op, g, traj, _t(gY, cuda), path="general")
+    torch.cuda.synchronize()
+    want = O.backward_np64(A, graphs, hyp, y0, d0, Yo, Go, Uro, gY, variant=variant)
+    _close(dh.cpu().numpy().astype(np.float64), want)
+
+
+def test_general_adjoint_non_ascending_adjacency(cuda):
+    """P = 10 graphs whose adjacency lists are not ascending (the progressive driver's
+    connectivity patch appends edges): the fused adjoint cannot follow them (P > 8), the general
+    adjoint uses the visit lists."""
+    import networkx as nx
+    from dadmm_hip.ops import backward_raw
+    P, m, n, B, K = 10, 24, 64, 6, 4
+    graphs = []
+    for s in range(B):
+        G = nx.Graph()
+        G.add_nodes_from(range(P))
+        r = np.random.default_rng(40 + s)
+        for q in r.permutation(P):
+            for t in r.choice(P, 3, replace=False):
+                if t != q:
+                    G.add_edge(int(q), int(t))
+        graphs.append(G)
+    A, b, _ = O.make_problem(P, m, n, B, seed=3)
+    y0, U0, d0 = _inits(B, P, n)
+    hyp = O.hyp_table((0.5 * np.random.default_rng(1).standard_normal((K, P, 4))).astype(np.float32), MAXP)
+    op, g, Y, _, st, traj = _record(cuda, A, b, graphs, hyp, y0, U0, d0)
+    assert st == 0 and not g.fused_ok
+    gY = np.random.default_rng(2).standard_normal((K, B, P, n)).astype(np.float32)
+    dh = backward_raw(op, g, traj, _t(gY, cuda))
+    want = O.backward_np64(A, graphs, hyp, y0, d0, Y.cpu().numpy(), traj.Grec[..., :n].cpu().numpy(),
+                           traj.Urec[..., :n].cpu().numpy(), gY)
+    _close(dh.cpu().numpy().astype(np.float64), want)
+
+
+def test_general_adjoint_deterministic(cuda):
+    from dadmm_hip.ops import backward_raw
+    P, m, n, B, K = 16, 100, 512, 40, 5
+    A, b, _ = O.make_problem(P, m, n, B, seed=4)
+    graphs = _graphs(P, B, 0.3, True)
+    y0, U0, d0 = _inits(B, P, n)
+    hyp = O.hyp_table(np.zeros((K, P, 4), np.float32), MAXP)
+    op, g, Y, _, st, traj = _record(cuda, A, b, graphs, hyp, y0, U0, d0)
+    gY = torch.randn(Y.shape, device=cuda, generator=torch.Generator(cuda).manual_seed(1))
+    d1 = backward_raw(op, g, traj, gY)
+    d2 = backward_raw(op, g, traj, gY)
+    assert torch.equal(d1, d2)
+
+
 def test_adjoint_deterministic(cuda):
     from dadmm_hip.ops import backward_raw
     P, m, n, B, K = 5, 64, 256, 300, 25

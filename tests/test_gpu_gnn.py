@@ -179,6 +179,40 @@ def test_guard_on_nonfinite_y0_bit_exact(cuda):
     assert np.array_equal(Y[..., 0].cpu().numpy(), Yo)
 
 
+@pytest.mark.parametrize("k_bad", [1, 3])
+def test_guard_on_nonfinite_ynext_bit_exact(cuda, k_bad):
+    """A NaN alpha from the hypernetwork at iteration k_bad makes y_next non-finite: the
+    reference keeps y_k and appends it (gnn_dlasso_models_progressive.py:235-237), so Y[k_bad]
+    must hold y_k, also when k_bad < K - 1 (the slot is rewritten by the next iteration)."""
+    P, m, n, B, K = 4, 16, 32, 8, 5
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", True)
+    model.eval()
+    model.hyper_backend = "torch"
+    orig = model.hypernetwork
+    calls = []
+
+    def patched(*args):
+        out = orig(*args)
+        if len(calls) == k_bad:
+            out[0][2, 1] = float("nan")   # alpha of sample 2, agent 1
+        calls.append(1)
+        return out
+
+    model.hypernetwork = patched
+    rec = _recording(model)
+    with torch.no_grad():
+        Y, _ = model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in inits))
+    st = int(model.last_status.item())
+    table = _hyp_table(rec, B, P)
+    assert np.isnan(table[k_bad]).any()
+    y0, U0, d0 = inits
+    Yo, _, sto = O.forward_f32_gram(A, b, graphs, table, y0, U0, d0, variant=1, hyp_mode=1)
+    assert st == sto and st & 8
+    Yg = Y[..., 0].cpu().numpy()
+    assert np.isfinite(Yg).all()
+    assert np.array_equal(Yg, Yo)
+
+
 def test_train_mode_step_updates_bn_and_trains(cuda):
     """train(): dropout on, per-sample BatchNorm statistics, running stats updated B*K times per
     forward; loss.backward() + AdamW step run (progressive driver's loop, :196-214)."""

@@ -135,12 +135,33 @@ BIG_SHAPES = [
     (50, 32, 1024, 3, 3, 0.5, True),    # configs[4]: P=50, n=1024, m=32, graph_prob 0.5
     (9, 40, 320, 18, 5, 0.4, False),
     (64, 16, 64, 2, 3, 0.2, True),      # the uint64-mask / uint8-id limit
+    # m > 64: two m-groups of 64 rows per agent (the reference's default m = 100, n = 500,
+    # configurations.py:6-9, and its shipped A.pt [1,5,100,500])
+    (5, 100, 500, 20, 8, 0.5, False),
+    (16, 100, 512, 9, 4, 0.3, True),
+    (5, 128, 256, 33, 6, 0.5, True),     # exactly two m-groups, n within the fused range
+    (3, 70, 64, 17, 5, 0.9, False),
+]
+# m beyond the tiled kernel's two m-groups: the stepwise path (any number of m-groups)
+STEPWISE_ONLY_SHAPES = [
+    (5, 200, 256, 10, 4, 0.5, True),
+    (2, 300, 128, 6, 3, 1.0, False),
 ]
 
 
 @pytest.mark.parametrize("path", ["auto", "stepwise", "tiled"])
-@pytest.mark.parametrize("P,m,n,B,K,prob,per_sample", SHAPES + BIG_SHAPES)
-def test_shapes_bit_exact(cuda, P, m, n, B, K, prob, per_sample, path):
+@pytest.mark.parametrize("P,m,n,B,K,prob,per_sample",
+                         SHAPES + BIG_SHAPES + [pytest.param(*s, marks=pytest.mark.stepwise_only)
+                                                for s in STEPWISE_ONLY_SHAPES])
+def test_shapes_bit_exact(cuda, P, m, n, B, K, prob, per_sample, path, request):
+    if path == "tiled" and request.node.get_closest_marker("stepwise_only"):
+        from dadmm_hip._lib import DadmmError
+        with pytest.raises(DadmmError, match="not a tiled shape"):
+            A, b, _ = O.make_problem(P, m, n, B, seed=1)
+            y0, U0, d0 = _inits(B, P, n)
+            _run_hip(cuda, A, b, [O.er_graph(P, prob, seed=3)] * B,
+                     O.hyp_table(np.zeros((K, P, 4), np.float32), MAXP), y0, U0, d0, path=path)
+        return
     A, b, _ = O.make_problem(P, m, n, B, seed=P * 100 + n)
     if per_sample:
         graphs = [O.connected_er_graph(P, prob, seed=1000 + s) for s in range(B)]
@@ -233,10 +254,11 @@ def test_guards_bit_exact(cuda, path):
         np.testing.assert_array_equal(U, Uo, err_msg=name)
 
 
-def test_guards_bit_exact_tiled_shapes(cuda):
-    """Shapes beyond the fused kernel (P = 9, n = 320): the tiled per-iteration kernel flags, the
-    gated persistent recomputation makes every guard exact."""
-    P, m, n, B, K = 9, 40, 320, 37, 5
+@pytest.mark.parametrize("m", [40, 100])
+def test_guards_bit_exact_tiled_shapes(cuda, m):
+    """Shapes beyond the fused kernel (P = 9, n = 320; m = 100: two m-groups): the tiled
+    per-iteration kernel flags, the gated persistent recomputation makes every guard exact."""
+    P, n, B, K = 9, 320, 37, 5
     graphs = [O.connected_er_graph(P, 0.4, seed=70 + s) for s in range(B)]
     for name, A, b, hyp, y0, U0, d0 in _guard_cases(P, m, n, B, K, seed=13):
         Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0, path="auto")
