@@ -44,6 +44,17 @@
 
 int oracle_abi_version(void) { return ORACLE_ABI_VERSION; }
 
+/* OpenMP team size of the restatements (the CPU-baseline legs time 1 thread and all host threads) */
+int oracle_set_threads(int t) {
+#ifdef _OPENMP
+    if (t > 0) omp_set_num_threads(t);
+    return omp_get_max_threads();
+#else
+    (void)t;
+    return 1;
+#endif
+}
+
 static int perm16(int idx) { return (idx & ~15) + 4 * (idx & 3) + ((idx & 15) >> 2); }
 
 static void hyp_at(int hyp_mode, int H, int B, const float* hyp, int k, int s, int p, float out[4]) {

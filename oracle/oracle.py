@@ -24,6 +24,7 @@ __all__ = [
     "lib", "hyp_table", "graph_arrays", "forward_f32", "forward_f64", "forward_np64",
     "forward_f32_rec", "forward_f32_gram", "laplacians", "backward_np64",
     "compute_loss", "make_problem", "load_fixture_tensor", "er_graph", "connected_er_graph",
+    "set_threads",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -48,8 +49,15 @@ def lib() -> ctypes.CDLL:
         L.oracle_forward_f32_rec.restype = ctypes.c_int
         L.oracle_forward_f32_rec.argtypes = [i, i, i, i, i, i, i, i] + [fp] * 14
         L.oracle_abi_version.restype = ctypes.c_int
+        L.oracle_set_threads.restype = ctypes.c_int
+        L.oracle_set_threads.argtypes = [i]
         _LIB = L
     return _LIB
+
+
+def set_threads(t: int) -> int:
+    """OpenMP threads of the C restatements (CPU-baseline legs); returns the team size now set."""
+    return int(lib().oracle_set_threads(int(t)))
 
 
 # --------------------------------------------------------------------------------------------

@@ -87,6 +87,60 @@ def forward(A, b, graph_list, hyp, y0, U0, d0, variant=0, dtype=torch.float32):
     return torch.stack(Y)[..., 0].numpy()
 
 
+def forward_vectorized(A, b, graph_list, hyp, y0, U0, d0, variant=0, dtype=torch.float32):
+    """The reference forward vectorised for the CPU (SURVEY.md §7 item 1, §8(d) CPU baseline (i)):
+    the same algorithm as ``forward`` — Gram form AtA @ y (unfolded_DLASSO.py:16, :69-71), the
+    guards, the clamps — with the P per-agent GEMVs as one batched matmul and compute_delta's
+    edge loop (:127-140) as the Laplacian product delta = 2 (D - Adj) y (one bmm per forward
+    iteration). fp32 results differ from the loop form only by summation order. Timing leg of the
+    CPU baseline; never the product path."""
+    A = torch.as_tensor(np.asarray(A), dtype=dtype)
+    if A.dim() == 4:
+        A = A[0]
+    P, m, n = A.shape
+    B = y0.shape[0]
+    b = torch.as_tensor(np.asarray(b), dtype=dtype).reshape(B, P, m)
+    hyp = torch.as_tensor(np.asarray(hyp), dtype=dtype)
+    AtA = torch.matmul(A.transpose(1, 2), A)                       # [P, n, n]
+    Atb = torch.einsum("pmn,bpm->bpn", A, b)                       # [B, P, n]
+    adj = np.zeros((len(graph_list), P, P), np.float32)
+    for s, G in enumerate(graph_list):
+        for p in range(P):
+            for q in G.neighbors(p):
+                adj[s, p, q] += 1.0
+    adj = torch.from_numpy(adj).to(dtype)
+    deg = adj.sum(-1, keepdim=True)                                # [G, P, 1]
+    lap2 = 2.0 * (torch.diag_embed(deg[..., 0]) - adj)             # 2 L, [G, P, P]
+    y = torch.as_tensor(np.asarray(y0), dtype=dtype).reshape(B, P, n).clone()
+    U = torch.as_tensor(np.asarray(U0), dtype=dtype).reshape(B, P, n).clone()
+    d = torch.as_tensor(np.asarray(d0), dtype=dtype).reshape(B, P, n).clone()
+    Y = torch.empty((hyp.shape[0], B, P, n), dtype=dtype)
+    for k in range(hyp.shape[0]):
+        if not torch.isfinite(y).all():
+            y = torch.zeros_like(y)
+        if not torch.isfinite(U).all():
+            U = torch.zeros_like(U)
+        h = hyp[k]
+        al, ta, rh, et = (h[:, c].reshape(1, -1, 1) for c in range(4))
+        AtAy = torch.bmm(AtA, y.permute(1, 2, 0)).permute(2, 0, 1)  # [B, P, n]
+        grad = AtAy - Atb + y.sign() * ta + U * deg + d * rh
+        gclip = max(1.0, 30.0 - k) if variant == 0 else 10.0
+        vclip = max(10.0, 200.0 - k * 3) if variant == 0 else 100.0
+        grad = torch.clamp(grad, -gclip, gclip)
+        if not torch.isfinite(grad).all():
+            grad = torch.zeros_like(grad)
+        yn = torch.clamp(y - al * grad, -vclip, vclip)
+        d = torch.matmul(lap2, yn)
+        if variant != 0:
+            d = torch.clamp(d, -20.0, 20.0)
+        U = torch.clamp(U + d * et, -vclip, vclip)
+        if not torch.isfinite(yn).all():
+            yn = y
+        y = yn
+        Y[k] = y
+    return Y.numpy()
+
+
 def forward_autograd(A, b, graph_list, hyp, y0, U0, d0, variant=0, dtype=torch.float64):
     """The same op sequence as ``forward`` (no guards: finite inputs only) on torch tensors that keep
     the autograd graph, so ``torch.autograd.grad`` takes exactly the derivative the reference's
