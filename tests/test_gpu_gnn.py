@@ -118,6 +118,45 @@ def test_hypernetwork_matches_numpy_restatement(cuda):
             np.testing.assert_allclose(g, w, rtol=1e-4, atol=1e-4 * np.abs(w).max())
 
 
+def test_configs4_model_vs_numpy_restatement(cuda):
+    """BASELINE configs[4]'s model: P = 50 agents, n = 1024, m = 32, GHyp_hidden = 100, per-sample
+    connected ER(0.5) graphs, K = 10 iterations, eval mode (fused HIP hypernetwork), with
+    non-trivial BatchNorm running statistics. Every iteration's (alpha, tau, rho, eta) against the
+    numpy fp64 restatement of GNNHypernetwork3 + decoder + fc (oracle/gnn_np.py) on the features
+    the kernels produced, and the whole recurrence bit-exact against oracle.forward_f32_gram
+    given those hyper-parameters."""
+    P, m, n, B, K = 50, 32, 1024, 3, 10
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", True, seed=4, hidden=100)
+    g = torch.Generator().manual_seed(9)
+    with torch.no_grad():
+        for name, buf in model.named_buffers():
+            if name.endswith("running_mean"):
+                buf.copy_(0.1 * torch.randn(buf.shape, generator=g))
+            elif name.endswith("running_var"):
+                buf.copy_(0.5 + torch.rand(buf.shape, generator=g))
+        for name, prm in model.named_parameters():
+            if ".bn" in name:
+                prm.add_(0.05 * torch.randn(prm.shape, generator=g).to(prm.device))
+    model.eval()
+    rec = _recording(model)
+    with torch.no_grad():
+        Y, _ = model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in inits))
+    assert int(model.last_status.item()) == 0
+    assert len(rec) == K
+    sd = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in model.state_dict().items()}
+    maxima = tuple(float(np.float32(v)) for v in (0.1, 0.99, 0.99, 0.99))
+    for AtAy, Atb, out in rec:
+        feats = torch.cat([AtAy, Atb], dim=2).cpu().numpy().astype(np.float64)
+        want = gnn_np.hypernetwork(sd, feats, graphs, maxima, False)
+        for got, w in zip(out, want):
+            got = got[..., 0, 0].cpu().numpy()
+            np.testing.assert_allclose(got, w, rtol=1e-4, atol=1e-4 * np.abs(w).max())
+    table = _hyp_table(rec, B, P)
+    Yo, _, st = O.forward_f32_gram(A, b, graphs, table, *inits, variant=1, hyp_mode=1)
+    assert st == 0
+    assert np.array_equal(Y[..., 0].cpu().numpy(), Yo), np.abs(Y[..., 0].cpu().numpy() - Yo).max()
+
+
 def test_features_are_the_reference_gram_and_atb(cuda):
     """AtAy_0 = AtA @ y0 and Atb = compute_Atx(b) (fp64 check, fp32 tolerance)."""
     P, m, n, B, K = 4, 24, 48, 10, 1

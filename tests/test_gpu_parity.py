@@ -177,6 +177,24 @@ def test_shapes_bit_exact(cuda, P, m, n, B, K, prob, per_sample, path, request):
     assert np.array_equal(U, Uo)
 
 
+def test_configs2_full_depth_bit_exact(cuda):
+    """BASELINE configs[2] at full depth: P = 16, n = 512, m = 64, K = 25, per-sample connected
+    ER(p = 0.3) graphs (the progressive driver's connectivity patch, gnn_dlasso_progressive.py:
+    181-191), B = 64 — the tiled path with the gated guard recompute, every iterate bit-exact
+    (the k-dependent clamp schedule runs through k = 24, unfolded_DLASSO.py:80, 92)."""
+    P, m, n, B, K = 16, 64, 512, 64, 25
+    A, b, _ = O.make_problem(P, m, n, B, seed=1616)
+    graphs = [O.connected_er_graph(P, 0.3, seed=4000 + s) for s in range(B)]
+    y0, U0, d0 = _inits(B, P, n, seed=16)
+    rng = np.random.default_rng(25)
+    hyp = O.hyp_table((0.4 * rng.standard_normal((K, P, 4))).astype(np.float32), MAXP)
+    Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0, path="auto")
+    Yo, Uo, sto = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
+    assert st == sto == 0
+    assert np.array_equal(Y, Yo), f"max |diff| {np.abs(Y - Yo).max()}"
+    assert np.array_equal(U, Uo)
+
+
 @pytest.mark.parametrize("path", ["auto", "stepwise", "tiled"])
 def test_same_mode_and_gnn_variant(cuda, path):
     """'same' hyper-parameters (H = 1) and the GNN variant's fixed clamps / delta clamp."""
