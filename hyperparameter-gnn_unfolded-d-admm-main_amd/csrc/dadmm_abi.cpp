@@ -520,6 +520,22 @@ int dadmm_prologue(uint64_t seed, uint64_t offset, int64_t numel, int32_t n, int
 }
 
 
+int dadmm_graph_generate(int32_t B, int32_t P, float prob, uint64_t seed, int32_t connect,
+                         int64_t* nbr, float* deg, int32_t* order, int32_t* vptr, uint8_t* vq,
+                         int32_t* scratch, void* stream) {
+    if (B < 0 || P < 1 || P > 64) return fail(DADMM_EINVAL, "bad graph dims B=%d P=%d (P <= 64)", B, P);
+    if (!(prob >= 0.0f && prob <= 1.0f)) return fail(DADMM_EINVAL, "edge probability %g not in [0, 1]", prob);
+    if (order != nullptr && P > 8) return fail(DADMM_EINVAL, "order packs 4-bit agent ids: P <= 8");
+    if (B == 0) return ok();
+    if (!nbr || !deg || !vptr || !scratch) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if ((int64_t)B * 2 * P * (P - 1) >= ((int64_t)1 << 31))
+        return fail(DADMM_EUNSUPPORTED, "visit lists past 2^31 entries (split the batch)");
+    dadmm::GraphGenArgs a{B, P, prob, seed, connect ? 1 : 0, nbr, deg, order, scratch, vptr, vq};
+    hipError_t e = dadmm::launch_graphgen(a, vq == nullptr ? 0 : 1, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "graph generation launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 size_t dadmm_tiled_scratch_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;
     return 3 * align256(sizeof(float) * (size_t)d->B * d->P * d->n);   // U ping-pong, delta

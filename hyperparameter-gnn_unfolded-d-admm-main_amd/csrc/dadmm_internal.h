@@ -226,6 +226,21 @@ struct RowNormArgs {
 };
 hipError_t launch_rownorm(const RowNormArgs& a, hipStream_t st);
 
+// ---- device-side ER graph generation (dadmm_graphgen.hip) ---------------------------------------
+struct GraphGenArgs {
+    int B, P;
+    float prob;
+    uint64_t seed;
+    int connect;            // apply the progressive driver's connectivity patch
+    int64_t* nbr;           // [B][P] neighbour masks
+    float* deg;             // [B][P]
+    int32_t* order;         // [B][P] packed adjacency order (P <= 8) or nullptr
+    int32_t* counts;        // scratch [B]: visit entries per sample, then their offsets
+    int32_t* vptr;          // [B*P + 1]
+    uint8_t* vq;            // visit lists (nullptr: offsets only)
+};
+hipError_t launch_graphgen(const GraphGenArgs& a, int pass, hipStream_t st);
+
 // ---- forward prologue (dadmm_rng.hip) -----------------------------------------------------------
 struct PrologueArgs {
     uint64_t seed, offset, offset_step;   // torch Philox state; per-tensor offset increment

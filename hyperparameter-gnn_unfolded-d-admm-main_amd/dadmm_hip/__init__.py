@@ -5,7 +5,8 @@ live next to this package; put its parent directory on ``sys.path`` and the refe
 import them unchanged.
 """
 from . import _lib
-from .graph import GraphBatch, from_csr, ingest
+from .graph import GraphBatch, from_csr, generate_er, ingest, to_networkx
 from .ops import PreparedOperator, forward_raw
 
-__all__ = ["_lib", "GraphBatch", "from_csr", "ingest", "PreparedOperator", "forward_raw"]
+__all__ = ["_lib", "GraphBatch", "from_csr", "generate_er", "ingest", "to_networkx",
+           "PreparedOperator", "forward_raw"]

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -50,6 +50,7 @@ EXPORTED_SYMBOLS = (
     "dadmm_prologue",
     "dadmm_tiled_scratch_bytes",
     "dadmm_forward_tiled",
+    "dadmm_graph_generate",
     "dadmm_loss_scratch_bytes",
     "dadmm_loss",
     "dadmm_loss_grad",
@@ -122,6 +123,8 @@ def load() -> ctypes.CDLL:
     L.dadmm_tiled_scratch_bytes.argtypes = [D]
     L.dadmm_forward_tiled.restype = ctypes.c_int
     L.dadmm_forward_tiled.argtypes = [D] + [vp] * 14
+    L.dadmm_graph_generate.restype = ctypes.c_int
+    L.dadmm_graph_generate.argtypes = [i32, i32, f32, u64, i32] + [vp] * 7
     L.dadmm_loss_scratch_bytes.restype = ctypes.c_size_t
     L.dadmm_loss_scratch_bytes.argtypes = [i32, i64, i32]
     L.dadmm_loss.restype = ctypes.c_int

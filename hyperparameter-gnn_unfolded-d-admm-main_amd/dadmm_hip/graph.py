@@ -291,6 +291,74 @@ def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
     return _batch([per[id(g)] for g in graph_list], P, device)
 
 
+def generate_er(B: int, P: int, prob: float, seed: int, device, connect: bool = True) -> GraphBatch:
+    """B per-sample Erdos-Renyi graphs on agents 0..P-1 generated ON THE DEVICE, already in the
+    kernels' layouts (dadmm_graph_generate, csrc/dadmm_graphgen.hip): the progressive driver's
+    ``nx.erdos_renyi_graph(P, prob)`` + connectivity patch (gnn_dlasso_progressive.py:181-191)
+    and its ingestion, without networkx. Reproducible from ``seed`` (not networkx's RNG)."""
+    import ctypes
+    from . import _lib
+    if P > 64:
+        raise ValueError(f"P={P} > 64 agents does not fit the uint64 neighbour mask")
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise RuntimeError("generate_er runs on a ROCm GPU (device must be cuda/hip)")
+    L = _lib.load()
+    nbr = torch.empty((B, P), dtype=torch.int64, device=device)
+    deg = torch.empty((B, P), dtype=torch.float32, device=device)
+    with_order = connect and P <= 8
+    order = torch.empty((B, P), dtype=torch.int32, device=device) if with_order else None
+    vptr = torch.empty(B * P + 1, dtype=torch.int32, device=device)
+    scratch = torch.empty(max(B, 1), dtype=torch.int32, device=device)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None   # noqa: E731
+    with torch.cuda.device(device):
+        stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+        args = (B, P, float(prob), int(seed) & (2 ** 64 - 1), int(connect))
+        _lib.check("dadmm_graph_generate", L.dadmm_graph_generate(
+            *args, vp(nbr), vp(deg), vp(order), vp(vptr), None, vp(scratch), stream))
+        total = int(vptr[-1].item()) if B > 0 else 0      # sizes the visit lists (one sync)
+        vq = torch.empty(max(total, 1), dtype=torch.uint8, device=device)
+        if B > 0:
+            _lib.check("dadmm_graph_generate", L.dadmm_graph_generate(
+                *args, vp(nbr), vp(deg), vp(order), vp(vptr), vp(vq), vp(scratch), stream))
+        else:
+            vptr.zero_()
+    # non-ascending adjacency (connectivity edges) is followed through order (P <= 8) or the
+    # visit lists; the fused kernel needs the former
+    return GraphBatch(nbr, deg, False, order, vptr, vq, fused_ok=not (connect and P > 8))
+
+
+def to_networkx(gb: GraphBatch, P: int):
+    """networkx graphs with the adjacency order a GraphBatch encodes (the own-list segment of each
+    agent's visit list): the inverse of ingest(), for checking a GraphBatch against the host path
+    and the oracle. Per-sample batches only."""
+    import networkx as nx
+    if gb.shared:
+        raise ValueError("to_networkx needs a per-sample GraphBatch")
+    nbr = gb.nbr.cpu().numpy().view(np.uint64)
+    vptr = gb.vptr.cpu().numpy()
+    vq = gb.vq.cpu().numpy()
+    out = []
+    for s in range(nbr.shape[0]):
+        adj = {}
+        for p in range(P):
+            m = int(nbr[s, p])
+            below = bin(m & ((1 << p) - 1)).count("1")
+            d = bin(m).count("1")
+            o = int(vptr[s * P + p]) + below
+            adj[p] = [int(q) for q in vq[o:o + d]]
+        # each agent's adjacency dict filled in the recorded order (graph.neighbors(p) follows
+        # it); one shared attribute dict per undirected edge, as add_edge would make
+        G = nx.Graph()
+        G.add_nodes_from(range(P))
+        data = {}
+        for p in range(P):
+            for q in adj[p]:
+                G._adj[p][q] = data.setdefault((min(p, q), max(p, q)), {})
+        out.append(G)
+    return out
+
+
 def from_csr(nbr_ptr, nbr_idx, deg, P: int, device) -> GraphBatch:
     """GraphBatch from neighbour lists already in CSR form (no networkx): ``nbr_ptr`` [B*P+1],
     ``nbr_idx`` (adjacency order), ``deg`` [B, P]. The tensor fast path for callers that keep

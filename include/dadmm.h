@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 9
+#define DADMM_ABI_VERSION 10
 
 enum {
     DADMM_OK = 0,
@@ -213,6 +213,21 @@ int dadmm_backward(const dadmm_dims* d, const void* op, const uint64_t* nbr,
                    const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
                    const float* d0, const float* Y, const float* Grec, const float* Urec,
                    const float* gY, float* dhyp, void* scratch, void* stream);
+
+/* Per-sample Erdos-Renyi agent graphs generated on the device, directly in the graph layouts
+ * above: nbr [B][P], deg [B][P], order [B][P] (nullable; P <= 8), vptr [B*P+1], vq.
+ * Replaces: the progressive driver's per-batch host loop (gnn_dlasso_progressive.py:181-191:
+ *           nx.erdos_renyi_graph(P, prob) per sample, and with `connect` the edges that join its
+ *           connected components in order) plus the ingestion of those graphs
+ *           (unfolded_DLASSO.py:111-118, :127-140's graph walk).
+ * Pair u < v of sample s is an edge iff a counter-based hash of (seed, s, u, v) maps below
+ * `prob` (dadmm_graphgen.hip; reproducible, not networkx's RNG stream). Two calls: with
+ * vq = NULL it writes nbr / deg / order / vptr (vptr[B*P] = the number of visit entries; the
+ * caller reads it to size vq) and keeps per-sample offsets in `scratch` (B int32); the second
+ * call, same arguments plus vq, writes the visit lists. */
+int dadmm_graph_generate(int32_t B, int32_t P, float prob, uint64_t seed, int32_t connect,
+                         int64_t* nbr, float* deg, int32_t* order, int32_t* vptr, uint8_t* vq,
+                         int32_t* scratch, void* stream);
 
 /* Bytes of device scratch dadmm_adjoint needs for `d` (256-byte aligned pointer). */
 size_t dadmm_adjoint_scratch_bytes(const dadmm_dims* d);
