@@ -314,11 +314,20 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
         g5 = GM.DLASSO_GNNHyp3_Progressive(torch.from_numpy(A5)[None].to(dev), args5).to(dev).eval()
         graphs5 = [O.connected_er_graph(P5, 0.5, seed=500 + s) for s in range(B5)]
         b5t = torch.from_numpy(b5)[..., None].to(dev)
+        from dadmm_hip.graph import generate_er as _gen5
         from dadmm_hip.graph import ingest as _ing5
         t0 = time.perf_counter()
         gb5 = _ing5(graphs5, P5, B5, dev)
         torch.cuda.synchronize()
         ingest5_ms = 1e3 * (time.perf_counter() - t0)
+        # the same graph model generated on the device (gnn_dlasso_progressive.py:181-191)
+        _gen5(B5, P5, 0.5, 1, dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(5):
+            _gen5(B5, P5, 0.5, 2 + i, dev)
+        torch.cuda.synchronize()
+        gen5_ms = 1e3 * (time.perf_counter() - t0) / 5
 
         def g5fwd():
             with torch.no_grad():
@@ -328,8 +337,11 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
                                  "graph_prob": 0.5, "ms": ms5,
                                  "units_per_s": B5 * K5 / (ms5 * 1e-3),
                                  "graph_ingest_ms": ingest5_ms,
+                                 "graph_generate_device_ms": gen5_ms,
                                  "note": "per-GPU shard of configs[4] (8192 / 8); forward with "
-                                         "pre-ingested graphs, ingestion timed separately"}
+                                         "pre-ingested graphs; host networkx ingestion and "
+                                         "on-device generation (dadmm_graph_generate, incl. "
+                                         "one host sync) timed separately"}
         del g5, b5t
     except Exception as e:
         out["c5_error"] = repr(e)[:300]

@@ -21,7 +21,7 @@ class GnnRun:
     table (y0, y_1 .. y_K) and its device pointer array."""
 
     def __init__(self, op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, K: int, H: int,
-                 variant: int, y0, U0, d0, grad: bool):
+                 variant: int, y0, U0, d0, grad: bool, begin: bool = True):
         _dev_check(b, y0, U0, d0, graphs.deg)
         B, P, m = b.shape
         ns = op.n_store
@@ -47,10 +47,15 @@ class GnnRun:
         self.Atb = torch.empty((B, P, ns), device=dev)
         self.G = torch.empty((B, P, ns), device=dev)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
-        with torch.cuda.device(dev):
+        if begin:
+            self.begin()
+
+    def begin(self):
+        """Zero the guard flags, the k = 0 guards, Atb = A^T b (dadmm_gnn_begin); enqueued."""
+        with torch.cuda.device(self.dev):
             _lib.check("dadmm_gnn_begin", self.L.dadmm_gnn_begin(
-                ctypes.byref(self.d), _ptr(op.workspace), _ptr(self.b), _ptr(self.y0),
-                _ptr(self.U0), _ptr(self.Atb), _ptr(self.flags), _stream(dev)))
+                ctypes.byref(self.d), _ptr(self.op.workspace), _ptr(self.b), _ptr(self.y0),
+                _ptr(self.U0), _ptr(self.Atb), _ptr(self.flags), _stream(self.dev)))
 
     def gram(self, k: int, x: torch.Tensor = None) -> torch.Tensor:
         """A^T A y_k (guard-resolved y_k) or, with ``x``, A^T A x."""

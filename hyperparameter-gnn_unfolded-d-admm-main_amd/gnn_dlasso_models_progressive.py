@@ -176,6 +176,10 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         # "auto": the fused HIP hypernetwork in inference (eval + no_grad), torch otherwise;
         # "torch": always the torch composition (tests compare the two)
         self.hyper_backend = "auto"
+        # inference forwards replay a captured HIP graph of the K-iteration loop (one launch of
+        # ~16 K kernels instead of as many host calls); False: issue them one by one
+        self.use_hip_graph = True
+        self._graph_plans = {}
         # optional observer, called every iteration with (AtAy_k, Atb, (alpha, tau, rho, eta))
         self.on_hyp = None
 
@@ -243,6 +247,8 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         ys = []
         # inference (model.eval() under no_grad): the hypernetwork runs on the fused HIP kernels
         fused = self.hyper_backend == "auto" and not grad and hyper_ops.supported(self, n)
+        if fused and self.use_hip_graph and self.on_hyp is None:
+            return self._forward_graphed(bb, graphs, a_hat.contiguous(), y0, U0, d0, K, H)
         if fused:
             enc = self.encoder
             bufs = hyper_ops.HyperBuffers(batch_size, self.P, enc.conv5.lin.out_features,
@@ -267,6 +273,22 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         Y = Y[..., :n].unsqueeze(-1)
         return Y, (alpha_k, tau_k, rho_k, eta_k)
 
+    def _forward_graphed(self, bb, graphs, a_hat, y0, U0, d0, K, H):
+        """The inference forward as one replay of a captured HIP graph (_EvalGraphPlan); the
+        plan is captured once per (shapes, graph layout, parameter storage) and reused."""
+        key = (tuple(bb.shape), K, H, graphs.shared, graphs.order is not None,
+               tuple(a_hat.shape), str(bb.device),
+               tuple(t.data_ptr() for t in list(self.parameters()) + list(self.buffers())),
+               self.operator().workspace.data_ptr())
+        plan = self._graph_plans.get(key)
+        if plan is None or plan.vq_cap < graphs.vq.numel():
+            if len(self._graph_plans) >= 4:
+                self._graph_plans.clear()
+            plan = _EvalGraphPlan(self, bb, graphs, a_hat, K, H)
+            self._graph_plans[key] = plan
+        Y, hyp, self.last_status = plan.run(bb, graphs, a_hat, y0, U0, d0)
+        return Y[..., :self.n].unsqueeze(-1), hyp
+
     # kept for API parity with the reference (:245-276); not used by the HIP forward
     def compute_sum_neighbors(self, graph_list):
         g = ingest(graph_list, self.P, len(graph_list), self.A.device)
@@ -276,3 +298,84 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
     def compute_Atx(self, x):
         A = self.A.to(x.device)
         return torch.einsum('pmn,bpmc->bpnc', A[0], x)
+
+
+class _EvalGraphPlan:
+    """A captured HIP graph of the inference forward's K-iteration loop (model.eval() under
+    no_grad, fused hypernetwork): dadmm_gnn_begin, then per iteration the gram, the 13
+    hypernetwork launches and the step pair, then dadmm_gnn_finish — about 16 K launches replayed
+    as one, so the forward is bound by the GPU, not by host calls.
+
+    Inputs are copied into the plan's static buffers before each replay (b, inits, the graph
+    layouts and a_hat: a few MB), and each replay writes a FRESH output Y: the kernels find the
+    iterates through the device pointer table ``yptr`` (y0, y_1 .. y_K), which is re-pointed at
+    the new Y on the device before the replay. The returned hyper-parameters are copies."""
+
+    def __init__(self, model, bb, graphs, a_hat, K, H):
+        from dadmm_hip.graph import GraphBatch
+        dev = bb.device
+        op = model.operator()
+        B, P, _ = bb.shape
+        ns = op.n_store
+        self.K, self.ns, self.B, self.P = K, ns, B, P
+        self.vq_cap = max(int(graphs.vq.numel()), 1)
+        self.b = torch.empty_like(bb, memory_format=torch.contiguous_format)
+        self.y0, self.U0, self.d0 = (torch.zeros((B, P, ns), device=dev) for _ in range(3))
+        self.gb = GraphBatch(graphs.nbr.clone(), graphs.deg.clone(), graphs.shared,
+                             graphs.order.clone() if graphs.order is not None else None,
+                             graphs.vptr.clone(), torch.zeros(self.vq_cap, dtype=torch.uint8, device=dev),
+                             graphs.fused_ok)
+        self.ahat = a_hat.clone()
+        self.run_ = GnnRun(op, self.b, self.gb, K, H, _lib.VARIANT_GNN, self.y0, self.U0, self.d0,
+                           False, begin=False)
+        enc = model.encoder
+        self.bufs = hyper_ops.HyperBuffers(B, P, enc.conv5.lin.out_features,
+                                           [model.decoder[i].out_features for i in (0, 4, 8)], H, dev)
+        self.steps = torch.arange(K, device=dev, dtype=torch.int64) * (B * P * ns * 4)
+        self._load(bb, graphs, a_hat, None, None, None)
+        n = model.n
+        per_sample = not graphs.shared
+
+        def body():
+            run = self.run_
+            run.begin()
+            y, U, D = run.ys[0], run.U0, run.d0
+            for k in range(K):
+                AtAy = run.gram(k)
+                hyper_ops.hypernetwork_eval(model, AtAy, run.Atb, n, self.ahat, per_sample, self.bufs)
+                y, U, D = run.step(k, AtAy, self.bufs.hyp, U, D)
+            run.finish()
+
+        cur = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            body()                          # warm-up outside the capture (first-call setup)
+        cur.wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            body()
+
+    def _load(self, bb, graphs, a_hat, y0, U0, d0):
+        self.b.copy_(bb)
+        for dst, src in ((self.y0, y0), (self.U0, U0), (self.d0, d0)):
+            if src is not None:
+                dst[..., :src.shape[-1]].copy_(src)
+        g = self.gb
+        g.nbr.copy_(graphs.nbr)
+        g.deg.copy_(graphs.deg)
+        g.vptr.copy_(graphs.vptr)
+        g.vq[:graphs.vq.numel()].copy_(graphs.vq)
+        if g.order is not None:
+            g.order.copy_(graphs.order)
+        self.ahat.copy_(a_hat)
+
+    def run(self, bb, graphs, a_hat, y0, U0, d0):
+        self._load(bb, graphs, a_hat, y0, U0, d0)
+        Y = torch.empty((self.K, self.B, self.P, self.ns), device=bb.device)
+        self.run_.yptr[1:].copy_(self.steps + Y.data_ptr())     # the replay writes this Y
+        self.graph.replay()
+        h = self.bufs.hyp.clone()
+        H = h.shape[2]
+        hyp = tuple(h[:, c].view(self.B, H, 1, 1) for c in range(4))
+        return Y, hyp, self.run_.status.clone()

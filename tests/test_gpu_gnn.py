@@ -157,6 +157,40 @@ def test_configs4_model_vs_numpy_restatement(cuda):
     assert np.array_equal(Y[..., 0].cpu().numpy(), Yo), np.abs(Y[..., 0].cpu().numpy() - Yo).max()
 
 
+@pytest.mark.parametrize("P,m,n,B,K,mode,per_sample", [(5, 32, 64, 24, 6, "diff", True),
+                                                        (5, 16, 64, 10, 4, "same", False),
+                                                        (13, 40, 200, 9, 3, "diff", True)])
+def test_hip_graph_replay_matches_eager(cuda, P, m, n, B, K, mode, per_sample):
+    """The inference forward replayed from a captured HIP graph (_EvalGraphPlan) equals the
+    launch-by-launch forward bit for bit, call after call with new inputs (b, inits, graphs):
+    the plan copies them in and writes a fresh Y each time."""
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, mode, per_sample, seed=2)
+    model.eval()
+    outs = {}
+    for use in (False, True):
+        model.use_hip_graph = use
+        res = []
+        for call in range(3):
+            rng = np.random.default_rng(100 + call)
+            y0, U0, d0 = (1e-2 * rng.standard_normal((3, B, P, n))).astype(np.float32)
+            bb = b * (1.0 + 0.1 * call)
+            gs = graphs if call != 1 else [O.connected_er_graph(P, 0.6, seed=900 + s) for s in range(B)]
+            if not per_sample:
+                gs = [gs[0]] * B
+            with torch.no_grad():
+                Y, hyp = model(_t(bb, cuda)[..., None], gs,
+                               inits=tuple(_t(v, cuda) for v in (y0, U0, d0)))
+            res.append((Y.clone(), [h.clone() for h in hyp], int(model.last_status.item())))
+        outs[use] = res
+    assert len(model._graph_plans) >= 1
+    for (Ye, he, se), (Yg, hg, sg) in zip(outs[False], outs[True]):
+        assert se == sg == 0
+        assert torch.equal(Ye, Yg)
+        assert all(torch.equal(a, c) for a, c in zip(he, hg))
+    # fresh outputs: the first call's Y is not overwritten by the later replays
+    assert not torch.equal(outs[True][0][0], outs[True][2][0])
+
+
 def test_features_are_the_reference_gram_and_atb(cuda):
     """AtAy_0 = AtA @ y0 and Atb = compute_Atx(b) (fp64 check, fp32 tolerance)."""
     P, m, n, B, K = 4, 24, 48, 10, 1
