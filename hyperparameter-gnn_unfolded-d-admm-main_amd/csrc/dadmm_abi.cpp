@@ -790,6 +790,120 @@ int dadmm_hyper_linear_ln(int32_t rows, int32_t K, int32_t N, const float* x, in
     return ok();
 }
 
+int dadmm_hyper_gcn_train(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1, int32_t ld1,
+                          int32_t K1, const float* x2, int32_t ld2, const float* W, const float* bias,
+                          const float* ahat, int32_t ahat_per_sample, const float* bn_weight,
+                          const float* bn_bias, float bn_eps, float slope, float drop_p, uint64_t seed,
+                          int32_t site, float* y, int32_t ldy, float* m_out, float* mean_out,
+                          float* var_out, void* stream) {
+    if (B < 0 || P < 2 || P > 64)
+        return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d (training BatchNorm needs P >= 2)", B, P);
+    if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(DADMM_EINVAL, "dropout p=%g not in [0, 1)", drop_p);
+    dadmm::HyperArgs a;
+    int rc = hyper_input(B * P, K, N, x1, ld1, K1, x2, ld2, W, y, ldy, &a);
+    if (rc) return rc;
+    if (!bias || !ahat || !bn_weight || !bn_bias || !m_out || !mean_out || !var_out)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(m_out) || (N & 3) || (ldy & 3) || !aligned16(y))
+        return fail(DADMM_EUNSUPPORTED, "training GCN needs N %% 4 == 0 and 16-byte aligned y / m_out");
+    a.bias = bias;
+    a.B = B;
+    a.P = P;
+    a.ahat = ahat;
+    a.ahat_per_sample = ahat_per_sample ? 1 : 0;
+    a.bn_w = bn_weight;
+    a.bn_b = bn_bias;
+    a.bn_eps = bn_eps;
+    a.slope = slope;
+    a.save_m = m_out;
+    a.save_mean = mean_out;
+    a.save_var = var_out;
+    a.drop_p = drop_p;
+    a.seed = seed;
+    a.site = site;
+    hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_GCN_TRAIN, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "gcn train launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_hyper_gcn_train_bwd(int32_t B, int32_t P, int32_t N, const float* dy, const float* m,
+                              const float* mean, const float* var, const float* bn_weight,
+                              float bn_eps, const float* ahat, int32_t ahat_per_sample, float slope,
+                              float drop_p, uint64_t seed, int32_t site, float* dz, float* part,
+                              void* stream) {
+    if (B < 0 || P < 2 || P > 64 || N < 1) return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d N=%d", B, P, N);
+    if (!dy || !m || !mean || !var || !bn_weight || !ahat || !dz || !part)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if ((int64_t)B * P * N >= ((int64_t)1 << 31)) return fail(DADMM_EUNSUPPORTED, "operand larger than 2^31 floats");
+    dadmm::GcnBwdArgs a{dy, m, mean, var, bn_weight, ahat, ahat_per_sample ? 1 : 0, dz, part, B, P, N,
+                        bn_eps, slope, drop_p, seed, site};
+    hipError_t e = dadmm::launch_gcn_bwd(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "gcn backward launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_hyper_linear_ln_train(int32_t rows, int32_t K, int32_t N, const float* x, int32_t ldx,
+                                const float* W, const float* bias, const float* ln_weight,
+                                const float* ln_bias, float eps, int32_t act, float slope, float drop_p,
+                                uint64_t seed, int32_t site, float* y, float* xd, void* scratch,
+                                void* stream) {
+    dadmm::HyperArgs a;
+    int rc = hyper_input(rows, K, N, x, ldx, K, nullptr, 0, W, y, N, &a);
+    if (rc) return rc;
+    if ((N & 3) || N > 2048) return fail(DADMM_EUNSUPPORTED, "LayerNorm width N=%d: N %% 4 == 0, N <= 2048", N);
+    if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(DADMM_EINVAL, "dropout p=%g not in [0, 1)", drop_p);
+    if (!bias || !ln_weight || !ln_bias || !scratch || !xd) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(scratch) || !aligned16(y) || !aligned16(xd) || !aligned16(bias) ||
+        !aligned16(ln_weight) || !aligned16(ln_bias))
+        return fail(DADMM_EINVAL, "y, xd, scratch, bias and the LayerNorm parameters must be 16-byte aligned");
+    if (rows == 0) return ok();
+    a.splits = dadmm::hyper_linear_splits(rows, K, N);
+    a.split_stride = (size_t)rows * N;
+    a.y = (float*)scratch;
+    a.ldy = N;
+    a.P = 1;
+    a.B = rows;
+    hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_BIAS, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "linear launch: %s", hipGetErrorString(e));
+    dadmm::RowNormArgs r{(const float*)scratch, ln_weight, ln_bias, y, rows, N, act ? 1 : 0, eps,
+                         slope, a.splits, a.split_stride, bias, drop_p, seed, site, xd};
+    e = dadmm::launch_rownorm(r, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "rownorm launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+size_t dadmm_hyper_rownorm_bwd_part_bytes(int32_t rows, int32_t C) {
+    if (rows < 0 || C < 1) return 0;
+    return 4 * (size_t)((rows + dadmm::ROWNORM_BWD_ROWS - 1) / dadmm::ROWNORM_BWD_ROWS) * 2 * C;
+}
+
+int dadmm_hyper_rownorm_bwd(int32_t rows, int32_t C, const float* dy, const float* xd,
+                            const float* weight, const float* bias, float eps, int32_t act,
+                            float slope, float drop_p, uint64_t seed, int32_t site, float* dx,
+                            float* part, void* stream) {
+    if (rows < 0 || C < 1) return fail(DADMM_EINVAL, "bad rownorm dims rows=%d C=%d", rows, C);
+    if ((C & 3) || C > 2048) return fail(DADMM_EUNSUPPORTED, "rownorm needs C %% 4 == 0, C <= 2048 (C=%d)", C);
+    if (!dy || !xd || !weight || !bias || !dx || !part) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(dy) || !aligned16(xd) || !aligned16(weight) || !aligned16(bias) || !aligned16(dx))
+        return fail(DADMM_EINVAL, "rownorm operands must be 16-byte aligned");
+    dadmm::RowNormBwdArgs a{dy, xd, weight, bias, dx, part, rows, C, act ? 1 : 0, eps, slope, drop_p,
+                            seed, site};
+    hipError_t e = dadmm::launch_rownorm_bwd(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "rownorm backward launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_hyper_head_act(int32_t mode, int32_t B, int32_t H, const float* z, const float* dhyp,
+                         float alpha_max, float tau_max, float rho_max, float eta_max, float* out,
+                         void* stream) {
+    if (B < 0 || H < 1 || (mode != 0 && mode != 1)) return fail(DADMM_EINVAL, "bad head dims/mode");
+    if (!z || !out || (mode == 1 && !dhyp)) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    const float mx[4] = {alpha_max, tau_max, rho_max, eta_max};
+    hipError_t e = dadmm::launch_head_act(mode, B, H, z, dhyp, mx, out, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "head launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;
     const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);

@@ -83,8 +83,9 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
     const int tl = xcd_tile(blockIdx.x, gridDim.x);
     const int ct = tl % gn, rt = (tl / gn) % gm, split = tl / (gn * gm);
 
+    constexpr bool GCN = EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN;
     int row0, rows_t, s0 = 0;
-    if (EPI == HYPER_EPI_GCN) {
+    if (GCN) {
         s0 = rt * a.S_t;
         const int ns = a.B - s0 < a.S_t ? a.B - s0 : a.S_t;
         row0 = s0 * a.P;
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
     }
 
     // lane (j, h) holds rows 16 (wr WR + i) + 4 h + r of column col0 + 16 (2 wcol + c) + j
-    if constexpr (EPI != HYPER_EPI_GCN) {
+    if constexpr (!GCN) {
         float* y = a.y + (size_t)split * a.split_stride;
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -254,6 +255,98 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
         const int nah = rows_t * P;                    // the tile's samples' A_hat rows
         const float* agl = a.ahat + (a.ahat_per_sample ? (size_t)s0 * P * P : 0);
         for (int i = threadIdx.x; i < nah; i += THREADS) ahs[i] = a.ahat_per_sample ? agl[i] : agl[i % (P * P)];
+        const int cols = a.N - col0 < TN ? a.N - col0 : TN;
+        if constexpr (EPI == HYPER_EPI_GCN_TRAIN) {
+            // training: BatchNorm on each sample's own statistics over its P nodes, then Dropout
+            //   pass 1: M = A_hat Z + bias (LDS mt, and saved for the backward)
+            //   pass 2: per (sample, column): mean and biased variance of leaky(M) over the P nodes
+            //   pass 3: y = Dropout((leaky(M) - mean) / sqrt(var + eps) * gamma + beta)
+            float* mt = colp + 4 * TN;                 // [TM][ZS]
+            float* smean = mt + TM * ZS;               // [S_t][TN]
+            float* srstd = smean + a.S_t * TN;         // [S_t][TN]
+            if (threadIdx.x < TN) {
+                const int col = col0 + threadIdx.x < a.N ? col0 + threadIdx.x : a.N - 1;
+                colp[threadIdx.x] = a.bias[col];
+                colp[2 * TN + threadIdx.x] = a.bn_w[col];
+                colp[3 * TN + threadIdx.x] = a.bn_b[col];
+            }
+            __syncthreads();
+            for (int task = threadIdx.x; task < rows_t * (TN / 4); task += THREADS) {
+                const int r = task / (TN / 4), c = 4 * (task - r * (TN / 4));
+                if (c >= cols) continue;
+                const int sl = r / P;
+                const float* ah = ahs + r * P;
+                const float* zc = zt + sl * P * ZS + c;
+                f32x4 v = zero;
+                for (int q = 0; q < P; ++q) {
+                    const float w = ah[q];
+                    const f32x4 z = *(const f32x4*)(zc + q * ZS);
+                    v = v + w * z;
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = v[e] + colp[c + e];
+                *(f32x4*)(mt + r * ZS + c) = v;
+                float* dst = a.save_m + (size_t)(row0 + r) * a.N + col0 + c;
+                if (c + 4 <= cols) {
+                    *(f32x4*)dst = v;
+                } else {
+                    for (int e = 0; e < cols - c; ++e) dst[e] = v[e];
+                }
+            }
+            __syncthreads();
+            const int ns = rows_t / P;
+            for (int task = threadIdx.x; task < ns * TN; task += THREADS) {
+                const int sl = task / TN, c = task - sl * TN;
+                if (c >= cols) continue;
+                const float* mc = mt + sl * P * ZS + c;
+                float sum = 0.0f;
+                for (int q = 0; q < P; ++q) {
+                    const float t = mc[q * ZS];
+                    sum += t > 0.0f ? t : t * a.slope;
+                }
+                const float mean = sum / (float)P;
+                float sq = 0.0f;
+                for (int q = 0; q < P; ++q) {
+                    const float t = mc[q * ZS];
+                    const float d = (t > 0.0f ? t : t * a.slope) - mean;
+                    sq += d * d;
+                }
+                const float var = sq / (float)P;
+                smean[sl * TN + c] = mean;
+                srstd[sl * TN + c] = 1.0f / sqrtf(var + a.bn_eps);
+                a.save_mean[(size_t)(s0 + sl) * a.N + col0 + c] = mean;
+                a.save_var[(size_t)(s0 + sl) * a.N + col0 + c] = var;
+            }
+            __syncthreads();
+            const uint32_t thr = drop_threshold(a.drop_p);
+            const float scale = a.drop_p > 0.0f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+            for (int task = threadIdx.x; task < rows_t * (TN / 4); task += THREADS) {
+                const int r = task / (TN / 4), c = 4 * (task - r * (TN / 4));
+                if (c >= cols) continue;
+                const int sl = r / P;
+                const f32x4 v = *(const f32x4*)(mt + r * ZS + c);
+                f32x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float t = v[e] > 0.0f ? v[e] : v[e] * a.slope;
+                    float u = (t - smean[sl * TN + c + e]) * srstd[sl * TN + c + e] * colp[2 * TN + c + e] +
+                              colp[3 * TN + c + e];
+                    if (a.drop_p > 0.0f) {
+                        const bool keep = drop_hash(a.seed, a.site, (uint32_t)(row0 + r),
+                                                    (uint32_t)(col0 + c + e)) >= thr;
+                        u = keep ? u * scale : 0.0f;
+                    }
+                    o[e] = u;
+                }
+                float* dst = a.y + (size_t)(row0 + r) * a.ldy + col0 + c;
+                if (c + 4 <= cols) {
+                    *(f32x4*)dst = o;
+                } else {
+                    for (int e = 0; e < cols - c; ++e) dst[e] = o[e];
+                }
+            }
+            return;
+        }
         if (threadIdx.x < TN) {
             const int col = col0 + threadIdx.x < a.N ? col0 + threadIdx.x : a.N - 1;
             const float sc = (1.0f / sqrtf(a.bn_var[col] + a.bn_eps)) * a.bn_w[col];
@@ -263,7 +356,6 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             colp[3 * TN + threadIdx.x] = a.bn_b[col];
         }
         __syncthreads();
-        const int cols = a.N - col0 < TN ? a.N - col0 : TN;
         for (int task = threadIdx.x; task < rows_t * (TN / 4); task += THREADS) {
             const int r = task / (TN / 4), c = 4 * (task - r * (TN / 4));
             if (c >= cols) continue;
@@ -312,6 +404,15 @@ __global__ __launch_bounds__(THREADS) void rownorm_kernel(RowNormArgs a) {
             // split-K partial sums of the producing linear, added in split order, then its bias
             for (int q = 1; q < a.nsum; ++q) v[u] += *(const f32x4*)(x + (size_t)q * a.sum_stride + 4 * c4);
             if (a.pre_bias != nullptr) v[u] += *(const f32x4*)(a.pre_bias + 4 * c4);
+            if (a.drop_p > 0.0f) {   // training: Dropout on the LayerNorm input (:94-104)
+                const uint32_t thr = drop_threshold(a.drop_p);
+                const float scale = 1.0f / (1.0f - a.drop_p);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    v[u][e] = drop_hash(a.seed, a.site, (uint32_t)row, (uint32_t)(4 * c4 + e)) >= thr
+                                  ? v[u][e] * scale : 0.0f;
+            }
+            if (a.xd != nullptr) *(f32x4*)(a.xd + (size_t)row * a.C + 4 * c4) = v[u];
         }
         s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
     }
@@ -354,8 +455,9 @@ __global__ __launch_bounds__(THREADS) void rownorm_kernel(RowNormArgs a) {
 template <int WR, int EPI, bool SPLIT>
 hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
     size_t lds = 0;
-    if (EPI == HYPER_EPI_GCN) {
+    if (EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN) {
         lds = 4 * ((size_t)32 * WR * ZS + (size_t)a.S_t * a.P * a.P + 4 * TN);
+        if (EPI == HYPER_EPI_GCN_TRAIN) lds += 4 * ((size_t)32 * WR * ZS + 2 * (size_t)a.S_t * TN);
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void*)linear_kernel<WR, EPI, SPLIT>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -387,8 +489,9 @@ hipError_t launch_epi(int wr, int grid, const HyperArgs& a, hipStream_t st) {
 // Row tiling: the largest tile (32 WR rows; whole samples of P rows for the GCN epilogue) that
 // still gives ~two workgroups per CU; smaller tiles for small batches.
 static int pick_tiles(HyperArgs& a, int epi) {
-    const int unit = epi == HYPER_EPI_GCN ? a.P : 1;          // rows per tiling unit
-    const int units = epi == HYPER_EPI_GCN ? a.B : a.rows;
+    const bool gcn = epi == HYPER_EPI_GCN || epi == HYPER_EPI_GCN_TRAIN;
+    const int unit = gcn ? a.P : 1;                             // rows per tiling unit
+    const int units = gcn ? a.B : a.rows;
     a.gn = (a.N + hyper::TN - 1) / hyper::TN;
     int wr = 0;
     for (int cand = 4; cand >= 1; cand >>= 1) {
@@ -426,7 +529,7 @@ static int pick_split_tiles(HyperArgs& a, int K, int& splits) {
 }
 
 hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st) {
-    const int units = epi == HYPER_EPI_GCN ? a.B : a.rows;
+    const int units = (epi == HYPER_EPI_GCN || epi == HYPER_EPI_GCN_TRAIN) ? a.B : a.rows;
     if (units <= 0 || a.N <= 0) return hipSuccess;
     if (a.K1 < a.K && (a.K1 & 15)) return hipErrorInvalidValue;
     int wr = 0;
@@ -444,6 +547,7 @@ hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st) {
         case HYPER_EPI_BIAS: return hyper::launch_epi<HYPER_EPI_BIAS>(wr, grid, a, st);
         case HYPER_EPI_GCN: return hyper::launch_epi<HYPER_EPI_GCN>(wr, grid, a, st);
         case HYPER_EPI_HEAD: return hyper::launch_epi<HYPER_EPI_HEAD>(wr, grid, a, st);
+        case HYPER_EPI_GCN_TRAIN: return hyper::launch_epi<HYPER_EPI_GCN_TRAIN>(wr, grid, a, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -1,0 +1,261 @@
+// dadmm_hyper_train.hip — training-mode backward of the GNN hypernetwork of
+// DLASSO_GNNHyp3_Progressive (gnn_dlasso_models_progressive.py:9-72 GNNHypernetwork3, :93-123
+// decoder / fc, :165-196 head), everything but the plain GEMMs:
+//   gcn_bwd_kernel    : one GCN block  Dropout(BN_batch(leaky(A_hat Z + bias)))  from dy to dZ,
+//                       with per-sample partial sums of dgamma, dbeta, dbias;
+//   rownorm_bwd_kernel: LayerNorm (+ LeakyReLU) rows from dy to dx (through the decoder's
+//                       Dropout when it has one), with per-block partial sums of dweight, dbias;
+//   head_act_kernel   : the hyper-parameter head (sigmoid, clamps, maxima) forward and backward.
+// The forward kernels are the train epilogues of dadmm_hyper.hip (HYPER_EPI_GCN_TRAIN and the
+// rownorm dropout); the dropout masks are regenerated here from the same counter-based stream
+// (drop_hash), never stored. The weight / input gradients of the linears (dW = dZ^T X,
+// dX = dZ W) are plain GEMMs and run on hipBLASLt through torch.matmul (dadmm_hip/hyper_ops.py).
+//
+// Every formula is the derivative torch's autograd applies to the reference's modules:
+//   Dropout: dx = dy * keep / (1 - p);   leaky_relu: dx = dy * (x > 0 ? 1 : slope);
+//   BatchNorm (batch statistics of the P nodes of a sample, biased variance):
+//     dx = gamma rstd (dxn - mean(dxn) - xhat mean(dxn xhat)),  dgamma = sum dxn xhat, dbeta = sum dxn;
+//   LayerNorm over C columns: the same with the row's statistics and per-column affine;
+//   clamp(x, lo, hi): dx = dy * (lo <= x <= hi);  sigmoid: dx = dy * s (1 - s).
+// Sums run in fixed orders (deterministic); results agree with torch to f32 rounding.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dadmm_internal.h"
+
+namespace dadmm {
+namespace hyper_train {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int THREADS = 256;
+constexpr int CB = 64;   // columns per gcn_bwd workgroup
+
+// One workgroup per (sample, 64 columns). LDS: M, then dM [P][CB]; A_hat block [P][P].
+__global__ __launch_bounds__(THREADS) void gcn_bwd_kernel(GcnBwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int P = a.P, N = a.N;
+    const int ncb = (N + CB - 1) / CB;
+    const int s = blockIdx.x / ncb, c0 = (blockIdx.x % ncb) * CB;
+    float* dm = lds;                 // [P][CB]
+    float* ah = dm + P * CB;         // [P][P]
+    const float* ahg = a.ahat + (a.ahat_per_sample ? (size_t)s * P * P : 0);
+    for (int i = threadIdx.x; i < P * P; i += THREADS) ah[i] = ahg[i];
+    const size_t row0 = (size_t)s * P;
+    const uint32_t thr = drop_threshold(a.drop_p);
+    const float scale = a.drop_p > 0.0f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+    if (threadIdx.x < CB && c0 + (int)threadIdx.x < N) {
+        const int c = c0 + threadIdx.x;
+        const float mean = a.mean[(size_t)s * N + c];
+        const float rstd = 1.0f / sqrtf(a.var[(size_t)s * N + c] + a.eps);
+        const float gam = a.gamma[c];
+        // pass 1: dxn = dropout'(dy), the two BatchNorm sums
+        float sb = 0.0f, sg = 0.0f;
+        for (int p = 0; p < P; ++p) {
+            const size_t o = (row0 + p) * N + c;
+            const float mv = a.m[o];
+            const float t = mv > 0.0f ? mv : mv * a.slope;
+            const float xh = (t - mean) * rstd;
+            float g = a.dy[o];
+            if (a.drop_p > 0.0f)
+                g = drop_hash(a.seed, a.site, (uint32_t)(row0 + p), (uint32_t)c) >= thr ? g * scale : 0.0f;
+            sb += g;
+            sg += g * xh;
+            dm[p * CB + threadIdx.x] = g;
+        }
+        // pass 2: BatchNorm and leaky_relu backward -> dM
+        const float inv = 1.0f / (float)P;
+        float sbias = 0.0f;
+        for (int p = 0; p < P; ++p) {
+            const size_t o = (row0 + p) * N + c;
+            const float mv = a.m[o];
+            const float t = mv > 0.0f ? mv : mv * a.slope;
+            const float xh = (t - mean) * rstd;
+            const float g = dm[p * CB + threadIdx.x];
+            const float dt = gam * rstd * (g - sb * inv - xh * (sg * inv));
+            const float d = mv > 0.0f ? dt : dt * a.slope;
+            sbias += d;
+            dm[p * CB + threadIdx.x] = d;
+        }
+        a.part[(size_t)s * N + c] = sg;                          // dgamma
+        a.part[((size_t)a.B + s) * N + c] = sb;                  // dbeta
+        a.part[((size_t)2 * a.B + s) * N + c] = sbias;           // dbias (GCNConv.bias)
+    }
+    __syncthreads();
+    // dZ[q] = sum_p A_hat[p][q] dM[p]  (the mix M = A_hat Z, transposed)
+    const int cols = N - c0 < CB ? N - c0 : CB;
+    for (int task = threadIdx.x; task < P * CB; task += THREADS) {
+        const int q = task / CB, c = task - q * CB;
+        if (c >= cols) continue;
+        float acc = 0.0f;
+        for (int p = 0; p < P; ++p) acc += ah[p * P + q] * dm[p * CB + c];
+        a.dz[(row0 + q) * N + c0 + c] = acc;
+    }
+}
+
+// One wave per row, ROWNORM_BWD_ROWS rows per workgroup (16 per wave); per-lane column partials
+// of dweight / dbias are combined across the 4 waves in LDS in wave order (deterministic).
+constexpr int CH = 8;   // C <= 64 * 4 * CH
+__global__ __launch_bounds__(THREADS) void rownorm_bwd_kernel(RowNormBwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float red[4][2][2048];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int C = a.C, C4 = C / 4;
+    f32x4 pw[CH], pb[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) pw[u] = pb[u] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    const uint32_t thr = drop_threshold(a.drop_p);
+    const float scale = a.drop_p > 0.0f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+    const float invC = 1.0f / (float)C;
+    constexpr int RPW = ROWNORM_BWD_ROWS / 4;
+    for (int i = 0; i < RPW; ++i) {
+        const int row = blockIdx.x * ROWNORM_BWD_ROWS + w * RPW + i;
+        if (row >= a.rows) break;
+        const float* x = a.xd + (size_t)row * C;
+        const float* dy = a.dy + (size_t)row * C;
+        f32x4 v[CH], g[CH];
+        float s = 0.0f;
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int c4 = lane + 64 * u;
+            v[u] = c4 < C4 ? *(const f32x4*)(x + 4 * c4) : (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+            s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        const float mean = s * invC;
+        float q = 0.0f;
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int c4 = lane + 64 * u;
+            if (c4 < C4) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float d = v[u][e] - mean;
+                    q += d * d;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+        const float rstd = 1.0f / sqrtf(q * invC + a.eps);
+        // xhat, dt (through the LeakyReLU), the affine partials, dxhat and its two row sums
+        float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int c4 = lane + 64 * u;
+            if (c4 >= C4) continue;
+            const f32x4 wv = *(const f32x4*)(a.weight + 4 * c4);
+            const f32x4 bv = *(const f32x4*)(a.bias + 4 * c4);
+            const f32x4 dv = *(const f32x4*)(dy + 4 * c4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float xh = (v[u][e] - mean) * rstd;
+                float dt = dv[e];
+                if (a.act) {
+                    const float t = xh * wv[e] + bv[e];
+                    dt = t > 0.0f ? dt : dt * a.slope;
+                }
+                pw[u][e] += dt * xh;
+                pb[u][e] += dt;
+                const float dxh = dt * wv[e];
+                s1 += dxh;
+                s2 += dxh * xh;
+                v[u][e] = xh;
+                g[u][e] = dxh;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            s1 += __shfl_xor(s1, o);
+            s2 += __shfl_xor(s2, o);
+        }
+        const float m1 = s1 * invC, m2 = s2 * invC;
+        float* dx = a.dx + (size_t)row * C;
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int c4 = lane + 64 * u;
+            if (c4 >= C4) continue;
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float d = rstd * (g[u][e] - m1 - v[u][e] * m2);
+                if (a.drop_p > 0.0f)
+                    d = drop_hash(a.seed, a.site, (uint32_t)row, (uint32_t)(4 * c4 + e)) >= thr ? d * scale : 0.0f;
+                o[e] = d;
+            }
+            *(f32x4*)(dx + 4 * c4) = o;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        const int c4 = lane + 64 * u;
+        if (c4 < C4) {
+            *(f32x4*)(&red[w][0][4 * c4]) = pw[u];
+            *(f32x4*)(&red[w][1][4 * c4]) = pb[u];
+        }
+    }
+    __syncthreads();
+    float* part = a.part + (size_t)blockIdx.x * 2 * C;
+    for (int i = threadIdx.x; i < 2 * C; i += THREADS) {
+        const int k = i / C, c = i - k * C;
+        part[i] = ((red[0][k][c] + red[1][k][c]) + red[2][k][c]) + red[3][k][c];
+    }
+}
+
+// mode 0: out = hyp = head(z); mode 1: out = dz = dhyp * head'(z). Element (b, i) of [B][4H],
+// channel c = i / H (the reference's h.view(B, 4, H)):
+//   s = sigmoid(z); u = clamp(s, 1e-4, 0.9999); v = u * max_c; hyp = c > 0 ? min(v, 0.9999) : v
+__global__ __launch_bounds__(THREADS) void head_act_kernel(int mode, int B, int H, const float* z,
+                                                           const float* dhyp, float m0, float m1,
+                                                           float m2, float m3, float* out) {
+    const int idx = blockIdx.x * THREADS + threadIdx.x;
+    if (idx >= B * 4 * H) return;
+    const int c = (idx % (4 * H)) / H;
+    const float mx = c == 0 ? m0 : (c == 1 ? m1 : (c == 2 ? m2 : m3));
+    const float s = 1.0f / (1.0f + expf(-z[idx]));
+    const float u = fminf(fmaxf(s, 1e-4f), 0.9999f);
+    const float v = u * mx;
+    if (mode == 0) {
+        out[idx] = c > 0 ? fminf(v, 0.9999f) : v;
+        return;
+    }
+    float g = dhyp[idx];
+    if (c > 0 && !(v <= 0.9999f)) g = 0.0f;           // clamp(max=0.9999)
+    g = g * mx;
+    if (!(s >= 1e-4f && s <= 0.9999f)) g = 0.0f;      // clamp(1e-4, 0.9999)
+    out[idx] = g * ((1.0f - s) * s);                   // sigmoid
+}
+
+}  // namespace hyper_train
+
+hipError_t launch_gcn_bwd(const GcnBwdArgs& a, hipStream_t st) {
+    if (a.B <= 0 || a.N <= 0) return hipSuccess;
+    const size_t lds = 4 * ((size_t)a.P * hyper_train::CB + (size_t)a.P * a.P);
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)hyper_train::gcn_bwd_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    const int ncb = (a.N + hyper_train::CB - 1) / hyper_train::CB;
+    hipLaunchKernelGGL(hyper_train::gcn_bwd_kernel, dim3(a.B * ncb), dim3(hyper_train::THREADS), lds, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rownorm_bwd(const RowNormBwdArgs& a, hipStream_t st) {
+    if (a.rows <= 0) return hipSuccess;
+    const int nblk = (a.rows + ROWNORM_BWD_ROWS - 1) / ROWNORM_BWD_ROWS;
+    hipLaunchKernelGGL(hyper_train::rownorm_bwd_kernel, dim3(nblk), dim3(hyper_train::THREADS), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_head_act(int mode, int B, int H, const float* z, const float* dhyp, const float* maxv4,
+                           float* out, hipStream_t st) {
+    const int n = B * 4 * H;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(hyper_train::head_act_kernel, dim3((n + hyper_train::THREADS - 1) / hyper_train::THREADS),
+                       dim3(hyper_train::THREADS), 0, st, mode, B, H, z, dhyp, maxv4[0], maxv4[1],
+                       maxv4[2], maxv4[3], out);
+    return hipGetLastError();
+}
+
+}  // namespace dadmm

@@ -188,6 +188,8 @@ hipError_t launch_loss_grad(const LossArgs& a, const float* gout, float* dY, hip
 #define HYPER_EPI_BIAS 0   // y = x W^T + bias
 #define HYPER_EPI_GCN 1    // y = BN(leaky(A_hat (x W^T) + bias)) per sample of P rows
 #define HYPER_EPI_HEAD 2   // y = min(clamp(sigmoid(x W^T + bias), 1e-4, 0.9999) * max_c, ...)
+#define HYPER_EPI_GCN_TRAIN 3   // y = Dropout(BN_batch(leaky(A_hat (x W^T) + bias))) per sample,
+                                //     saving M = A_hat (x W^T) + bias and the samples' BN statistics
 struct HyperArgs {
     const float* x1;        // input columns [0, K1): row r at x1 + r * ld1
     const float* x2;        // input columns [K1, K): row r at x2 + r * ld2 (nullable if K1 == K)
@@ -210,7 +212,30 @@ struct HyperArgs {
     int splits;             // BIAS: split-K factor; split q writes y + q * split_stride (no bias)
     size_t split_stride;
     int gm, gn;             // tile grid (set by the launcher)
+    // GCN_TRAIN: saved activations and the dropout stream
+    float* save_m;          // [rows][N] M = A_hat (x W^T) + bias (pre-activation)
+    float* save_mean;       // [B][N] per-sample BatchNorm batch mean over the P nodes
+    float* save_var;        // [B][N] per-sample biased batch variance
+    float drop_p;           // dropout probability (0: none)
+    uint64_t seed;          // dropout stream: keep(site, row, col) = hash(seed, site, row, col) >= p
+    int site;
 };
+
+// Counter-based dropout mask shared by the training forward and backward kernels (the backward
+// regenerates it instead of storing it): keep element (row, col) of dropout site `site` iff
+// hash(seed, site, row, col) >= p * 2^32; kept elements are scaled by 1 / (1 - p) (nn.Dropout).
+__host__ __device__ inline uint32_t drop_hash(uint64_t seed, int site, uint32_t row, uint32_t col) {
+    uint64_t z = seed ^ ((uint64_t)(uint32_t)site << 56) ^ ((uint64_t)row << 20) ^ (uint64_t)col;
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (uint32_t)(z >> 32);
+}
+__host__ __device__ inline uint32_t drop_threshold(float p) {
+    const double t = (double)p * 4294967296.0;
+    return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
 hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st);
 int hyper_linear_splits(int rows, int K, int N);
 struct RowNormArgs {
@@ -223,7 +248,50 @@ struct RowNormArgs {
     int nsum;               // split-K partials summed (in order) before the LayerNorm
     size_t sum_stride;
     const float* pre_bias;  // nullable: the producing linear's bias, added after the sum
+    // training: dropout on the LayerNorm input (decoder: Linear -> Dropout -> LayerNorm), and the
+    // post-dropout LayerNorm input saved for the backward (xd, nullable)
+    float drop_p;
+    uint64_t seed;
+    int site;
+    float* xd;
 };
+// LayerNorm (+ LeakyReLU) backward of rownorm rows: dx (w.r.t. the pre-dropout input when
+// drop_p > 0) and per-block partial sums of dweight / dbias ([nblk][2][C], nblk = ceil(rows / 64))
+struct RowNormBwdArgs {
+    const float* dy;        // [rows][C]
+    const float* xd;        // [rows][C] LayerNorm input (post-dropout)
+    const float* weight;
+    const float* bias;
+    float* dx;              // [rows][C]
+    float* part;            // [nblk][2][C]
+    int rows, C, act;
+    float eps, slope, drop_p;
+    uint64_t seed;
+    int site;
+};
+hipError_t launch_rownorm_bwd(const RowNormBwdArgs& a, hipStream_t st);
+constexpr int ROWNORM_BWD_ROWS = 64;   // rows per partial-sum block
+// GCN layer (train mode) backward, everything but the two GEMMs: from dy (w.r.t. the layer's
+// dropout output) to dZ (w.r.t. Z = x W^T), with per-sample partials of dgamma, dbeta, dbias
+struct GcnBwdArgs {
+    const float* dy;        // [B*P][N]
+    const float* m;         // [B*P][N] saved M
+    const float* mean;      // [B][N]
+    const float* var;       // [B][N]
+    const float* gamma;     // [N]
+    const float* ahat;      // [B or 1][P][P]
+    int ahat_per_sample;
+    float* dz;              // [B*P][N]
+    float* part;            // [3][B][N]: dgamma, dbeta, dbias per sample
+    int B, P, N;
+    float eps, slope, drop_p;
+    uint64_t seed;
+    int site;
+};
+hipError_t launch_gcn_bwd(const GcnBwdArgs& a, hipStream_t st);
+// hyper-parameter head: mode 0: hyp = head(z); mode 1: dz = dhyp * head'(z); z, hyp, dhyp [B][4H]
+hipError_t launch_head_act(int mode, int B, int H, const float* z, const float* dhyp, const float* maxv4,
+                           float* out, hipStream_t st);
 hipError_t launch_rownorm(const RowNormArgs& a, hipStream_t st);
 
 // ---- device-side ER graph generation (dadmm_graphgen.hip) ---------------------------------------

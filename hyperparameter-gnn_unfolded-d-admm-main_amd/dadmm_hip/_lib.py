@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -40,6 +40,12 @@ EXPORTED_SYMBOLS = (
     "dadmm_hyper_head",
     "dadmm_hyper_linear_ln_scratch_bytes",
     "dadmm_hyper_linear_ln",
+    "dadmm_hyper_gcn_train",
+    "dadmm_hyper_gcn_train_bwd",
+    "dadmm_hyper_linear_ln_train",
+    "dadmm_hyper_rownorm_bwd_part_bytes",
+    "dadmm_hyper_rownorm_bwd",
+    "dadmm_hyper_head_act",
     "dadmm_gnn_flag_bytes",
     "dadmm_gnn_begin",
     "dadmm_gnn_gram",
@@ -153,6 +159,21 @@ def load() -> ctypes.CDLL:
         f.argtypes = args
     L.dadmm_hyper_linear_ln_scratch_bytes.restype = ctypes.c_size_t
     L.dadmm_hyper_linear_ln_scratch_bytes.argtypes = [i32, i32, i32]
+    # training mode (model.train()): forward with dropout / batch statistics, and the backward
+    for name, args in (("dadmm_hyper_gcn_train", [i32] * 4 + [vp, i32, i32, vp, i32] + [vp] * 3 + [i32]
+                        + [vp, vp, f32, f32, f32, u64, i32, vp, i32, vp, vp, vp, vp]),
+                       ("dadmm_hyper_gcn_train_bwd", [i32] * 3 + [vp] * 5 + [f32, vp, i32, f32, f32, u64,
+                                                                          i32, vp, vp, vp]),
+                       ("dadmm_hyper_linear_ln_train", [i32, i32, i32, vp, i32, vp, vp, vp, vp, f32, i32,
+                                                        f32, f32, u64, i32, vp, vp, vp, vp]),
+                       ("dadmm_hyper_rownorm_bwd", [i32, i32, vp, vp, vp, vp, f32, i32, f32, f32, u64,
+                                                    i32, vp, vp, vp]),
+                       ("dadmm_hyper_head_act", [i32, i32, i32, vp, vp] + [f32] * 4 + [vp, vp])):
+        f = getattr(L, name)
+        f.restype = ctypes.c_int
+        f.argtypes = args
+    L.dadmm_hyper_rownorm_bwd_part_bytes.restype = ctypes.c_size_t
+    L.dadmm_hyper_rownorm_bwd_part_bytes.argtypes = [i32, i32]
     v = L.dadmm_abi_version()
     if v != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {v}, expected {ABI_VERSION}")

@@ -105,3 +105,224 @@ def hypernetwork_eval(model, AtAy, Atb, n, ahat, per_sample, bufs: HyperBuffers)
             float(model.eta_max), _ptr(bufs.hyp), stream))
     h = bufs.hyp
     return tuple(h[:, c].view(B, H, 1, 1) for c in range(4))
+
+
+# ---- training mode (model.train()) ------------------------------------------------------------
+
+def supported_train(model, n: int) -> bool:
+    """Whether the training-mode hypernetwork can run on the HIP kernels: train mode, the
+    standard modules of the reference (Dropout, BatchNorm1d with affine + running statistics,
+    LayerNorm), P >= 2 (batch statistics over the nodes) and 4-aligned feature widths."""
+    if not model.training or model.P < 2:
+        return False
+    enc = model.encoder
+    bns = (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)
+    if any(not (bn.affine and bn.track_running_stats and bn.momentum is not None) for bn in bns):
+        return False
+    drops = [enc.dropout] + [model.decoder[i] for i in (1, 5, 9)]
+    if any(not isinstance(d, nn.Dropout) for d in drops):
+        return False
+    lns = [enc.norm] + [model.decoder[i] for i in (2, 6, 10)]
+    if any(not isinstance(ln, nn.LayerNorm) or not ln.elementwise_affine or len(ln.normalized_shape) != 1
+           or ln.normalized_shape[0] > 2048 for ln in lns):
+        return False
+    widths = [n, enc.conv1.lin.out_features, enc.conv2.lin.out_features, enc.conv3.lin.out_features,
+              enc.conv5.lin.out_features, model.decoder[0].out_features, model.decoder[4].out_features,
+              model.decoder[8].out_features]
+    return all(w % 4 == 0 for w in widths)
+
+
+def _hyper_params(model):
+    """The hypernetwork's parameters in the order HyperTrainFn takes them."""
+    enc = model.encoder
+    out = []
+    for conv, bn in zip((enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5),
+                        (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)):
+        out += [conv.lin.weight, conv.bias, bn.weight, bn.bias]
+    out += [enc.norm.weight, enc.norm.bias]
+    for blk in range(3):
+        lin, ln = model.decoder[4 * blk], model.decoder[4 * blk + 2]
+        out += [lin.weight, lin.bias, ln.weight, ln.bias]
+    out += [model.fc.weight, model.fc.bias]
+    return out
+
+
+def _update_running_stats(bn, mean, var, P):
+    """bn's running statistics after the reference's B sequential per-sample calls (train mode),
+    in closed form: r <- (1 - m) r + m s_b for b = 0 .. B-1 (unbiased variance)."""
+    B = mean.shape[0]
+    m = bn.momentum
+    w = m * (1.0 - m) ** torch.arange(B - 1, -1, -1, device=mean.device, dtype=torch.float64)
+    decay = (1.0 - m) ** B
+    bn.running_mean.copy_((decay * bn.running_mean.double() + w @ mean.double()).float())
+    bn.running_var.copy_((decay * bn.running_var.double() + w @ (var.double() * (P / (P - 1)))).float())
+    bn.num_batches_tracked += B
+
+
+class HyperTrainFn(torch.autograd.Function):
+    """hyp_k [B, 4, H] = the training-mode hypernetwork of one iteration
+    (gnn_dlasso_models_progressive.py:165-196 with :52-72 in train mode) on the HIP kernels;
+    differentiable w.r.t. AtAy_k and every hypernetwork parameter. Forward: the GCN layers as
+    f32 MFMA GEMMs with the mix / leaky_relu / batch-statistics BatchNorm / Dropout epilogue
+    (dadmm_hyper_gcn_train), LayerNorm, the decoder blocks (dadmm_hyper_linear_ln_train) and the
+    head. Backward: dadmm_hyper_head_act / dadmm_hyper_rownorm_bwd / dadmm_hyper_gcn_train_bwd
+    for everything but the linears' plain GEMMs (dW = dZ^T X, dX = dZ W: hipBLASLt via torch)."""
+
+    @staticmethod
+    def forward(ctx, AtAy, Atb, ahat, model, n, per_sample, seed, *params):
+        L = _lib.load()
+        B, P, ns = AtAy.shape
+        dev = AtAy.device
+        stream = _stream(dev)
+        enc = model.encoder
+        convs = (enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5)
+        bns = (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)
+        p_enc = float(enc.dropout.p)
+        rows = B * P
+        if n % 16 == 0:   # cat(AtAy, Atb) (:165) read in place
+            x1, ld1, K1, x2, ld2, K = AtAy, ns, n, Atb, ns, 2 * n
+        else:
+            xc = torch.cat([AtAy[..., :n], Atb[..., :n]], dim=2).reshape(rows, 2 * n).contiguous()
+            x1, ld1, K1, x2, ld2, K = xc, 2 * n, 2 * n, None, 0, 2 * n
+        saved = []          # per GCN layer: (M, mean, var)
+        xs = []             # per GCN layer: its input rows (None for layer 1: rebuilt from AtAy / Atb)
+        with torch.cuda.device(dev):
+            for i, (conv, bn) in enumerate(zip(convs, bns)):
+                N = conv.lin.out_features
+                y = torch.empty((rows, N), device=dev)
+                M = torch.empty((rows, N), device=dev)
+                mean = torch.empty((B, N), device=dev)
+                var = torch.empty((B, N), device=dev)
+                _lib.check("dadmm_hyper_gcn_train", L.dadmm_hyper_gcn_train(
+                    B, P, K, N, _ptr(x1), ld1, K1, _ptr(x2), ld2, _ptr(conv.lin.weight),
+                    _ptr(conv.bias), _ptr(ahat), int(per_sample), _ptr(bn.weight), _ptr(bn.bias),
+                    float(bn.eps), LEAKY_SLOPE, p_enc if i < 4 else 0.0, seed, i, _ptr(y), N, _ptr(M),
+                    _ptr(mean), _ptr(var), stream))
+                with torch.no_grad():
+                    _update_running_stats(bn, mean, var, P)
+                saved.append((M, mean, var))
+                xs.append(None if i == 0 else x1)
+                x1, ld1, K1, x2, ld2, K = y, N, N, None, 0, N
+            # self.norm (:69) over 4h per node, then the flattened decoder input
+            ln = enc.norm
+            x5 = x1
+            e = torch.empty_like(x5)
+            _lib.check("dadmm_hyper_rownorm", L.dadmm_hyper_rownorm(
+                rows, K, _ptr(x5), _ptr(ln.weight), _ptr(ln.bias), float(ln.eps), 0, 0.0, _ptr(e), stream))
+            x, width = e.view(B, P * K), P * K
+            dec_in, dec_xd = [], []
+            for blk in range(3):
+                lin, lnd = model.decoder[4 * blk], model.decoder[4 * blk + 2]
+                N = lin.out_features
+                out = torch.empty((B, N), device=dev)
+                xd = torch.empty((B, N), device=dev)
+                scratch = torch.empty(max(L.dadmm_hyper_linear_ln_scratch_bytes(B, width, N), 16) // 4,
+                                      device=dev)
+                _lib.check("dadmm_hyper_linear_ln_train", L.dadmm_hyper_linear_ln_train(
+                    B, width, N, _ptr(x), width, _ptr(lin.weight), _ptr(lin.bias), _ptr(lnd.weight),
+                    _ptr(lnd.bias), float(lnd.eps), 1, float(model.decoder[4 * blk + 3].negative_slope),
+                    float(model.decoder[4 * blk + 1].p), seed, 4 + blk, _ptr(out), _ptr(xd),
+                    _ptr(scratch), stream))
+                dec_in.append(x)
+                dec_xd.append(xd)
+                x, width = out, N
+            H = model.fc.out_features // 4
+            z = torch.empty((B, 4 * H), device=dev)
+            _lib.check("dadmm_hyper_linear", L.dadmm_hyper_linear(
+                B, width, 4 * H, _ptr(x), width, width, None, 0, _ptr(model.fc.weight),
+                _ptr(model.fc.bias), _ptr(z), 4 * H, stream))
+            hyp = torch.empty((B, 4, H), device=dev)
+            mx = [float(model.alpha_max), float(model.tau_max), float(model.rho_max), float(model.eta_max)]
+            _lib.check("dadmm_hyper_head_act", L.dadmm_hyper_head_act(
+                0, B, H, _ptr(z), None, *mx, _ptr(hyp), stream))
+        ctx.model, ctx.n, ctx.per_sample, ctx.seed, ctx.mx = model, n, per_sample, seed, mx
+        ctx.saved = saved
+        ctx.xs, ctx.x5, ctx.dec_in, ctx.dec_xd, ctx.x3, ctx.z = xs, x5, dec_in, dec_xd, x, z
+        ctx.AtAy, ctx.Atb, ctx.ahat = AtAy, Atb, ahat
+        return hyp
+
+    @staticmethod
+    def backward(ctx, dhyp):
+        L = _lib.load()
+        model, n = ctx.model, ctx.n
+        AtAy, Atb = ctx.AtAy, ctx.Atb
+        B, P, ns = AtAy.shape
+        rows = B * P
+        dev = AtAy.device
+        stream = _stream(dev)
+        enc = model.encoder
+        convs = (enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5)
+        bns = (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)
+        p_enc = float(enc.dropout.p)
+        H = model.fc.out_features // 4
+        g = {}
+        with torch.cuda.device(dev):
+            dhyp = dhyp.contiguous()
+            dz = torch.empty((B, 4 * H), device=dev)
+            _lib.check("dadmm_hyper_head_act", L.dadmm_hyper_head_act(
+                1, B, H, _ptr(ctx.z), _ptr(dhyp), *ctx.mx, _ptr(dz), stream))
+            g["fc.w"] = dz.t() @ ctx.x3
+            g["fc.b"] = dz.sum(0)
+            dx = dz @ model.fc.weight
+            for blk in (2, 1, 0):
+                lin, lnd = model.decoder[4 * blk], model.decoder[4 * blk + 2]
+                N = lin.out_features
+                dv = torch.empty((B, N), device=dev)
+                part = torch.empty(max(L.dadmm_hyper_rownorm_bwd_part_bytes(B, N), 16) // 4, device=dev)
+                _lib.check("dadmm_hyper_rownorm_bwd", L.dadmm_hyper_rownorm_bwd(
+                    B, N, _ptr(dx.contiguous()), _ptr(ctx.dec_xd[blk]), _ptr(lnd.weight), _ptr(lnd.bias),
+                    float(lnd.eps), 1, float(model.decoder[4 * blk + 3].negative_slope),
+                    float(model.decoder[4 * blk + 1].p), ctx.seed, 4 + blk, _ptr(dv), _ptr(part), stream))
+                pw = part[:(B + 63) // 64 * 2 * N].view(-1, 2, N).sum(0)
+                g[f"ln{blk}.w"], g[f"ln{blk}.b"] = pw[0], pw[1]
+                g[f"lin{blk}.w"] = dv.t() @ ctx.dec_in[blk]
+                g[f"lin{blk}.b"] = dv.sum(0)
+                dx = dv @ lin.weight
+            # self.norm backward (no dropout, no activation): input x5 [rows, 4h]
+            C = ctx.x5.shape[1]
+            dx = dx.reshape(rows, C).contiguous()
+            de = torch.empty((rows, C), device=dev)
+            part = torch.empty(max(L.dadmm_hyper_rownorm_bwd_part_bytes(rows, C), 16) // 4, device=dev)
+            ln = enc.norm
+            _lib.check("dadmm_hyper_rownorm_bwd", L.dadmm_hyper_rownorm_bwd(
+                rows, C, _ptr(dx), _ptr(ctx.x5), _ptr(ln.weight), _ptr(ln.bias), float(ln.eps), 0, 0.0,
+                0.0, ctx.seed, 99, _ptr(de), _ptr(part), stream))
+            pw = part[:(rows + 63) // 64 * 2 * C].view(-1, 2, C).sum(0)
+            g["norm.w"], g["norm.b"] = pw[0], pw[1]
+            dx = de
+            for i in (4, 3, 2, 1, 0):
+                conv, bn = convs[i], bns[i]
+                N = conv.lin.out_features
+                M, mean, var = ctx.saved[i]
+                dZ = torch.empty((rows, N), device=dev)
+                part = torch.empty((3, B, N), device=dev)
+                _lib.check("dadmm_hyper_gcn_train_bwd", L.dadmm_hyper_gcn_train_bwd(
+                    B, P, N, _ptr(dx.contiguous()), _ptr(M), _ptr(mean), _ptr(var), _ptr(bn.weight),
+                    float(bn.eps), _ptr(ctx.ahat), int(ctx.per_sample), LEAKY_SLOPE,
+                    p_enc if i < 4 else 0.0, ctx.seed, i, _ptr(dZ), _ptr(part), stream))
+                ps = part.sum(1)
+                g[f"bn{i}.w"], g[f"bn{i}.b"], g[f"conv{i}.b"] = ps[0], ps[1], ps[2]
+                xin = ctx.xs[i]
+                if xin is None:
+                    xin = torch.cat([AtAy[..., :n], Atb[..., :n]], dim=2).reshape(rows, 2 * n)
+                g[f"conv{i}.w"] = dZ.t() @ xin
+                dx = dZ @ conv.lin.weight
+            dAtAy = torch.zeros_like(AtAy)
+            dAtAy[..., :n] = dx.reshape(B, P, 2 * n)[..., :n]
+        grads = []
+        for i in range(5):
+            grads += [g[f"conv{i}.w"], g[f"conv{i}.b"], g[f"bn{i}.w"], g[f"bn{i}.b"]]
+        grads += [g["norm.w"], g["norm.b"]]
+        for blk in range(3):
+            grads += [g[f"lin{blk}.w"], g[f"lin{blk}.b"], g[f"ln{blk}.w"], g[f"ln{blk}.b"]]
+        grads += [g["fc.w"], g["fc.b"]]
+        ctx.saved = ctx.xs = ctx.dec_in = ctx.dec_xd = None
+        return (dAtAy, None, None, None, None, None, None, *grads)
+
+
+def hypernetwork_train(model, AtAy, Atb, n, ahat, per_sample, seed=None):
+    """hyp_k [B, 4, H] of one iteration in training mode (HyperTrainFn); ``seed`` names the
+    dropout stream (default: drawn from torch's CPU generator, so torch.manual_seed fixes it)."""
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    return HyperTrainFn.apply(AtAy, Atb, ahat, model, n, per_sample, seed, *_hyper_params(model))

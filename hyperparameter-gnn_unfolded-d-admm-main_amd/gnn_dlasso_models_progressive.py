@@ -14,7 +14,10 @@ library one iteration at a time (``dadmm_hip.gnn_ops``). The hypernetwork betwee
 runs over all B per-sample graphs at once (the reference loops over samples in Python, :37-40):
 in inference (model.eval() under no_grad) on the fused HIP kernels of ``dadmm_hip.hyper_ops``
 (f32 MFMA GEMMs with the adjacency mix, leaky_relu and BatchNorm in their epilogues); in training
-(autograd, Dropout, per-sample BatchNorm statistics) as batched torch with hipBLASLt GEMMs.
+(model.train(): Dropout, per-sample BatchNorm batch statistics, autograd) on the training kernels
+(``hyper_ops.HyperTrainFn``: the same GEMMs with train epilogues, and HIP backward kernels for
+everything but the linears' plain weight / input GEMMs, which run on hipBLASLt).
+``hyper_backend = "torch"`` selects the batched torch composition below instead (tests).
 
 GCNConv (torch_geometric; absent here, unpinned version) is restated from its
 published algorithm: out = D^-1/2 (Adj + I) D^-1/2 (X W^T) + bias, self-loops added where missing,
@@ -247,8 +250,13 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         ys = []
         # inference (model.eval() under no_grad): the hypernetwork runs on the fused HIP kernels
         fused = self.hyper_backend == "auto" and not grad and hyper_ops.supported(self, n)
+        # training (model.train()): the HIP training-mode hypernetwork (dropout, batch statistics,
+        # its backward) — HyperTrainFn
+        train_hip = self.hyper_backend == "auto" and hyper_ops.supported_train(self, n)
         if fused and self.use_hip_graph and self.on_hyp is None:
             return self._forward_graphed(bb, graphs, a_hat.contiguous(), y0, U0, d0, K, H)
+        if fused or train_hip:
+            a_hat = a_hat.contiguous()
         if fused:
             enc = self.encoder
             bufs = hyper_ops.HyperBuffers(batch_size, self.P, enc.conv5.lin.out_features,
@@ -261,6 +269,9 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
                 alpha_k, tau_k, rho_k, eta_k = hyper_ops.hypernetwork_eval(
                     self, AtAy, run.Atb, n, a_hat, not graphs.shared, bufs)
                 hyp_k = bufs.hyp
+            elif train_hip:
+                hyp_k = hyper_ops.hypernetwork_train(self, AtAy, run.Atb, n, a_hat, not graphs.shared)
+                alpha_k, tau_k, rho_k, eta_k = (hyp_k[:, c].view(batch_size, H, 1, 1) for c in range(4))
             else:
                 alpha_k, tau_k, rho_k, eta_k = self.hypernetwork(AtAy[..., :n], Atb, a_hat)
                 hyp_k = torch.stack([alpha_k, tau_k, rho_k, eta_k], dim=1).reshape(batch_size, 4, H)

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 10
+#define DADMM_ABI_VERSION 11
 
 enum {
     DADMM_OK = 0,
@@ -352,6 +352,54 @@ int dadmm_hyper_linear_ln(int32_t rows, int32_t K, int32_t N, const float* x, in
                           const float* W, const float* bias, const float* ln_weight,
                           const float* ln_bias, float eps, int32_t act, float slope, float* y,
                           void* scratch, void* stream);
+
+/* ---- GNN hypernetwork, training mode ---------------------------------------------------------
+ * The same hypernetwork with model.train() semantics (gnn_dlasso_models_progressive.py:52-72:
+ * Dropout(0.1) active, BatchNorm1d on each sample's own batch statistics over its P nodes) and the
+ * pieces of its backward that are not plain GEMMs (the caller runs dW = dZ^T X and dX = dZ W on
+ * hipBLASLt). Dropout masks come from a counter-based stream: element (row, col) of dropout site
+ * `site` is kept iff hash(seed, site, row, col) >= drop_p * 2^32 (drop_hash in the sources); the
+ * backward regenerates them. Results agree with torch's autograd of the same modules (given the
+ * same masks) to f32 rounding; the reference's own dropout draws are not reproducible anywhere.
+ *
+ * dadmm_hyper_gcn_train: y = Dropout_p(BN_batch(leaky(A_hat (x W^T) + bias))) per sample; saves
+ *   m_out [B*P][N] = A_hat (x W^T) + bias and the per-sample mean_out / var_out [B][N] (biased
+ *   variance: the normalisation; the caller updates the running statistics). P >= 2, N % 4 == 0.
+ *   Replaces: GCNConv + F.leaky_relu + bn_i (train) + self.dropout of graph_conv (:52-68).
+ * dadmm_hyper_gcn_train_bwd: from dy [B*P][N] (gradient of that y) to dz [B*P][N] (gradient of
+ *   x W^T), and part [3][B][N]: per-sample sums of dgamma, dbeta and d(GCNConv.bias).
+ * dadmm_hyper_linear_ln_train: one decoder block Linear -> Dropout_p -> LayerNorm -> LeakyReLU?
+ *   (:94-105) in train mode; xd [rows][N] = the LayerNorm input (post-dropout), for the backward.
+ * dadmm_hyper_rownorm_bwd: backward of LayerNorm (+ LeakyReLU when act) rows from their input xd:
+ *   dx w.r.t. the pre-dropout values when drop_p > 0 (same seed / site as the forward), part =
+ *   [ceil(rows / 64)][2][C] block partial sums of dweight, dbias (dadmm_hyper_rownorm_bwd_part_bytes).
+ * dadmm_hyper_head_act: mode 0: hyp [B][4H] = head(z) for the fc logits z (sigmoid, clamp
+ *   [1e-4, 0.9999], * max_c, clamp <= 0.9999 for tau / rho / eta: :167-196); mode 1: out = dz =
+ *   dhyp * head'(z). */
+int dadmm_hyper_gcn_train(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1, int32_t ld1,
+                          int32_t K1, const float* x2, int32_t ld2, const float* W, const float* bias,
+                          const float* ahat, int32_t ahat_per_sample, const float* bn_weight,
+                          const float* bn_bias, float bn_eps, float slope, float drop_p, uint64_t seed,
+                          int32_t site, float* y, int32_t ldy, float* m_out, float* mean_out,
+                          float* var_out, void* stream);
+int dadmm_hyper_gcn_train_bwd(int32_t B, int32_t P, int32_t N, const float* dy, const float* m,
+                              const float* mean, const float* var, const float* bn_weight,
+                              float bn_eps, const float* ahat, int32_t ahat_per_sample, float slope,
+                              float drop_p, uint64_t seed, int32_t site, float* dz, float* part,
+                              void* stream);
+int dadmm_hyper_linear_ln_train(int32_t rows, int32_t K, int32_t N, const float* x, int32_t ldx,
+                                const float* W, const float* bias, const float* ln_weight,
+                                const float* ln_bias, float eps, int32_t act, float slope, float drop_p,
+                                uint64_t seed, int32_t site, float* y, float* xd, void* scratch,
+                                void* stream);
+size_t dadmm_hyper_rownorm_bwd_part_bytes(int32_t rows, int32_t C);
+int dadmm_hyper_rownorm_bwd(int32_t rows, int32_t C, const float* dy, const float* xd,
+                            const float* weight, const float* bias, float eps, int32_t act,
+                            float slope, float drop_p, uint64_t seed, int32_t site, float* dx,
+                            float* part, void* stream);
+int dadmm_hyper_head_act(int32_t mode, int32_t B, int32_t H, const float* z, const float* dhyp,
+                         float alpha_max, float tau_max, float rho_max, float eta_max, float* out,
+                         void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,236 @@
+"""GPU: the training-mode hypernetwork on the HIP kernels (hyper_ops.HyperTrainFn:
+dadmm_hyper_gcn_train / _linear_ln_train / _head_act forward, dadmm_hyper_gcn_train_bwd /
+_rownorm_bwd / _head_act backward, hipBLASLt for the linears' weight / input GEMMs).
+
+Bar: against a plain torch fp32 autograd reference of the same modules in train mode
+(gnn_dlasso_models_progressive.py:52-72 GCNConv -> leaky_relu -> BatchNorm1d on the sample's P
+nodes -> Dropout, LayerNorm, the decoder's Linear -> Dropout -> LayerNorm -> LeakyReLU blocks, fc,
+sigmoid, clamps, maxima :165-196) given the SAME dropout masks — regenerated here from the
+kernels' counter-based stream (a numpy restatement of drop_hash, test infrastructure) — within
+f32 rounding of the different summation orders: hyp, d(AtAy) and every parameter gradient, and
+the BatchNorm running statistics after the update. Model level: a train-mode forward + loss +
+backward of DLASSO_GNNHyp3_Progressive runs on the HIP hypernetwork, and with dropout off it
+matches the torch backend's loss and gradients.
+"""
+import argparse
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+M64 = (1 << 64) - 1
+
+
+def _drop_hash(seed, site, rows, cols):
+    """numpy restatement of drop_hash (csrc/dadmm_internal.h) over a rows x cols grid."""
+    r = np.arange(rows, dtype=np.uint64)[:, None]
+    c = np.arange(cols, dtype=np.uint64)[None, :]
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) ^ (np.uint64(site) << np.uint64(56)) ^ (r << np.uint64(20)) ^ c
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(32)).astype(np.uint64)
+
+
+def _keep(seed, site, rows, cols, p, dev):
+    thr = np.uint64(min(int(p * 4294967296.0), 0xFFFFFFFF))
+    return torch.from_numpy((_drop_hash(seed, site, rows, cols) >= thr).astype(np.float32)).to(dev)
+
+
+def _model(dev, P, n, hidden, mode, seed=0):
+    import gnn_dlasso_models_progressive as G
+    A, b, _ = O.make_problem(P, 16, n, 64, seed=seed + 5)
+    torch.manual_seed(seed)
+    args = argparse.Namespace(GHN_iter_num=3, GHyp_hidden=hidden, DADMM_mode=mode, alpha_max=0.1,
+                              tau_max=0.99, rho_max=0.99, eta_max=0.99)
+    model = G.DLASSO_GNNHyp3_Progressive(torch.from_numpy(A)[None].to(dev), args).to(dev)
+    with torch.no_grad():
+        for i in range(1, 6):
+            bn = getattr(model.encoder, f"bn{i}")
+            bn.running_mean.normal_(0, 0.3)
+            bn.running_var.uniform_(0.5, 2.0)
+            bn.weight.normal_(1, 0.1)
+            bn.bias.normal_(0, 0.1)
+    return model.train(), A, b
+
+
+def _torch_reference(model, AtAy, Atb, n, ahat, seed):
+    """The reference's train-mode hypernetwork with explicit masks (torch autograd)."""
+    B, P, _ = AtAy.shape
+    enc = model.encoder
+    x = torch.cat([AtAy[..., :n], Atb[..., :n]], dim=2)
+    for i, (conv, bn) in enumerate(zip((enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5),
+                                       (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5))):
+        m = torch.matmul(ahat, x @ conv.lin.weight.t()) + conv.bias
+        t = F.leaky_relu(m, 0.01)
+        mean = t.mean(dim=1, keepdim=True)
+        var = t.var(dim=1, unbiased=False, keepdim=True)
+        xn = (t - mean) * torch.rsqrt(var + bn.eps) * bn.weight + bn.bias
+        if i < 4:
+            p = enc.dropout.p
+            xn = xn * _keep(seed, i, B * P, xn.shape[2], p, x.device).view(B, P, -1) * (1.0 / (1.0 - p))
+        x = xn
+    x = F.layer_norm(x, (x.shape[-1],), enc.norm.weight, enc.norm.bias, enc.norm.eps).reshape(B, -1)
+    for blk in range(3):
+        lin, ln = model.decoder[4 * blk], model.decoder[4 * blk + 2]
+        p = model.decoder[4 * blk + 1].p
+        v = F.linear(x, lin.weight, lin.bias)
+        v = v * _keep(seed, 4 + blk, B, v.shape[1], p, x.device) * (1.0 / (1.0 - p))
+        x = F.leaky_relu(F.layer_norm(v, (v.shape[1],), ln.weight, ln.bias, ln.eps),
+                         model.decoder[4 * blk + 3].negative_slope)
+    h = torch.clamp(torch.sigmoid(model.fc(x)), min=1e-4, max=0.9999)
+    H = model.fc.out_features // 4
+    h = h.view(B, 4, H)
+    return torch.stack([h[:, 0] * float(model.alpha_max),
+                        torch.clamp(h[:, 1] * float(model.tau_max), max=0.9999),
+                        torch.clamp(h[:, 2] * float(model.rho_max), max=0.9999),
+                        torch.clamp(h[:, 3] * float(model.eta_max), max=0.9999)], dim=1)
+
+
+def _close(got, want, rel=2e-4, name=""):
+    got, want = got.double(), want.double()
+    scale = want.abs().max().clamp_min(1e-30)
+    err = ((got - want).abs() / (scale * rel + 1e-6 * want.abs())).max()
+    assert torch.isfinite(got).all(), name
+    assert err <= 1.0, f"{name}: max |diff| {float((got - want).abs().max()):.3e} vs scale {float(scale):.3e}"
+
+
+def _close64(got, want32, want64, name=""):
+    """The HIP result's error against the fp64 reference is within 8x torch fp32's own error
+    (plus 1e-5 of the tensor's scale): f32 rounding in a different order, amplified alike by the
+    per-sample BatchNorm statistics of a few nodes, not a different formula."""
+    got, w32, w64 = got.double(), want32.double(), want64.double()
+    scale = float(w64.abs().max().clamp_min(1e-30))
+    e_hip = float((got - w64).abs().max())
+    e_t32 = float((w32 - w64).abs().max())
+    assert torch.isfinite(got).all(), name
+    assert e_hip <= 8.0 * e_t32 + 1e-5 * scale, f"{name}: |hip - fp64| {e_hip:.3e}, |torch32 - fp64| {e_t32:.3e}, scale {scale:.3e}"
+
+
+@pytest.mark.parametrize("P,n,hidden,mode,per_sample,B", [(5, 64, 16, "diff", True, 12),
+                                                          (5, 48, 12, "same", False, 9),
+                                                          (16, 32, 8, "diff", True, 5),
+                                                          (3, 100, 20, "diff", True, 70)])
+def test_train_hypernetwork_matches_torch_autograd(cuda, P, n, hidden, mode, per_sample, B):
+    import copy
+
+    import gnn_dlasso_models_progressive as G
+    from dadmm_hip import hyper_ops
+    from dadmm_hip.graph import ingest
+    model, _, _ = _model(cuda, P, n, hidden, mode)
+    ref = copy.deepcopy(model)
+    graphs = ([O.connected_er_graph(P, 0.5, seed=s) for s in range(B)] if per_sample
+              else [O.er_graph(P, 0.5, seed=3)] * B)
+    gb = ingest(graphs, P, B, cuda)
+    ahat = G.normalized_adjacency(gb.nbr, P)
+    ahat = (ahat[None] if gb.shared else ahat).contiguous()
+    ns = (n + 3) & ~3
+    g = torch.Generator(device=cuda).manual_seed(P * 100 + n)
+    AtAy = torch.zeros(B, P, ns, device=cuda)
+    Atb = torch.zeros(B, P, ns, device=cuda)
+    AtAy[..., :n] = torch.randn(B, P, n, device=cuda, generator=g)
+    Atb[..., :n] = torch.randn(B, P, n, device=cuda, generator=g)
+    AtAy.requires_grad_(True)
+    seed = 0x1234_5678_9ABC
+    hyp = hyper_ops.hypernetwork_train(model, AtAy, Atb, n, ahat, per_sample, seed=seed)
+    ref64 = copy.deepcopy(ref).double()
+    A2 = AtAy.detach().clone().requires_grad_(True)
+    A3 = AtAy.detach().double().requires_grad_(True)
+    want = _torch_reference(ref, A2, Atb, n, ahat, seed)
+    want64 = _torch_reference(ref64, A3, Atb.double(), n, ahat.double(), seed)
+    _close64(hyp, want, want64, name="hyp")
+    R = torch.randn(hyp.shape, device=cuda, generator=g)
+    (hyp * R).sum().backward()
+    (want * R).sum().backward()
+    (want64 * R.double()).sum().backward()
+    _close64(AtAy.grad[..., :n], A2.grad[..., :n], A3.grad[..., :n], name="dAtAy")
+    assert (AtAy.grad[..., n:] == 0).all()
+    for (name, p1), (_, p2), (_, p3) in zip(model.named_parameters(), ref.named_parameters(),
+                                            ref64.named_parameters()):
+        _close64(p1.grad, p2.grad, p3.grad, name=name)
+    for i in range(1, 6):
+        bn = getattr(model.encoder, f"bn{i}")
+        assert torch.isfinite(bn.running_mean).all() and torch.isfinite(bn.running_var).all()
+        assert int(bn.num_batches_tracked) == B
+
+
+def test_train_running_stats_match_sequential_updates(cuda):
+    """BatchNorm running statistics after one training forward == B sequential
+    nn.BatchNorm1d train-mode calls, one per sample, in sample order (the reference's loop)."""
+    import copy
+
+    import gnn_dlasso_models_progressive as G
+    from dadmm_hip import hyper_ops
+    from dadmm_hip.graph import ingest
+    P, n, hidden, B = 5, 32, 8, 7
+    model, _, _ = _model(cuda, P, n, hidden, "diff", seed=3)
+    for mod in [model.encoder.dropout] + [model.decoder[i] for i in (1, 5, 9)]:
+        mod.p = 0.0
+    ref = copy.deepcopy(model)
+    graphs = [O.connected_er_graph(P, 0.5, seed=s) for s in range(B)]
+    gb = ingest(graphs, P, B, cuda)
+    ahat = G.normalized_adjacency(gb.nbr, P).contiguous()
+    g = torch.Generator(device=cuda).manual_seed(5)
+    AtAy = torch.randn(B, P, n, device=cuda, generator=g)
+    Atb = torch.randn(B, P, n, device=cuda, generator=g)
+    with torch.no_grad():
+        hyper_ops.hypernetwork_train(model, AtAy, Atb, n, ahat, True, seed=1)
+        enc = ref.encoder
+        x = torch.cat([AtAy, Atb], dim=2)
+        for i, (conv, bn) in enumerate(zip((enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5),
+                                           (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5))):
+            outs = []
+            for s in range(B):   # the reference's per-sample calls (:37-40, :52-68)
+                m = ahat[s] @ (x[s] @ conv.lin.weight.t()) + conv.bias
+                outs.append(bn(F.leaky_relu(m, 0.01)))
+            x = torch.stack(outs)
+    for i in range(1, 6):
+        b1, b2 = getattr(model.encoder, f"bn{i}"), getattr(ref.encoder, f"bn{i}")
+        _close(b1.running_mean, b2.running_mean, rel=1e-4, name=f"bn{i}.running_mean")
+        _close(b1.running_var, b2.running_var, rel=1e-4, name=f"bn{i}.running_var")
+        assert int(b1.num_batches_tracked) == int(b2.num_batches_tracked) == B
+
+
+def test_model_train_step_uses_hip_hypernetwork(cuda):
+    """DLASSO_GNNHyp3_Progressive in train mode: forward + compute_loss + backward through the
+    HIP hypernetwork; with dropout off it equals the torch backend (loss and gradients)."""
+    import copy
+
+    import gnn_dlasso_utils as U
+    from dadmm_hip import hyper_ops
+    P, n, hidden, B, K = 5, 64, 16, 16, 3
+    model, A, b = _model(cuda, P, n, hidden, "diff", seed=7)
+    for mod in [model.encoder.dropout] + [model.decoder[i] for i in (1, 5, 9)]:
+        mod.p = 0.0
+    ref = copy.deepcopy(model)
+    ref.hyper_backend = "torch"
+    graphs = [O.connected_er_graph(P, 0.5, seed=s) for s in range(B)]
+    rng = np.random.default_rng(2)
+    inits = tuple(torch.from_numpy((1e-2 * rng.standard_normal((B, P, n))).astype(np.float32)).to(cuda)
+                  for _ in range(3))
+    bt = torch.from_numpy(b[:B]).to(cuda)[..., None]
+    label = torch.randn(B, n, 1, device=cuda)
+    calls = []
+    orig = hyper_ops.HyperTrainFn.apply
+    hyper_ops.HyperTrainFn.apply = lambda *a: (calls.append(1), orig(*a))[1]
+    try:
+        Y1, _ = model(bt, graphs, K, inits=inits)
+    finally:
+        hyper_ops.HyperTrainFn.apply = orig
+    assert len(calls) == K
+    Y2, _ = ref(bt, graphs, K, inits=inits)
+    l1, f1 = U.compute_loss(Y1, label)
+    l2, f2 = U.compute_loss(Y2, label)
+    assert abs(float(l1) - float(l2)) <= 1e-4 * abs(float(l2))
+    l1.backward()
+    l2.backward()
+    for (name, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
+        assert p1.grad is not None and torch.isfinite(p1.grad).all(), name
+        _close(p1.grad, p2.grad, rel=5e-3, name=name)
