@@ -281,6 +281,7 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
         import argparse as _ap
 
         import gnn_dlasso_models_progressive as GM
+        import gnn_dlasso_utils
         args = _ap.Namespace(GHN_iter_num=K, GHyp_hidden=100, DADMM_mode="diff", alpha_max=0.1,
                              tau_max=0.99, rho_max=0.99, eta_max=0.99)
         gnn = GM.DLASSO_GNNHyp3_Progressive(torch.from_numpy(A)[None].to(dev), args).to(dev).eval()
@@ -299,6 +300,26 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
                               "units_per_s": Bg * K / (ms * 1e-3),
                               "hypernetwork": "fused HIP (dadmm_hyper_*)",
                               "ms_torch_hypernetwork": ms_torch}
+        # training step of the GNN model (model.train(): dropout, batch statistics, autograd):
+        # forward + compute_loss + backward, HIP training hypernetwork vs the torch composition
+        Bt = 256
+        bgt = b[:Bt, ..., None].to(dev)
+        lab = x[:Bt].to(dev)[..., None]
+        gnn.train()
+
+        def gstep():
+            Y, _ = gnn(bgt, graphs[:Bt])
+            _, lf = gnn_dlasso_utils.compute_loss(Y, lab)
+            gnn.zero_grad()
+            lf.backward()
+        ms_tr = _event_ms(gstep, 3, warm=1)
+        gnn.hyper_backend = "torch"
+        ms_tr_torch = _event_ms(gstep, 2, warm=1)
+        gnn.hyper_backend = "auto"
+        gnn.eval()
+        out["gnn_train_step"] = {"B": Bt, "K": K, "ms": ms_tr, "units_per_s": Bt * K / (ms_tr * 1e-3),
+                                 "hypernetwork": "HIP training kernels (HyperTrainFn)",
+                                 "ms_torch_hypernetwork": ms_tr_torch}
     except Exception as e:
         out["gnn_error"] = repr(e)[:300]
     try:
@@ -432,10 +453,15 @@ def cpu_baseline(O, A, b, G, model, P, n, m, K, seconds):
       * c_port: oracle_forward_f32 (C, OpenMP over samples, the kernel's factored order);
       * torch_loop_faithful: oracle/ref_torch.forward — the reference's eager op sequence with its
         Python per-edge compute_delta loop (unfolded_DLASSO.py:127-140): its real cost profile;
-    each on every host thread this process may use and on 1 thread. The headline object is the
-    fastest leg at all threads; every leg is listed under "legs"."""
+    each on every host thread this process may use (the affinity mask, capped at the cgroup's CPU
+    quota: on the GPU boxes 256 hardware threads but a 16-CPU quota, where 256 software threads
+    only thrash) and on 1 thread. The headline object is the fastest leg at that thread count;
+    every leg is listed under "legs"."""
+    import math
+
     from oracle import ref_torch
-    all_threads, cpu_model, quota = _host_cpus()
+    hw_threads, cpu_model, quota = _host_cpus()
+    all_threads = min(hw_threads, max(1, math.ceil(quota))) if quota else hw_threads
     with torch.no_grad():
         table = model.hyp_table(K).cpu().numpy()
     bn = b.numpy()
@@ -473,7 +499,8 @@ def cpu_baseline(O, A, b, G, model, P, n, m, K, seconds):
     return {"value": best["value"], "unit": "ADMM-iters/s", "cores": all_threads, "kind": "port",
             "sample": f"{best_name.split('@')[0]} on {best['problems']} problems of the same shape "
                       f"(P={P} n={n} m={m} K={K}), {best['seconds']} s, {all_threads} threads",
-            "cpu_model": cpu_model, "cgroup_cpu_quota": quota, "legs": legs}
+            "cpu_model": cpu_model, "cgroup_cpu_quota": quota, "hardware_threads": hw_threads,
+            "legs": legs}
 
 
 if __name__ == "__main__":
