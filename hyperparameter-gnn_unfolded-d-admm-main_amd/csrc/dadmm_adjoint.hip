@@ -42,13 +42,15 @@ __device__ __forceinline__ void clips(int variant, int k, float& gclip, float& v
     }
 }
 
-// sum over p's visit list of (x_p - x_q): compute_delta's accumulation order (:127-140)
+// sum over p's visit list of (x_p - x_q): compute_delta's accumulation order (:127-140). The
+// sample's list starts vp [P + 1] (relative) and entries vq sit in this wave's LDS slice: the
+// list walk is LDS reads, not a chain of dependent global loads per agent.
 __device__ __forceinline__ float visit_sum(const float* __restrict__ x, const int32_t* __restrict__ vp,
-                                           const uint8_t* __restrict__ vq, int g0, int p, int lane) {
+                                           const uint8_t* __restrict__ vq, int p, int lane) {
     const float xp = x[p * 64 + lane];
     float acc = 0.0f;
-    const int t1 = vp[g0 + p + 1];
-    for (int t = vp[g0 + p]; t < t1; ++t) acc = acc + (xp - x[(int)vq[t] * 64 + lane]);
+    const int t1 = vp[p + 1];
+    for (int t = vp[p]; t < t1; ++t) acc = acc + (xp - x[(int)vq[t] * 64 + lane]);
     return acc;
 }
 
@@ -67,6 +69,9 @@ __global__ __launch_bounds__(THREADS) void adj_update_kernel(AdjArgs a, int k, i
     float* ds = xs + P * 64;                   // [P][64] d_bar (w.r.t. delta_{k+1})
     float* red = lds + WAVES * 2 * P * 64;     // [WAVES][P][4] partial sums
     float* rw = red + w * P * 4;
+    // per wave: the sample's visit-list starts [P + 1] and entries [<= 2 P^2 bytes]
+    int32_t* vpl = (int32_t*)(red + WAVES * P * 4) + w * (P + 1 + (2 * P * P + 3) / 4);
+    uint8_t* vql = (uint8_t*)(vpl + P + 1);
     for (int i = lane; i < P * 4; i += 64) rw[i] = 0.0f;
     const int item = blockIdx.x * WAVES + w;
     const size_t S = (size_t)a.B * P * n;
@@ -76,6 +81,11 @@ __global__ __launch_bounds__(THREADS) void adj_update_kernel(AdjArgs a, int k, i
         const bool cv = c < n;
         const size_t base = (size_t)s * P * n + (cv ? c : 0);
         const int g0 = a.graph_shared ? 0 : s * P;
+        {
+            const int v0 = a.vptr[g0], ve = a.vptr[g0 + P];
+            for (int i = lane; i <= P; i += 64) vpl[i] = a.vptr[g0 + i] - v0;
+            for (int i = lane; i < ve - v0; i += 64) vql[i] = a.vq[v0 + i];
+        }
         float gclip, vclip;
         clips(a.variant, k, gclip, vclip);
         auto hyp = [&](int kk, int p, int comp) {
@@ -83,11 +93,20 @@ __global__ __launch_bounds__(THREADS) void adj_update_kernel(AdjArgs a, int k, i
         };
         const float* __restrict__ y1 = a.Y + (size_t)k * S;                    // y_{k+1}
         const float* __restrict__ yk = k > 0 ? a.Y + (size_t)(k - 1) * S : a.y0;
+        // restrict-qualified views: the scratch state (yb, Ub, Gb) never aliases the recorded
+        // trajectory, so the compiler may batch the loads of several agents ahead of the stores
+        const float* __restrict__ gYk = a.gY + (size_t)k * S;
+        const float* __restrict__ Urk = a.Urec + (size_t)k * S;
+        const float* __restrict__ Grk = a.Grec + (size_t)k * S;
+        float* __restrict__ ybs = a.yb;
+        float* __restrict__ Ubs = a.Ub;
+        float* __restrict__ Gbs = a.Gb;
+#pragma unroll 4
         for (int p = 0; p < P; ++p) xs[p * 64 + lane] = cv ? y1[base + (size_t)p * n] : 0.0f;
         __builtin_amdgcn_wave_barrier();
         // dual-update adjoint of iteration k (:95-99): w = U_k + delta_{k+1} eta_k
         for (int p = 0; p < P; ++p) {
-            const float d1 = visit_sum(xs, a.vptr, a.vq, g0, p, lane);
+            const float d1 = visit_sum(xs, vpl, vql, p, lane);
             const bool md = a.variant == 0 || inside(d1, -20.0f, 20.0f);   // GNN clamp :229
             const float dcl = a.variant == 0 ? d1 : tclamp(d1, -20.0f, 20.0f);
             float pe = 0.0f, db = 0.0f;
@@ -95,25 +114,26 @@ __global__ __launch_bounds__(THREADS) void adj_update_kernel(AdjArgs a, int k, i
                 const size_t off = base + (size_t)p * n;
                 const float et = hyp(k, p, 3);
                 const float rh1 = k + 1 < K ? hyp(k + 1, p, 2) : 0.0f;
-                a.yb[off] = a.yb[off] + a.gY[(size_t)k * S + off];            // + gY[k]
-                const float wv = a.Urec[(size_t)k * S + off] + dcl * et;
-                const float wb = inside(wv, -vclip, vclip) ? a.Ub[off] : 0.0f;
+                ybs[off] = ybs[off] + gYk[off];                                 // + gY[k]
+                const float wv = Urk[off] + dcl * et;
+                const float wb = inside(wv, -vclip, vclip) ? Ubs[off] : 0.0f;
                 pe = wb * dcl;
-                db = md ? a.Gb[off] * rh1 + wb * et : 0.0f;
-                a.Ub[off] = wb;
+                db = md ? Gbs[off] * rh1 + wb * et : 0.0f;
+                Ubs[off] = wb;
             }
             ds[p * 64 + lane] = db;
             wave_accum(rw, p, 3, pe, lane);
         }
         __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
         for (int p = 0; p < P; ++p) xs[p * 64 + lane] = cv ? yk[base + (size_t)p * n] : 0.0f;
         __builtin_amdgcn_wave_barrier();
         // y_bar += 2 L d_bar; primal-update and gradient-clamp adjoint (:73-93)
         for (int p = 0; p < P; ++p) {
-            const float t = visit_sum(ds, a.vptr, a.vq, g0, p, lane);
+            const float t = visit_sum(ds, vpl, vql, p, lane);
             float dk = 0.0f;
             if (k > 0) {
-                dk = visit_sum(xs, a.vptr, a.vq, g0, p, lane);
+                dk = visit_sum(xs, vpl, vql, p, lane);
                 if (a.variant != 0) dk = tclamp(dk, -20.0f, 20.0f);
             }
             float pa = 0.0f, pt = 0.0f, pr = 0.0f;
@@ -122,19 +142,19 @@ __global__ __launch_bounds__(THREADS) void adj_update_kernel(AdjArgs a, int k, i
                 if (k == 0) dk = a.d0[off];
                 const float al = hyp(k, p, 0);
                 const float y = xs[p * 64 + lane];
-                const float gr = a.Grec[(size_t)k * S + off];
+                const float gr = Grk[off];
                 const float g = tclamp(gr, -gclip, gclip);
                 const float z = y - al * g;
-                const float ybv = a.yb[off] + t;
+                const float ybv = ybs[off] + t;
                 const float zb = inside(z, -vclip, vclip) ? ybv : 0.0f;
                 pa = -zb * g;
                 const float grb = inside(gr, -gclip, gclip) ? -al * zb : 0.0f;
                 pt = grb * sign_times(y, 1.0f);
                 pr = grb * dk;
                 const float dg = a.deg[g0 + p];
-                a.Ub[off] = a.Ub[off] + grb * dg;
-                a.yb[off] = zb;
-                a.Gb[off] = grb;
+                Ubs[off] = Ubs[off] + grb * dg;
+                ybs[off] = zb;
+                Gbs[off] = grb;
             }
             wave_accum(rw, p, 0, pa, lane);
             wave_accum(rw, p, 1, pt, lane);
@@ -153,7 +173,10 @@ __global__ __launch_bounds__(THREADS) void adj_update_kernel(AdjArgs a, int k, i
 
 }  // namespace adj
 
-size_t adjoint_lds_bytes(int P) { return 4 * ((size_t)adj::WAVES * 2 * P * 64 + (size_t)adj::WAVES * P * 4); }
+size_t adjoint_lds_bytes(int P) {
+    return 4 * ((size_t)adj::WAVES * 2 * P * 64 + (size_t)adj::WAVES * P * 4 +
+                (size_t)adj::WAVES * (P + 1 + (2 * P * P + 3) / 4));
+}
 int adjoint_workgroups(int B, int n) {
     const long items = (long)B * ((n + 63) / 64);
     return (int)((items + adj::WAVES - 1) / adj::WAVES);

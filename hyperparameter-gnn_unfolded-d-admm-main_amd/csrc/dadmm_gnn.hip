@@ -399,11 +399,14 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int P = a.P, n = a.n, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int H = a.hyp_rows;
-    float* sl = lds + wv * (3 * P * 64 + 4 * P);
+    const int VW = (P + 1) + (2 * P * P + 3) / 4;   // visit-list words per wave
+    float* sl = lds + wv * (3 * P * 64 + 4 * P + VW);
     float* y1l = sl;                           // [P][64] y_{k+1}
     float* dbl = sl + P * 64;                  // [P][64] d_bar_raw
     float* ybl = sl + 2 * P * 64;              // [P][64] 2 L d_bar_raw
     float* red = sl + 3 * P * 64;              // [4][H] per-sample hyp gradient
+    int32_t* vpl = (int32_t*)(red + 4 * P);    // the sample's visit lists: starts [P + 1], entries
+    uint8_t* vql = (uint8_t*)(vpl + P + 1);
     const int s = blockIdx.x * WAVES + wv;
     if (s >= a.B) return;                      // whole waves only: no block barrier below
     float gclip, vclip;
@@ -411,6 +414,12 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
     const float* ys = a.yk;
     const int g0 = a.graph_shared ? 0 : s * P;
     for (int i = lane; i < 4 * H; i += 64) red[i] = 0.0f;
+    {
+        const int v0 = a.vptr[g0], ve = a.vptr[g0 + P];
+        for (int i = lane; i <= P; i += 64) vpl[i] = a.vptr[g0 + i] - v0;
+        for (int i = lane; i < ve - v0; i += 64) vql[i] = a.vq[v0 + i];
+    }
+    __builtin_amdgcn_wave_barrier();
     auto accum = [&](int c, int p, float v) {   // wave-sum v into red[c][p or 0]
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
@@ -441,8 +450,8 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
         for (int p = 0; p < P; ++p) {
             const float yp = y1l[p * 64 + lane];
             float acc = 0.0f;
-            const int t1 = a.vptr[g0 + p + 1];
-            for (int t = a.vptr[g0 + p]; t < t1; ++t) acc = acc + (yp - y1l[(int)a.vq[t] * 64 + lane]);
+            const int t1 = vpl[p + 1];
+            for (int t = vpl[p]; t < t1; ++t) acc = acc + (yp - y1l[(int)vql[t] * 64 + lane]);
             float dbr = 0.0f, pe = 0.0f;
             if (cv) {
                 const size_t off = base + (size_t)p * n;
@@ -461,8 +470,8 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
         for (int p = 0; p < P; ++p) {   // 2 L d_bar_raw, same visit lists (the map is symmetric)
             const float xp = dbl[p * 64 + lane];
             float acc = 0.0f;
-            const int t1 = a.vptr[g0 + p + 1];
-            for (int t = a.vptr[g0 + p]; t < t1; ++t) acc = acc + (xp - dbl[(int)a.vq[t] * 64 + lane]);
+            const int t1 = vpl[p + 1];
+            for (int t = vpl[p]; t < t1; ++t) acc = acc + (xp - dbl[(int)vql[t] * 64 + lane]);
             ybl[p * 64 + lane] = acc;
         }
         // primal update + gradient clamp adjoint
@@ -552,7 +561,8 @@ hipError_t gnn_launch_finish(const GnnArgs& a, hipStream_t st) {
 }
 
 hipError_t gnn_launch_step_backward(const GnnArgs& a, int k, const GnnGrads& gg, hipStream_t st) {
-    const size_t lds = 4 * (size_t)gnn::WAVES * (3 * a.P * 64 + 4 * a.P);
+    const size_t lds = 4 * (size_t)gnn::WAVES * (3 * a.P * 64 + 4 * a.P + (a.P + 1) + (2 * a.P * a.P + 3) / 4);
+    if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)gnn::step_backward_kernel,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

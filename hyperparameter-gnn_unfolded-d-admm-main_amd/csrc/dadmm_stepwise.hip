@@ -221,6 +221,15 @@ __device__ void phase_update(const StepArgs& a, int k, int item, float* ylds) {
     clips(a, k, gclip, vclip);
     float* yl = ylds + (threadIdx.x >> 6) * (P * 64);   // this wave's [P][64] y_next
     const int lane = threadIdx.x & 63;
+    // this wave's copy of the sample's visit lists: starts [P + 1] (relative), entries (bytes)
+    int32_t* vpl = (int32_t*)(ylds + SW_WAVES * P * 64) + (threadIdx.x >> 6) * (P + 1 + (2 * P * P + 3) / 4);
+    uint8_t* vql = (uint8_t*)(vpl + P + 1);
+    const int g0 = a.graph_shared ? 0 : s * P;
+    {
+        const int v0 = a.vptr[g0], ve = a.vptr[g0 + P];
+        for (int i = lane; i <= P; i += 64) vpl[i] = a.vptr[g0 + i] - v0;
+        for (int i = lane; i < ve - v0; i += 64) vql[i] = a.vq[v0 + i];
+    }
 
     bool bad_y = false;
     for (int p = 0; p < P; ++p) {
@@ -236,16 +245,17 @@ __device__ void phase_update(const StepArgs& a, int k, int item, float* ylds) {
         }
         yl[p * 64 + lane] = v;
     }
-    // delta_{k+1}[p] = sum over p's visit list of (y_p - y_q), in the reference's order (:127-140)
-    const int g0 = a.graph_shared ? 0 : s * P;
+    // delta_{k+1}[p] = sum over p's visit list of (y_p - y_q), in the reference's order (:127-140),
+    // the list read from LDS (no chain of dependent global loads per agent)
+    __builtin_amdgcn_wave_barrier();
     bool bad_u = false;
     for (int p = 0; p < P; ++p) {
         float al, ta, rh, et;
         hyp_row(a, k, p, al, ta, rh, et);
         const float yp = yl[p * 64 + lane];
         float acc = 0.0f;
-        const int t1 = a.vptr[g0 + p + 1];
-        for (int t = a.vptr[g0 + p]; t < t1; ++t) acc = acc + (yp - yl[(int)a.vq[t] * 64 + lane]);
+        const int t1 = vpl[p + 1];
+        for (int t = vpl[p]; t < t1; ++t) acc = acc + (yp - yl[(int)vql[t] * 64 + lane]);
         if (a.variant != 0) acc = clamp_t(acc, -20.0f, 20.0f);             // GNN :229
         if (cv) {
             const size_t off = base + (size_t)p * n;
@@ -387,7 +397,9 @@ out:
 }
 
 size_t grad_lds_bytes(int n_pad, int m_pad) { return 4 * (size_t)(BT * (n_pad + 4) + BT * (m_pad + 4)); }
-size_t update_lds_bytes(int P) { return 4 * (size_t)SW_WAVES * P * 64; }
+size_t update_lds_bytes(int P) {
+    return 4 * ((size_t)SW_WAVES * P * 64 + (size_t)SW_WAVES * (P + 1 + (2 * P * P + 3) / 4));
+}
 
 }  // namespace
 
