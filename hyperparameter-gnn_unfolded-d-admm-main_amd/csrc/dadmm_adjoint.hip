@@ -104,61 +104,106 @@ __global__ __launch_bounds__(THREADS) void adj_update_kernel(AdjArgs a, int k, i
 #pragma unroll 4
         for (int p = 0; p < P; ++p) xs[p * 64 + lane] = cv ? y1[base + (size_t)p * n] : 0.0f;
         __builtin_amdgcn_wave_barrier();
-        // dual-update adjoint of iteration k (:95-99): w = U_k + delta_{k+1} eta_k
-        for (int p = 0; p < P; ++p) {
-            const float d1 = visit_sum(xs, vpl, vql, p, lane);
-            const bool md = a.variant == 0 || inside(d1, -20.0f, 20.0f);   // GNN clamp :229
-            const float dcl = a.variant == 0 ? d1 : tclamp(d1, -20.0f, 20.0f);
-            float pe = 0.0f, db = 0.0f;
-            if (cv) {
-                const size_t off = base + (size_t)p * n;
-                const float et = hyp(k, p, 3);
-                const float rh1 = k + 1 < K ? hyp(k + 1, p, 2) : 0.0f;
-                ybs[off] = ybs[off] + gYk[off];                                 // + gY[k]
-                const float wv = Urk[off] + dcl * et;
-                const float wb = inside(wv, -vclip, vclip) ? Ubs[off] : 0.0f;
-                pe = wb * dcl;
-                db = md ? Gbs[off] * rh1 + wb * et : 0.0f;
-                Ubs[off] = wb;
+        // dual-update adjoint of iteration k (:95-99): w = U_k + delta_{k+1} eta_k. Agents go in
+        // groups of GP: the group's visit sums (LDS) first, then all its loads in flight at once,
+        // then the arithmetic and the stores (a per-agent load -> use chain was latency-bound)
+        constexpr int GP = 4;
+        for (int p0 = 0; p0 < P; p0 += GP) {
+            float d1[GP], gy[GP], ur[GP], ub[GP], gb[GP], yb[GP];
+#pragma unroll
+            for (int i = 0; i < GP; ++i) d1[i] = p0 + i < P ? visit_sum(xs, vpl, vql, p0 + i, lane) : 0.0f;
+#pragma unroll
+            for (int i = 0; i < GP; ++i) {
+                const int p = p0 + i;
+                gy[i] = ur[i] = ub[i] = gb[i] = yb[i] = 0.0f;
+                if (cv && p < P) {
+                    const size_t off = base + (size_t)p * n;
+                    gy[i] = gYk[off];
+                    ur[i] = Urk[off];
+                    ub[i] = Ubs[off];
+                    gb[i] = Gbs[off];
+                    yb[i] = ybs[off];
+                }
             }
-            ds[p * 64 + lane] = db;
-            wave_accum(rw, p, 3, pe, lane);
+#pragma unroll
+            for (int i = 0; i < GP; ++i) {
+                const int p = p0 + i;
+                if (p >= P) break;
+                const bool md = a.variant == 0 || inside(d1[i], -20.0f, 20.0f);   // GNN clamp :229
+                const float dcl = a.variant == 0 ? d1[i] : tclamp(d1[i], -20.0f, 20.0f);
+                float pe = 0.0f, db = 0.0f;
+                if (cv) {
+                    const size_t off = base + (size_t)p * n;
+                    const float et = hyp(k, p, 3);
+                    const float rh1 = k + 1 < K ? hyp(k + 1, p, 2) : 0.0f;
+                    ybs[off] = yb[i] + gy[i];                                     // + gY[k]
+                    const float wv = ur[i] + dcl * et;
+                    const float wb = inside(wv, -vclip, vclip) ? ub[i] : 0.0f;
+                    pe = wb * dcl;
+                    db = md ? gb[i] * rh1 + wb * et : 0.0f;
+                    Ubs[off] = wb;
+                }
+                ds[p * 64 + lane] = db;
+                wave_accum(rw, p, 3, pe, lane);
+            }
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll 4
         for (int p = 0; p < P; ++p) xs[p * 64 + lane] = cv ? yk[base + (size_t)p * n] : 0.0f;
         __builtin_amdgcn_wave_barrier();
-        // y_bar += 2 L d_bar; primal-update and gradient-clamp adjoint (:73-93)
-        for (int p = 0; p < P; ++p) {
-            const float t = visit_sum(ds, vpl, vql, p, lane);
-            float dk = 0.0f;
-            if (k > 0) {
-                dk = visit_sum(xs, vpl, vql, p, lane);
-                if (a.variant != 0) dk = tclamp(dk, -20.0f, 20.0f);
+        // y_bar += 2 L d_bar; primal-update and gradient-clamp adjoint (:73-93), grouped as above
+        for (int p0 = 0; p0 < P; p0 += GP) {
+            float tv[GP], dk[GP], gr[GP], yb[GP], ub[GP];
+#pragma unroll
+            for (int i = 0; i < GP; ++i) {
+                const int p = p0 + i;
+                tv[i] = dk[i] = 0.0f;
+                if (p < P) {
+                    tv[i] = visit_sum(ds, vpl, vql, p, lane);
+                    if (k > 0) {
+                        dk[i] = visit_sum(xs, vpl, vql, p, lane);
+                        if (a.variant != 0) dk[i] = tclamp(dk[i], -20.0f, 20.0f);
+                    }
+                }
             }
-            float pa = 0.0f, pt = 0.0f, pr = 0.0f;
-            if (cv) {
-                const size_t off = base + (size_t)p * n;
-                if (k == 0) dk = a.d0[off];
-                const float al = hyp(k, p, 0);
-                const float y = xs[p * 64 + lane];
-                const float gr = Grk[off];
-                const float g = tclamp(gr, -gclip, gclip);
-                const float z = y - al * g;
-                const float ybv = ybs[off] + t;
-                const float zb = inside(z, -vclip, vclip) ? ybv : 0.0f;
-                pa = -zb * g;
-                const float grb = inside(gr, -gclip, gclip) ? -al * zb : 0.0f;
-                pt = grb * sign_times(y, 1.0f);
-                pr = grb * dk;
-                const float dg = a.deg[g0 + p];
-                Ubs[off] = Ubs[off] + grb * dg;
-                ybs[off] = zb;
-                Gbs[off] = grb;
+#pragma unroll
+            for (int i = 0; i < GP; ++i) {
+                const int p = p0 + i;
+                gr[i] = yb[i] = ub[i] = 0.0f;
+                if (cv && p < P) {
+                    const size_t off = base + (size_t)p * n;
+                    if (k == 0) dk[i] = a.d0[off];
+                    gr[i] = Grk[off];
+                    yb[i] = ybs[off];
+                    ub[i] = Ubs[off];
+                }
             }
-            wave_accum(rw, p, 0, pa, lane);
-            wave_accum(rw, p, 1, pt, lane);
-            wave_accum(rw, p, 2, pr, lane);
+#pragma unroll
+            for (int i = 0; i < GP; ++i) {
+                const int p = p0 + i;
+                if (p >= P) break;
+                float pa = 0.0f, pt = 0.0f, pr = 0.0f;
+                if (cv) {
+                    const size_t off = base + (size_t)p * n;
+                    const float al = hyp(k, p, 0);
+                    const float y = xs[p * 64 + lane];
+                    const float g = tclamp(gr[i], -gclip, gclip);
+                    const float z = y - al * g;
+                    const float ybv = yb[i] + tv[i];
+                    const float zb = inside(z, -vclip, vclip) ? ybv : 0.0f;
+                    pa = -zb * g;
+                    const float grb = inside(gr[i], -gclip, gclip) ? -al * zb : 0.0f;
+                    pt = grb * sign_times(y, 1.0f);
+                    pr = grb * dk[i];
+                    const float dg = a.deg[g0 + p];
+                    Ubs[off] = ub[i] + grb * dg;
+                    ybs[off] = zb;
+                    Gbs[off] = grb;
+                }
+                wave_accum(rw, p, 0, pa, lane);
+                wave_accum(rw, p, 1, pt, lane);
+                wave_accum(rw, p, 2, pr, lane);
+            }
         }
     }
     __syncthreads();
