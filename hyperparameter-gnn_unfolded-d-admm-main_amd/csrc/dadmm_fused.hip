@@ -36,6 +36,17 @@
 #ifndef DADMM_FUSED_REC
 #define DADMM_FUSED_REC 0
 #endif
+// GEMM2's A^T operand through a per-wave LDS ring filled by LDS-DMA (buffer_load ... lds):
+// DADMM_AT_QD quarter-chains (16 n-rows x 16 m, 1 KB per wave) deep, no VGPRs in flight
+#ifndef DADMM_AT_DMA
+#define DADMM_AT_DMA 1
+#endif
+#ifndef DADMM_A_RING
+#define DADMM_A_RING 3
+#endif
+#ifndef DADMM_AT_QD
+#define DADMM_AT_QD 5
+#endif
 
 namespace dadmm {
 
@@ -52,6 +63,25 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
 }
 __device__ __forceinline__ f32x4 bload4(rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+typedef __attribute__((address_space(3))) void lds_void;
+// s_waitcnt vmcnt(n) for a small compile-time n (the switch folds once the loops are unrolled)
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    }
 }
 __device__ __forceinline__ void bstore4(f32x4 v, rsrc_t r, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, voff, soff, 0);
@@ -149,10 +179,12 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     // deeper ring for the small-state instantiations perturbs the register allocation of the
     // large ones compiled in the same module (MI355X_MICROARCH §5.4 rule 19): measured 65 VGPR
     // spills for P=5, n=256 with a conditional depth, 3 with a uniform depth of 2.
-    constexpr int RING = 2;
+    constexpr int RING = DADMM_A_RING;
     float* __restrict__ Ylds = lds;                  // [P][BT][YS]   y_k, n contiguous
     float* __restrict__ Rlds = lds + P * BT * YS;    // [P][BT][RS]   A y - b, m contiguous
-    float* __restrict__ Blds = Rlds + P * BT * RS;   // [P][BT][RS]   -b
+    float* __restrict__ Blds = Rlds + P * BT * RS;   // [P][BT][RS]   -b (not with DADMM_AT_DMA)
+    constexpr int QD = DADMM_AT_QD;
+    float* __restrict__ Qlds = Rlds + P * BT * RS;   // [WAVES][QD][256] A^T ring (DADMM_AT_DMA)
 
     const int lane = threadIdx.x & 63;
     const int j = lane & 15;             // sample within the tile (MFMA column)
@@ -214,8 +246,10 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
             }
         }
     }
-    // -b for this wave's GEMM1 tiles (agent HALF + AS*i, rows m = 16*mb + 4h + r) lives in LDS
-    // next to R: it seeds every iteration's GEMM1 chains without holding registers.
+    // -b for this wave's GEMM1 tiles (agent HALF + AS*i, rows m = 16*mb + 4h + r) seeds every
+    // iteration's GEMM1 chains: in LDS next to R, or (DADMM_AT_DMA: that LDS holds the A^T ring)
+    // in registers
+    f32x4 bseed[THA];
 #pragma unroll
     for (int i = 0; i < TH; ++i) {
         const int p = HALF + AS * i;
@@ -225,7 +259,8 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
             const int mi = 16 * mb + 4 * h + r;
             v[r] = (sv && mi < m) ? -a.b[((size_t)s * P + p) * m + mi] : 0.0f;
         }
-        *(f32x4*)(Blds + (p * BT + j) * RS + 16 * mb + 4 * h) = v;
+        if constexpr (DADMM_AT_DMA) bseed[i] = v;
+        else *(f32x4*)(Blds + (p * BT + j) * RS + 16 * mb + 4 * h) = v;
     }
 
     // Reference guards at the top of an iteration (unfolded_DLASSO.py:55-61) can only fire at
@@ -252,6 +287,15 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     uint32_t voffAtw[T2];                                                 // rows of tile tt
 #pragma unroll
     for (int tt = 0; tt < T2; ++tt) voffAtw[tt] = voffAt + (uint32_t)(16 * (w * T2 + tt) * MP * 4);
+    // GEMM2 quarter q = 4 (p T2 + tt) + t: A^T_p rows of n-tile w T2 + tt, m-block t, DMA'd into
+    // ring slot q % QD of this wave (lane-linear: lane l's 16 bytes at l * 16, which is exactly the
+    // MFMA A-operand fragment lane l reads back)
+    auto dma_quarter = [&](const uint32_t (&vAt)[T2], int q) {
+        const int c = q >> 2, t = q & 3;
+        const int p = c / T2, tt = c % T2;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rAt, (lds_void*)(Qlds + (w * QD + q % QD) * 256), 16,
+                                                 vAt[tt] + 64 * t, (uint32_t)(p * NP * MP * 4), 0, 0);
+    };
 
     // GEMM1 A-operand ring: slot t % RING holds A rows of step t (16 columns) for the TH tiles.
     // The first step of every iteration is issued before the previous iteration's last Y stores,
@@ -265,7 +309,8 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
         for (int i = 0; i < TH; ++i)
             slot[i] = ABL_A(bload4(rA, vA + 64 * t, (uint32_t)((HALF + AS * i) * MP * NP * 4)));
     };
-    load_a(aring[0], 0);
+#pragma unroll
+    for (int t = 0; t + 1 < RING; ++t) load_a(aring[t], t);
     if (HALF == 1) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half loses arbitration
     __syncthreads();
     STAMP_DECL
@@ -339,14 +384,15 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
             f32x4 acc[THA];
 #pragma unroll
             for (int i = 0; i < TH; ++i)
-                acc[i] = *(const f32x4*)(Blds + ((HALF + AS * i) * BT + j) * RS + 16 * mb + 4 * h);
+                acc[i] = DADMM_AT_DMA ? bseed[i]
+                                      : *(const f32x4*)(Blds + ((HALF + AS * i) * BT + j) * RS + 16 * mb + 4 * h);
             f32x4 bring[2][THA];
 #pragma unroll
             for (int i = 0; i < TH; ++i)
                 bring[0][i] = *(const f32x4*)(brow + (HALF + AS * i) * BT * YS);
 #pragma unroll
             for (int t = 0; t < NB; ++t) {
-                if (t + 1 < NB) load_a(aring[(t + 1) % RING], t + 1);
+                if (t + RING - 1 < NB) load_a(aring[(t + RING - 1) % RING], t + RING - 1);
                 compiler_fence();
                 if (t + 1 < NB) {
 #pragma unroll
@@ -360,6 +406,13 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
                     for (int i = 0; i < TH; ++i) acc[i] = mfma4(av[i][r], bv[i][r], acc[i]);
+                if constexpr (DADMM_AT_DMA) {
+                    // GEMM2's first quarters, in flight across the barrier
+                    if (t == NB - 1 && has_tiles) {
+#pragma unroll
+                        for (int q = 0; q + 1 < QD && q < P * T2 * 4; ++q) dma_quarter(vAt, q);
+                    }
+                }
                 // rows e with e * NB / E == t
 #pragma unroll
                 for (int e = 0; e < E; ++e)
@@ -382,16 +435,20 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
             const rsrc_t rG = make_rsrc(REC ? a.Grec + (size_t)k * B * P * n : a.Y, REC ? state_bytes : 0u);
             const rsrc_t rUr = make_rsrc(REC ? a.Urec + (size_t)k * B * P * n : a.Y, REC ? state_bytes : 0u);
             constexpr int NS = P * T2;                       // chains: s = p*T2 + tt
+#if !DADMM_AT_DMA
             f32x4 tring[2][MP / 16];
+#endif
             f32x4 g[2];
             f32x4 rv[MP / 16];
             bool bad_g = false;
+#if !DADMM_AT_DMA
             auto load_at = [&](f32x4 (&slot)[MP / 16], int s2) {
                 const int p = s2 / T2, tt = s2 % T2;
 #pragma unroll
                 for (int t = 0; t < MP / 16; ++t)
                     slot[t] = ABL_AT(bload4(rAt, vAt[tt] + 64 * t, (uint32_t)(p * NP * MP * 4)));
             };
+#endif
             // primal update of (agent p, tile tt) from its G (:73-93); iterate to LDS and Y[k]
             auto primal_update = [&](int s2, const f32x4& gp) {
                 const int p = s2 / T2, tt = s2 % T2;
@@ -432,6 +489,45 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                     bstore4_stream(urv, rUr, o);
                 }
             };
+#if DADMM_AT_DMA
+            constexpr int NQ = NS * 4;
+            // stores of one primal update (Y[k], and Grec / Urec when recording)
+            constexpr int SPQ = REC ? 3 : 1;
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2) {
+                compiler_fence();
+                if (s2 % T2 == 0) {
+                    const int p = s2 / T2;
+#pragma unroll
+                    for (int t = 0; t < MP / 16; ++t)
+                        rv[t] = *(const f32x4*)(Rlds + (p * BT + j) * RS + 4 * h + 16 * t);
+                }
+                f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int t = 0; t < MP / 16; ++t) {
+                    const int q = s2 * 4 + t;
+                    if (q + QD - 1 < NQ) dma_quarter(vAt, q + QD - 1);
+                    // quarter q has landed once no more than the VMEM ops issued after its DMA
+                    // are in flight: the later DMAs, and the primal updates' stores issued after
+                    // quarters u in [q - QD + 1, q - 1] with u = 3 mod 4, u >= 7 (chain >= 1)
+                    int younger = NQ - 1 - q < QD - 1 ? NQ - 1 - q : QD - 1;
+#pragma unroll
+                    for (int u = q - QD + 1; u < q; ++u)
+                        if (u >= 7 && (u & 3) == 3) younger += SPQ;
+                    wait_vm(younger);
+                    const f32x4 av = ABL_AT(*(const f32x4*)(Qlds + (w * QD + q % QD) * 256 + lane * 4));
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) gc = mfma4(av[r], rv[t][r], gc);
+                }
+                g[s2 & 1] = gc;
+                if (s2 + 1 == NS && k + 1 < a.K) {
+                    // next iteration's first GEMM1 steps, after every ring wait (so no wait has
+                    // to count them), before the last chain's Y stores
+                    for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
+                }
+                if (s2 > 0) primal_update(s2 - 1, g[(s2 - 1) & 1]);
+            }
+#else
             load_at(tring[0], 0);
 #pragma unroll
             for (int s2 = 0; s2 < NS; ++s2) {
@@ -439,7 +535,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                     load_at(tring[(s2 + 1) & 1], s2 + 1);
                 } else if (k + 1 < a.K) {
                     // next iteration's first GEMM1 steps: before the last chains' Y stores
-                    load_a(aring[0], 0);
+                    for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
                 }
                 compiler_fence();
                 if (s2 % T2 == 0) {
@@ -456,10 +552,11 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 g[s2 & 1] = gc;
                 if (s2 > 0) primal_update(s2 - 1, g[(s2 - 1) & 1]);
             }
+#endif
             primal_update(NS - 1, g[(NS - 1) & 1]);
             status |= bad_g ? 4u : 0u;
         } else if (k + 1 < a.K) {
-            load_a(aring[0], 0);
+            for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
         }
 #pragma unroll
         for (int p = 0; p < P; ++p) et_prev[p] = et[p];
@@ -505,7 +602,9 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
 template <int P, int NT, int GRAPH, int WV, bool REC>
 __global__ __launch_bounds__(WV * 64) void fused_forward_kernel(FusedArgs a) {
     constexpr int NP = NT * 64;
-    __shared__ __attribute__((aligned(16))) float lds[P * BT * ((NP + 4) + 2 * (M_PAD + 4))];
+    __shared__ __attribute__((aligned(16))) float lds[DADMM_AT_DMA
+        ? P * BT * ((NP + 4) + (M_PAD + 4)) + WV * DADMM_AT_QD * 256
+        : P * BT * ((NP + 4) + 2 * (M_PAD + 4))];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave id, in an SGPR
     if constexpr (WV == 4) {
         fused_body<P, NT, GRAPH, 4, 0, REC>(a, lds, w);
