@@ -60,6 +60,22 @@ __device__ __forceinline__ uint32_t fresh_s(uint32_t x) {
 }
 
 constexpr int WAVES = 8;
+// GEMM2's A^T operand through a per-wave LDS ring filled by LDS-DMA, as in the forward
+// (dadmm_fused.hip): BWD_QD quarter-chains of 1 KB per wave, BWD_QD - 1 in flight
+#ifndef DADMM_BWD_AT_DMA
+#define DADMM_BWD_AT_DMA 1
+#endif
+constexpr int BWD_QD = 5;
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n folded at compile time
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    }
+}
 
 // GNN variant: delta = clamp(delta, -20, 20) (gnn_dlasso_models_progressive.py:229) in place;
 // returns bit 4p+r set where the pre-clamp value was inside (the clamp passes the gradient)
@@ -93,6 +109,7 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
     float* __restrict__ Glds = lds;                 // [P][BT][YS]  gr_bar (GEMM B operand)
     float* __restrict__ Rlds = lds + P * BT * YS;   // [P][BT][RS]  A gr_bar
     float* __restrict__ red = Rlds + P * BT * RS;   // [WAVES][P][4] partial sums
+    float* __restrict__ Qlds = red + WAVES * P * 4;  // [WAVES][BWD_QD][256] A^T ring (DMA)
 
     const int lane = threadIdx.x & 63;
     const int j = lane & 15;
@@ -145,6 +162,14 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
     const uint32_t voffA = (uint32_t)(((16 * mb + j) * NP + 4 * h) * 4);
     const uint32_t voffAt = (uint32_t)((j * MP + 4 * h) * 4);
     const float* brow = Glds + j * YS + 4 * h;
+    // quarter q = 4 (p T2 + tt) + t: A^T_p rows of n-tile w T2 + tt, m-block t -> slot q % BWD_QD
+    auto dma_quarter = [&](int q) {
+        const int c = q >> 2, t = q & 3;
+        const int p = c / T2, tt = c % T2;
+        const uint32_t vAt = voffAt + (uint32_t)(16 * (w * T2 + tt) * MP * 4);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rAt, (lds_void*)(Qlds + (w * BWD_QD + q % BWD_QD) * 256), 16,
+                                                 vAt + 64 * t, (uint32_t)(p * NP * MP * 4), 0, 0);
+    };
     __syncthreads();
 
     for (int k = K - 1; k >= 0; --k) {
@@ -296,6 +321,12 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 #pragma unroll
                     for (int r = 0; r < 4; ++r) acc[i] = mfma4(av[t & 1][i][r], bv[r], acc[i]);
                 }
+                if constexpr (DADMM_BWD_AT_DMA) {
+                    if (t == NB - 1 && has_tiles) {   // GEMM2's first quarters, across the barrier
+#pragma unroll
+                        for (int q = 0; q + 1 < BWD_QD && q < P * T2 * 4; ++q) dma_quarter(q);
+                    }
+                }
             }
 #pragma unroll
             for (int i = 0; i < TH; ++i)
@@ -305,6 +336,34 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 
         // ---- GEMM2: y_bar_p += A_p^T R_p on this wave's n-tiles, as (agent, tile) chains of 16
         //      MFMAs; the A^T rows of the next chain load under the current one ----------------
+#if DADMM_BWD_AT_DMA
+        if (has_tiles) {
+            constexpr int NS = P * T2;
+            constexpr int NQ = NS * 4;
+            const int lane = threadIdx.x & 63;
+#pragma unroll
+            for (int c = 0; c < NS; ++c) {
+                const int p = c / T2, tt = c % T2;
+                f32x4 rv[MP / 16];
+#pragma unroll
+                for (int t = 0; t < MP / 16; ++t)
+                    rv[t] = *(const f32x4*)(Rlds + (p * BT + j) * RS + 4 * h + 16 * t);
+                f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int t = 0; t < MP / 16; ++t) {
+                    const int q = c * 4 + t;
+                    if (q + BWD_QD - 1 < NQ) dma_quarter(q + BWD_QD - 1);
+                    // no other VMEM op is issued in this loop: the younger ops are the later DMAs
+                    wait_vm(NQ - 1 - q < BWD_QD - 1 ? NQ - 1 - q : BWD_QD - 1);
+                    const f32x4 av = *(const f32x4*)(Qlds + (w * BWD_QD + q % BWD_QD) * 256 + lane * 4);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) gc = mfma4(av[r], rv[t][r], gc);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) yb[p][4 * tt + r] += gc[r];
+            }
+        }
+#else
         if (has_tiles) {
             constexpr int NS = P * T2;
             f32x4 tring[2][MP / 16];
@@ -335,6 +394,8 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
             }
         }
 
+#endif
+
         // ---- dhyp partial sums of iteration k: lane -> wave -> workgroup --------------------
 #pragma unroll
         for (int p = 0; p < P; ++p)
@@ -360,7 +421,8 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 template <int P, int NT, int GRAPH>
 __global__ __launch_bounds__(WAVES * 64) void backward_kernel(BackwardArgs a) {
     constexpr int NP = NT * 64;
-    __shared__ __attribute__((aligned(16))) float lds[P * BT * ((NP + 4) + (M_PAD + 4)) + WAVES * P * 4];
+    __shared__ __attribute__((aligned(16))) float lds[P * BT * ((NP + 4) + (M_PAD + 4)) + WAVES * P * 4 +
+                                                      (DADMM_BWD_AT_DMA ? WAVES * BWD_QD * 256 : 0)];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (w < 4)
         body<P, NT, GRAPH, 0>(a, lds, w);
