@@ -243,8 +243,8 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
         // Output (node p of sample s, columns c..c+3):
         //   BN(leaky(sum_q A_hat[s][p][q] Z[s, q][c] + bias[c])), BatchNorm on running statistics
         const int P = a.P;
-        float* ahs = zt + TM * ZS;
-        float* colp = ahs + a.S_t * P * P;
+        float* ahs = zt + TM * ZS;                     // [S_t][P][P]
+        float* colp = ahs + ((a.S_t * P * P + 3) & ~3);
 #pragma unroll
         for (int i = 0; i < WR; ++i)
 #pragma unroll
@@ -252,10 +252,40 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     zt[(16 * (wr * WR + i) + 4 * h + r) * ZS + 16 * (2 * wcol + c) + j] = acc[i][c][r];
-        const int nah = rows_t * P;                    // the tile's samples' A_hat rows
+        const int ns = rows_t / P;
         const float* agl = a.ahat + (a.ahat_per_sample ? (size_t)s0 * P * P : 0);
-        for (int i = threadIdx.x; i < nah; i += THREADS) ahs[i] = a.ahat_per_sample ? agl[i] : agl[i % (P * P)];
+        if (a.ahat_per_sample) {
+            for (int i = threadIdx.x; i < ns * P * P; i += THREADS) ahs[i] = agl[i];
+        } else {
+            for (int i = threadIdx.x; i < P * P; i += THREADS)
+                for (int sl = 0; sl < ns; ++sl) ahs[sl * P * P + i] = agl[i];
+        }
         const int cols = a.N - col0 < TN ? a.N - col0 : TN;
+        // the mix sum_q A_hat[p][q] Z[q] of 4 nodes x 4 columns per task: each q reads four A_hat
+        // words and one Z quad for 16 fma (one node x 4 columns per task read two LDS words per
+        // 4 fma and made the epilogue as long as the 400-deep GEMM). emit(row, col, sums).
+        auto mix = [&](auto&& emit) {
+            const int ng = (P + 3) >> 2;
+            for (int task = threadIdx.x; task < ns * ng * (TN / 4); task += THREADS) {
+                const int cq = task % (TN / 4), rest = task / (TN / 4);
+                const int g = rest % ng, sl = rest / ng;
+                const int c = 4 * cq;
+                if (c >= cols) continue;
+                const float* at[4];                    // rows 4g..4g+3 (clamped: never emitted)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) at[e] = ahs + (sl * P + (4 * g + e < P ? 4 * g + e : P - 1)) * P;
+                const float* zc = zt + sl * P * ZS + c;
+                f32x4 v[4] = {zero, zero, zero, zero};
+                for (int q = 0; q < P; ++q) {
+                    const f32x4 z = *(const f32x4*)(zc + q * ZS);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = __builtin_elementwise_fma((f32x4)(at[e][q]), z, v[e]);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (4 * g + e < P) emit(sl * P + 4 * g + e, c, v[e]);
+            }
+        };
         if constexpr (EPI == HYPER_EPI_GCN_TRAIN) {
             // training: BatchNorm on each sample's own statistics over its P nodes, then Dropout
             //   pass 1: M = A_hat Z + bias (LDS mt, and saved for the backward)
@@ -271,18 +301,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
                 colp[3 * TN + threadIdx.x] = a.bn_b[col];
             }
             __syncthreads();
-            for (int task = threadIdx.x; task < rows_t * (TN / 4); task += THREADS) {
-                const int r = task / (TN / 4), c = 4 * (task - r * (TN / 4));
-                if (c >= cols) continue;
-                const int sl = r / P;
-                const float* ah = ahs + r * P;
-                const float* zc = zt + sl * P * ZS + c;
-                f32x4 v = zero;
-                for (int q = 0; q < P; ++q) {
-                    const float w = ah[q];
-                    const f32x4 z = *(const f32x4*)(zc + q * ZS);
-                    v = v + w * z;
-                }
+            mix([&](int r, int c, f32x4 v) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = v[e] + colp[c + e];
                 *(f32x4*)(mt + r * ZS + c) = v;
@@ -292,9 +311,8 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
                 } else {
                     for (int e = 0; e < cols - c; ++e) dst[e] = v[e];
                 }
-            }
+            });
             __syncthreads();
-            const int ns = rows_t / P;
             for (int task = threadIdx.x; task < ns * TN; task += THREADS) {
                 const int sl = task / TN, c = task - sl * TN;
                 if (c >= cols) continue;
@@ -356,18 +374,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             colp[3 * TN + threadIdx.x] = a.bn_b[col];
         }
         __syncthreads();
-        for (int task = threadIdx.x; task < rows_t * (TN / 4); task += THREADS) {
-            const int r = task / (TN / 4), c = 4 * (task - r * (TN / 4));
-            if (c >= cols) continue;
-            const int sl = r / P;
-            const float* ah = ahs + r * P;             // row p of sample sl's block
-            const float* zc = zt + sl * P * ZS + c;
-            f32x4 v = zero;
-            for (int q = 0; q < P; ++q) {
-                const float w = ah[q];
-                const f32x4 z = *(const f32x4*)(zc + q * ZS);
-                v = v + w * z;
-            }
+        mix([&](int r, int c, const f32x4& v) {
             f32x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -381,7 +388,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             } else {
                 for (int e = 0; e < cols - c; ++e) dst[e] = o[e];
             }
-        }
+        });
     }
 }
 
@@ -456,7 +463,7 @@ template <int WR, int EPI, bool SPLIT>
 hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
     size_t lds = 0;
     if (EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN) {
-        lds = 4 * ((size_t)32 * WR * ZS + (size_t)a.S_t * a.P * a.P + 4 * TN);
+        lds = 4 * ((size_t)32 * WR * ZS + (((size_t)a.S_t * a.P * a.P + 3) & ~(size_t)3) + 4 * TN);
         if (EPI == HYPER_EPI_GCN_TRAIN) lds += 4 * ((size_t)32 * WR * ZS + 2 * (size_t)a.S_t * TN);
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void*)linear_kernel<WR, EPI, SPLIT>,
