@@ -20,8 +20,9 @@
 //   linear_kernel<MB, EPI_HEAD> : fc + sigmoid + clamps + maxima, written as hyp_k [B][4][H]
 //                                 (the reference's view(B, 4, H) layout);
 //   rownorm_kernel              : LayerNorm (+ LeakyReLU) of every row, one wave per row.
-// Tile: 16*MB rows (whole samples for the GCN epilogue) x 64 output columns, 4 waves (one
-// 16-column block each, all MB row blocks); operands stream from L2 through a register ring.
+// Tile: 32*WR rows (whole samples for the GCN epilogue) x 64 output columns, 4 waves in a 2 x 2
+// layout; operands stream through an LDS-DMA ring on long K loops, a per-wave register ring on
+// short ones.
 // Numerics: f32 throughout; results match torch's eager hypernetwork to f32 rounding (the sums
 // run in a different order than hipBLASLt's), not bit-for-bit.
 
@@ -56,6 +57,53 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // scheduling barrier: pins where the ring's loads issue (between the steps' MFMAs)
 __device__ __forceinline__ void mem_fence() { __builtin_amdgcn_sched_barrier(0); }
 
+// Main-loop operand staging. DMA = 1: the workgroup's A rows and W columns of a k-step go HBM/L2
+// -> LDS once (LDS-DMA, lane-linear 1 KB fragment images, DQ k-steps in flight) and every wave
+// reads its MFMA fragments from there; DMA = 0: each wave streams its own fragments into a
+// register ring (the two waves that share a row block, or a column block, both fetch it).
+#ifndef DADMM_HYPER_DMA
+#define DADMM_HYPER_DMA 1       // 0: never the DMA ring (A/B builds)
+#endif
+#ifndef DADMM_HYPER_DMA_MIN
+#define DADMM_HYPER_DMA_MIN 32  // k-steps per workgroup from which the DMA ring is used
+#endif
+#ifndef DADMM_HYPER_DQ
+#define DADMM_HYPER_DQ 4
+#endif
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, size_t bytes) {
+    const uint32_t nb = bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)nb, 0x00020000);
+}
+// one lane-linear 1 KB LDS-DMA: lane l's 16 bytes from voff land at lds + 16 l
+__device__ __forceinline__ void dma16(rsrc_t r, float* lds, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, 0, 0, 0);
+}
+// s_waitcnt vmcnt(n) for a runtime n (the wait counts of the DMA ring depend on the wave)
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+        case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    }
+}
+// this wave's LDS reads done, then the workgroup barrier (no vmcnt drain: DMAs stay in flight)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // XCD-aware tile order: the dispatcher deals blocks round-robin over the 8 XCDs (each with its
 // own L2); consecutive tile numbers — the column tiles of one row tile, which read the same input
 // rows — are given to blocks of one XCD.
@@ -70,9 +118,9 @@ __device__ __forceinline__ int xcd_tile(int bid, int G) {
 // accumulators). Operands stream from L2 into a register ring D k-steps (16 k) deep; rows past the
 // tile / columns past N load clamped (valid) rows whose results are never stored, so the main loop
 // has no masks; a K tail that is not a multiple of 16 runs as one masked step.
-template <int WR, int EPI, bool SPLIT>
+template <int WR, int EPI, bool SPLIT, bool DMA>
 __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
-    constexpr int D = 4;                           // operand ring depth (k-steps in flight)
+    [[maybe_unused]] constexpr int D = 4;          // register ring depth (k-steps in flight)
     constexpr int TM = 32 * WR;                    // rows per workgroup tile
     extern __shared__ __attribute__((aligned(16))) float zt[];   // GCN epilogue (dynamic)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -184,7 +232,96 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
         for (int u = 0; u < D; ++u)
             if (t0 + u < te) mma(ar[u], br[u]);
     };
-    if (SPLIT) {   // cat(x1, x2): K1 is a multiple of 16 (checked by the launcher)
+    if constexpr (DMA) {
+        // ring slot: the tile's NBA row blocks, then its 4 column blocks (16 x 16 floats each, as
+        // lane-linear fragment images: lane (j, h) of block q holds row/column 16 q + j, k 4h..4h+3)
+        constexpr int DQ = DADMM_HYPER_DQ;
+        constexpr int NBA = 2 * WR, NB = NBA + 4, NBW = (NB + 3) / 4, SLOT = NB * 256;
+        const int wu = __builtin_amdgcn_readfirstlane(w) & 3;   // provably uniform, in [0, 4)
+        const int nbw = NB % 4 == 0 ? NB / 4 : (NB - wu + 3) / 4;   // blocks this wave copies per k-step
+        const int T = t_end - t_begin, t1 = SPLIT ? K1 / 16 : KF;
+        const int kq = 4 * (lane >> 4);
+        const rsrc_t rx1 = make_rsrc(a.x1 + (size_t)row0 * a.ld1, (size_t)rows_t * a.ld1 * 4);
+        const rsrc_t rx2 = make_rsrc(SPLIT ? a.x2 + (size_t)row0 * a.ld2 : a.x1, SPLIT ? (size_t)rows_t * a.ld2 * 4 : 0);
+        const rsrc_t rw = make_rsrc(a.W, (size_t)a.N * K * 4);
+        uint32_t o1[NBW], o2[NBW];
+#pragma unroll
+        for (int i = 0; i < NBW; ++i) {
+            const int q = wu + 4 * i;
+            if (q < NBA) {
+                int r = 16 * q + j;
+                r = r < rows_t ? r : rows_t - 1;
+                o1[i] = (uint32_t)(((size_t)r * a.ld1 + kq) * 4);
+                o2[i] = SPLIT ? (uint32_t)(((size_t)r * a.ld2 + kq) * 4) : 0u;
+            } else {
+                int nn = col0 + 16 * (q - NBA) + j;
+                nn = nn < a.N ? nn : a.N - 1;
+                o1[i] = o2[i] = (uint32_t)(((size_t)nn * K + kq) * 4);
+            }
+        }
+        auto dma = [&](int t) {
+            float* slot = zt + ((t - t_begin) % DQ) * SLOT;
+            const bool seg2 = SPLIT && t >= t1;
+            const uint32_t ka = seg2 ? (uint32_t)(64 * t - 4 * K1) : (uint32_t)(64 * t);
+#pragma unroll
+            for (int i = 0; i < NBW; ++i) {
+                const int q = wu + 4 * i;
+                if (q < NBA) {
+                    if (seg2)
+                        dma16(rx2, slot + q * 256, o2[i] + ka);
+                    else
+                        dma16(rx1, slot + q * 256, o1[i] + ka);
+                } else if (q < NB) {
+                    dma16(rw, slot + q * 256, o1[i] + (uint32_t)(64 * t));
+                }
+            }
+        };
+        auto frag = [&](f32x4 (&fa)[WR], f32x4 (&fb)[2], int t) {
+            const float* slot = zt + ((t - t_begin) % DQ) * SLOT + 4 * lane;
+#pragma unroll
+            for (int i = 0; i < WR; ++i) fa[i] = *(const f32x4*)(slot + (wr * WR + i) * 256);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) fb[c] = *(const f32x4*)(slot + (NBA + 2 * wcol + c) * 256);
+        };
+        // step u: wait for step u + 1's copies (this wave's: the count of its younger DMAs), the
+        // barrier (every wave's), refill the slot step u - 1 left, then step u's MFMAs with step
+        // u + 1's fragment reads issued after the first quarter of them. Branch-free but for the
+        // refill (past the last step the wait is vmcnt(0) and the reads are of a stale slot, never
+        // used), so the compiler's LDS-read waits are exact and no MFMA waits for the next reads.
+        auto body = [&](int u, f32x4 (&fa)[WR], f32x4 (&fb)[2], f32x4 (&na)[WR], f32x4 (&nb)[2]) {
+            int younger = DQ - 2 < T - 2 - u ? DQ - 2 : T - 2 - u;
+            younger = younger > 0 ? younger : 0;
+            wait_vm(nbw * younger);
+            lds_barrier();
+            if (u + DQ < T) dma(t_begin + u + DQ);
+#pragma unroll
+            for (int i = 0; i < WR; ++i)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) acc[i][c] = mfma4(fa[i][0], fb[c][0], acc[i][c]);
+            mem_fence();
+            frag(na, nb, t_begin + u + 1);
+            mem_fence();
+#pragma unroll
+            for (int r = 1; r < 4; ++r)
+#pragma unroll
+                for (int i = 0; i < WR; ++i)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) acc[i][c] = mfma4(fa[i][r], fb[c][r], acc[i][c]);
+        };
+        if (T > 0) {
+            const int pre = T < DQ ? T : DQ;
+            for (int u = 0; u < pre; ++u) dma(t_begin + u);
+            wait_vm(nbw * (pre - 1));
+            lds_barrier();
+            f32x4 fa0[WR], fb0[2], fa1[WR], fb1[2];
+            frag(fa0, fb0, t_begin);
+            for (int u = 0; u < T; u += 2) {
+                body(u, fa0, fb0, fa1, fb1);
+                if (u + 1 < T) body(u + 1, fa1, fb1, fa0, fb0);
+            }
+            lds_barrier();   // the ring's last reads before the epilogue reuses the LDS
+        }
+    } else if constexpr (SPLIT) {   // cat(x1, x2): K1 is a multiple of 16 (checked by the launcher)
         const int t1 = K1 / 16;
         segment(a.x1, oa, 0, t_begin, t_end < t1 ? t_end : t1);
         segment(a.x2, ob, K1, t_begin > t1 ? t_begin : t1, t_end);
@@ -459,36 +596,43 @@ __global__ __launch_bounds__(THREADS) void rownorm_kernel(RowNormArgs a) {
     }
 }
 
-template <int WR, int EPI, bool SPLIT>
+template <int WR, int EPI, bool SPLIT, bool DMA>
 hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
-    size_t lds = 0;
-    if (EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN) {
-        lds = 4 * ((size_t)32 * WR * ZS + (((size_t)a.S_t * a.P * a.P + 3) & ~(size_t)3) + 4 * TN);
-        if (EPI == HYPER_EPI_GCN_TRAIN) lds += 4 * ((size_t)32 * WR * ZS + 2 * (size_t)a.S_t * TN);
-        if (lds > 64 * 1024) {
-            hipError_t e = hipFuncSetAttribute((const void*)linear_kernel<WR, EPI, SPLIT>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-        }
+    size_t lds = DMA ? 4 * (size_t)DADMM_HYPER_DQ * (2 * WR + 4) * 256 : 0;   // the ring
+    if (EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN) {   // the epilogue (reuses the ring)
+        size_t e = 4 * ((size_t)32 * WR * ZS + (((size_t)a.S_t * a.P * a.P + 3) & ~(size_t)3) + 4 * TN);
+        if (EPI == HYPER_EPI_GCN_TRAIN) e += 4 * ((size_t)32 * WR * ZS + 2 * (size_t)a.S_t * TN);
+        lds = e > lds ? e : lds;
     }
-    hipLaunchKernelGGL((linear_kernel<WR, EPI, SPLIT>), dim3(grid), dim3(THREADS), lds, st, a);
+    if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)linear_kernel<WR, EPI, SPLIT, DMA>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((linear_kernel<WR, EPI, SPLIT, DMA>), dim3(grid), dim3(THREADS), lds, st, a);
     return hipGetLastError();
 }
 
 template <int EPI, bool SPLIT>
-hipError_t launch_wr(int wr, int grid, const HyperArgs& a, hipStream_t st) {
+hipError_t launch_wr(int wr, bool dma, int grid, const HyperArgs& a, hipStream_t st) {
     switch (wr) {
-        case 1: return launch_one<1, EPI, SPLIT>(grid, a, st);
-        case 2: return launch_one<2, EPI, SPLIT>(grid, a, st);
-        case 4: return launch_one<4, EPI, SPLIT>(grid, a, st);
+        case 1: return launch_one<1, EPI, SPLIT, false>(grid, a, st);
+        case 2: return dma ? launch_one<2, EPI, SPLIT, true>(grid, a, st) : launch_one<2, EPI, SPLIT, false>(grid, a, st);
+        case 4: return dma ? launch_one<4, EPI, SPLIT, true>(grid, a, st) : launch_one<4, EPI, SPLIT, false>(grid, a, st);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <int EPI>
 hipError_t launch_epi(int wr, int grid, const HyperArgs& a, hipStream_t st) {
-    if (a.K1 < a.K) return launch_wr<EPI, true>(wr, grid, a, st);
-    return launch_wr<EPI, false>(wr, grid, a, st);
+    // the LDS-DMA ring pays for its per-step barrier on long K loops (configs[4]: the 2n-deep
+    // first GCN layer 360 -> 310 us, the split-K decoder 247 -> 185 us) and not on short ones
+    // (the 400-deep GCN layers: 191 -> 200 us)
+    const int per = (a.K / 16 + a.splits - 1) / a.splits;
+    const bool dma = DADMM_HYPER_DMA && per >= DADMM_HYPER_DMA_MIN;
+    if (a.K1 < a.K) return launch_wr<EPI, true>(wr, dma, grid, a, st);
+    return launch_wr<EPI, false>(wr, dma, grid, a, st);
 }
 
 }  // namespace hyper
