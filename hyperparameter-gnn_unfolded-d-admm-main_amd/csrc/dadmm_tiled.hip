@@ -64,9 +64,15 @@ constexpr int ST = HALVES * BT;      // samples per workgroup
 // MB = m-groups of 64 rows per agent (m_pad = 64 MB; MB in {1, 2}). The update phase works in
 // chunks of CH = 2 / MB n-tiles, so that a chunk's A^T rows (CH x 4 MB vectors) take the same
 // registers for both; with MB = 2 the GEMM2 B operand (R) is read from LDS, not held.
+// DADMM_TILED_DB (MB = 1): chunks of one n-tile, double-buffered (chunk c + 1's loads in flight
+// under chunk c's update) in the registers one 2-tile chunk took (160 VGPRs instead of 192)
+#ifndef DADMM_TILED_DB
+#define DADMM_TILED_DB 1
+#endif
 template <int MB>
 struct Chunk {                       // one chunk's operands
-    static constexpr int CH = 2 / MB;            // n-tiles per chunk of the update phase
+    static constexpr bool DB = DADMM_TILED_DB > 0 && MB == 1;
+    static constexpr int CH = DB ? 1 : 2 / MB;   // n-tiles per chunk of the update phase
     static constexpr int RG = CH * HALVES;       // row groups per chunk
     f32x4 yp[RG], up[RG], dv[RG];
     f32x4 atv[CH][4 * MB];
@@ -370,9 +376,21 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
             }
         }
     };
-    for (int c0 = 0; c0 < ntw; c0 += CH) {
-        if (c0 > 0) load_chunk(c0, cA);
-        compute_chunk(c0, cA);
+    if constexpr (Chunk<MB>::DB) {
+        Chunk<MB> cB;
+        for (int c0 = 0; c0 < ntw; c0 += 2 * CH) {
+            if (c0 + CH < ntw) load_chunk(c0 + CH, cB);
+            compute_chunk(c0, cA);
+            if (c0 + CH < ntw) {
+                if (c0 + 2 * CH < ntw) load_chunk(c0 + 2 * CH, cA);
+                compute_chunk(c0 + CH, cB);
+            }
+        }
+    } else {
+        for (int c0 = 0; c0 < ntw; c0 += CH) {
+            if (c0 > 0) load_chunk(c0, cA);
+            compute_chunk(c0, cA);
+        }
     }
     status |= (bad_u0 ? 2u : 0u) | (bad_g ? 4u : 0u) | (bad_y ? 8u : 0u);
     if (a.status != nullptr) {
