@@ -47,9 +47,12 @@ def L():
     return _lib.load()
 
 
+# the last three shapes take the LDS-DMA operand ring (>= 32 k-steps per workgroup) with 128-row
+# (9000 rows) and 64-row (6000 rows) tiles, a K tail (K % 16 = 8) and a split input
 @pytest.mark.parametrize("rows,K,N,K1", [(1, 4, 4, 4), (17, 20, 20, 20), (300, 100, 200, 100),
                                          (1024, 2000, 400, 2000), (1000, 512, 100, 256),
-                                         (129, 36, 65, 16)])
+                                         (129, 36, 65, 16), (9000, 1000, 400, 1000),
+                                         (9000, 1032, 400, 512), (6000, 600, 400, 600)])
 def test_linear_matches_torch(cuda, L, rows, K, N, K1):
     g = torch.Generator(device=cuda).manual_seed(rows + K)
     x = torch.randn(rows, K, device=cuda, generator=g)
@@ -77,7 +80,8 @@ def _ahat(nbr, P, dev):
 
 @pytest.mark.parametrize("B,P,K,N,per_sample", [(7, 5, 512, 100, True), (33, 5, 100, 200, False),
                                                 (9, 16, 200, 400, True), (3, 50, 400, 400, True),
-                                                (1, 1, 8, 4, False), (40, 2, 64, 36, True)])
+                                                (1, 1, 8, 4, False), (40, 2, 64, 36, True),
+                                                (512, 50, 1024, 100, True)])   # DMA ring, 128 rows
 def test_gcn_layer_matches_torch(cuda, L, B, P, K, N, per_sample):
     from dadmm_hip.graph import ingest
     G = B if per_sample else 1
