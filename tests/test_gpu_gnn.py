@@ -286,6 +286,38 @@ def test_guard_on_nonfinite_ynext_bit_exact(cuda, k_bad):
     assert np.array_equal(Yg, Yo)
 
 
+@pytest.mark.parametrize("k_bad", [0, 2])
+def test_guard_on_nan_gradient_bit_exact(cuda, k_bad):
+    """A NaN tau at iteration k_bad makes the gradient NaN: the reference zeroes the whole batch's
+    gradient (gnn_dlasso_models_progressive.py:216-218). The fused step forms the gradient
+    optimistically and its resolve launch redoes the update with G = 0; Y must match the oracle."""
+    P, m, n, B, K = 4, 16, 32, 8, 4
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", True)
+    model.eval()
+    model.hyper_backend = "torch"
+    orig = model.hypernetwork
+    calls = []
+
+    def patched(*args):
+        out = orig(*args)
+        if len(calls) == k_bad:
+            out[1][5, 2] = float("nan")   # tau of sample 5, agent 2
+        calls.append(1)
+        return out
+
+    model.hypernetwork = patched
+    rec = _recording(model)
+    with torch.no_grad():
+        Y, _ = model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in inits))
+    st = int(model.last_status.item())
+    table = _hyp_table(rec, B, P)
+    assert np.isnan(table[k_bad]).any()
+    y0, U0, d0 = inits
+    Yo, _, sto = O.forward_f32_gram(A, b, graphs, table, y0, U0, d0, variant=1, hyp_mode=1)
+    assert st == sto and st & 4
+    assert np.array_equal(Y[..., 0].cpu().numpy(), Yo)
+
+
 def test_train_mode_step_updates_bn_and_trains(cuda):
     """train(): dropout on, per-sample BatchNorm statistics, running stats updated B*K times per
     forward; loss.backward() + AdamW step run (progressive driver's loop, :196-214)."""
