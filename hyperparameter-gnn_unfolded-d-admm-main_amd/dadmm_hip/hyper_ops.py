@@ -147,16 +147,49 @@ def _hyper_params(model):
     return out
 
 
+_RS_WEIGHTS = {}
+
+
+def _rs_weights(T, m, device):
+    """m (1 - m)^(T-1-t), t = 0 .. T-1 (float64; cached per length, momentum and device)."""
+    key = (T, float(m), str(device))
+    w = _RS_WEIGHTS.get(key)
+    if w is None:
+        if len(_RS_WEIGHTS) > 64:
+            _RS_WEIGHTS.clear()
+        w = m * (1.0 - m) ** torch.arange(T - 1, -1, -1, device=device, dtype=torch.float64)
+        _RS_WEIGHTS[key] = w
+    return w
+
+
 def _update_running_stats(bn, mean, var, P):
-    """bn's running statistics after the reference's B sequential per-sample calls (train mode),
-    in closed form: r <- (1 - m) r + m s_b for b = 0 .. B-1 (unbiased variance)."""
-    B = mean.shape[0]
+    """bn's running statistics after the reference's sequential per-sample calls (train mode),
+    in closed form: r <- (1 - m) r + m s_t for t = 0 .. T-1 (unbiased variance). mean / var are
+    [T, N]: the B samples of one call, or those of several calls stacked in call order."""
+    T = mean.shape[0]
     m = bn.momentum
-    w = m * (1.0 - m) ** torch.arange(B - 1, -1, -1, device=mean.device, dtype=torch.float64)
-    decay = (1.0 - m) ** B
+    w = _rs_weights(T, m, mean.device)
+    decay = (1.0 - m) ** T
     bn.running_mean.copy_((decay * bn.running_mean.double() + w @ mean.double()).float())
     bn.running_var.copy_((decay * bn.running_var.double() + w @ (var.double() * (P / (P - 1)))).float())
-    bn.num_batches_tracked += B
+    bn.num_batches_tracked += T
+
+
+def flush_running_stats(model):
+    """Apply the BatchNorm running-statistics updates that training-mode hypernetwork calls with
+    ``defer=True`` queued on ``model`` — one closed-form update per layer over every queued call,
+    in call order (what the per-call updates give, without their per-iteration launches)."""
+    pending = getattr(model, "_bn_pending", None)
+    if not pending:
+        return
+    model._bn_pending = []
+    with torch.no_grad():
+        for i in range(len(pending[0][0])):
+            bn = pending[0][0][i][0]
+            P = pending[0][1]
+            mean = torch.cat([call[0][i][1] for call in pending])
+            var = torch.cat([call[0][i][2] for call in pending])
+            _update_running_stats(bn, mean, var, P)
 
 
 class HyperTrainFn(torch.autograd.Function):
@@ -169,7 +202,7 @@ class HyperTrainFn(torch.autograd.Function):
     for everything but the linears' plain GEMMs (dW = dZ^T X, dX = dZ W: hipBLASLt via torch)."""
 
     @staticmethod
-    def forward(ctx, AtAy, Atb, ahat, model, n, per_sample, seed, *params):
+    def forward(ctx, AtAy, Atb, ahat, model, n, per_sample, seed, defer, *params):
         L = _lib.load()
         B, P, ns = AtAy.shape
         dev = AtAy.device
@@ -185,6 +218,7 @@ class HyperTrainFn(torch.autograd.Function):
             xc = torch.cat([AtAy[..., :n], Atb[..., :n]], dim=2).reshape(rows, 2 * n).contiguous()
             x1, ld1, K1, x2, ld2, K = xc, 2 * n, 2 * n, None, 0, 2 * n
         saved = []          # per GCN layer: (M, mean, var)
+        stats = []          # per GCN layer: (bn, mean, var) for the running statistics
         xs = []             # per GCN layer: its input rows (None for layer 1: rebuilt from AtAy / Atb)
         with torch.cuda.device(dev):
             for i, (conv, bn) in enumerate(zip(convs, bns)):
@@ -198,8 +232,11 @@ class HyperTrainFn(torch.autograd.Function):
                     _ptr(conv.bias), _ptr(ahat), int(per_sample), _ptr(bn.weight), _ptr(bn.bias),
                     float(bn.eps), LEAKY_SLOPE, p_enc if i < 4 else 0.0, seed, i, _ptr(y), N, _ptr(M),
                     _ptr(mean), _ptr(var), stream))
-                with torch.no_grad():
-                    _update_running_stats(bn, mean, var, P)
+                if defer:
+                    stats.append((bn, mean, var))
+                else:
+                    with torch.no_grad():
+                        _update_running_stats(bn, mean, var, P)
                 saved.append((M, mean, var))
                 xs.append(None if i == 0 else x1)
                 x1, ld1, K1, x2, ld2, K = y, N, N, None, 0, N
@@ -235,6 +272,10 @@ class HyperTrainFn(torch.autograd.Function):
             mx = [float(model.alpha_max), float(model.tau_max), float(model.rho_max), float(model.eta_max)]
             _lib.check("dadmm_hyper_head_act", L.dadmm_hyper_head_act(
                 0, B, H, _ptr(z), None, *mx, _ptr(hyp), stream))
+        if defer:
+            if not hasattr(model, "_bn_pending"):
+                model._bn_pending = []
+            model._bn_pending.append((stats, P))
         ctx.model, ctx.n, ctx.per_sample, ctx.seed, ctx.mx = model, n, per_sample, seed, mx
         ctx.saved = saved
         ctx.xs, ctx.x5, ctx.dec_in, ctx.dec_xd, ctx.x3, ctx.z = xs, x5, dec_in, dec_xd, x, z
@@ -317,12 +358,14 @@ class HyperTrainFn(torch.autograd.Function):
             grads += [g[f"lin{blk}.w"], g[f"lin{blk}.b"], g[f"ln{blk}.w"], g[f"ln{blk}.b"]]
         grads += [g["fc.w"], g["fc.b"]]
         ctx.saved = ctx.xs = ctx.dec_in = ctx.dec_xd = None
-        return (dAtAy, None, None, None, None, None, None, *grads)
+        return (dAtAy, None, None, None, None, None, None, None, *grads)
 
 
-def hypernetwork_train(model, AtAy, Atb, n, ahat, per_sample, seed=None):
+def hypernetwork_train(model, AtAy, Atb, n, ahat, per_sample, seed=None, defer=False):
     """hyp_k [B, 4, H] of one iteration in training mode (HyperTrainFn); ``seed`` names the
-    dropout stream (default: drawn from torch's CPU generator, so torch.manual_seed fixes it)."""
+    dropout stream (default: drawn from torch's CPU generator, so torch.manual_seed fixes it).
+    defer: queue the BatchNorm running-statistics update on ``model`` for flush_running_stats
+    (the model's forward flushes once after its K iterations)."""
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-    return HyperTrainFn.apply(AtAy, Atb, ahat, model, n, per_sample, seed, *_hyper_params(model))
+    return HyperTrainFn.apply(AtAy, Atb, ahat, model, n, per_sample, seed, defer, *_hyper_params(model))

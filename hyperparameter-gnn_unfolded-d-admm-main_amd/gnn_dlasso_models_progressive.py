@@ -270,7 +270,8 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
                     self, AtAy, run.Atb, n, a_hat, not graphs.shared, bufs)
                 hyp_k = bufs.hyp
             elif train_hip:
-                hyp_k = hyper_ops.hypernetwork_train(self, AtAy, run.Atb, n, a_hat, not graphs.shared)
+                hyp_k = hyper_ops.hypernetwork_train(self, AtAy, run.Atb, n, a_hat, not graphs.shared,
+                                                     defer=True)
                 alpha_k, tau_k, rho_k, eta_k = (hyp_k[:, c].view(batch_size, H, 1, 1) for c in range(4))
             else:
                 alpha_k, tau_k, rho_k, eta_k = self.hypernetwork(AtAy[..., :n], Atb, a_hat)
@@ -279,6 +280,8 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
                 self.on_hyp(AtAy[..., :n], Atb, (alpha_k, tau_k, rho_k, eta_k))
             y, U, D = StepFn.apply(y, U, D, AtAy, hyp_k.contiguous(), run, k)
             ys.append(y)
+        if train_hip:   # the K iterations' BatchNorm running-statistics updates, in call order
+            hyper_ops.flush_running_stats(self)
         self.last_status = run.finish()
         Y = torch.stack(ys) if run.Y is None else run.Y
         Y = Y[..., :n].unsqueeze(-1)

@@ -198,6 +198,37 @@ def test_train_running_stats_match_sequential_updates(cuda):
         assert int(b1.num_batches_tracked) == int(b2.num_batches_tracked) == B
 
 
+def test_deferred_running_stats_match_per_call_updates(cuda):
+    """The model's forward queues every iteration's BatchNorm statistics and applies them once
+    (flush_running_stats): the same running statistics as one update per call, in call order."""
+    import copy
+
+    import gnn_dlasso_models_progressive as G
+    from dadmm_hip import hyper_ops
+    from dadmm_hip.graph import ingest
+    P, n, hidden, B, calls = 5, 32, 8, 9, 3
+    model, _, _ = _model(cuda, P, n, hidden, "diff", seed=4)
+    ref = copy.deepcopy(model)
+    graphs = [O.connected_er_graph(P, 0.5, seed=s) for s in range(B)]
+    gb = ingest(graphs, P, B, cuda)
+    ahat = G.normalized_adjacency(gb.nbr, P).contiguous()
+    g = torch.Generator(device=cuda).manual_seed(9)
+    with torch.no_grad():
+        for c in range(calls):
+            AtAy = torch.randn(B, P, n, device=cuda, generator=g)
+            Atb = torch.randn(B, P, n, device=cuda, generator=g)
+            hyper_ops.hypernetwork_train(model, AtAy, Atb, n, ahat, True, seed=c, defer=True)
+            hyper_ops.hypernetwork_train(ref, AtAy, Atb, n, ahat, True, seed=c, defer=False)
+        b0 = model.encoder.bn3.running_mean.clone()
+        hyper_ops.flush_running_stats(model)
+        assert not torch.equal(b0, model.encoder.bn3.running_mean)   # the flush applied them
+    for i in range(1, 6):
+        b1, b2 = getattr(model.encoder, f"bn{i}"), getattr(ref.encoder, f"bn{i}")
+        _close(b1.running_mean, b2.running_mean, rel=1e-5, name=f"bn{i}.running_mean")
+        _close(b1.running_var, b2.running_var, rel=1e-5, name=f"bn{i}.running_var")
+        assert int(b1.num_batches_tracked) == int(b2.num_batches_tracked) == B * calls
+
+
 def test_model_train_step_uses_hip_hypernetwork(cuda):
     """DLASSO_GNNHyp3_Progressive in train mode: forward + compute_loss + backward through the
     HIP hypernetwork; with dropout off it equals the torch backend (loss and gradients)."""
