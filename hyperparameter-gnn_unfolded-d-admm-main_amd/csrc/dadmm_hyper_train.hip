@@ -93,7 +93,7 @@ __global__ __launch_bounds__(THREADS) void gcn_bwd_kernel(GcnBwdArgs a) {
     }
 }
 
-// One wave per row, ROWNORM_BWD_ROWS rows per workgroup (16 per wave); per-lane column partials
+// One wave per row, ROWNORM_BWD_ROWS rows per workgroup (2 per wave); per-lane column partials
 // of dweight / dbias are combined across the 4 waves in LDS in wave order (deterministic).
 constexpr int CH = 8;   // C <= 64 * 4 * CH
 __global__ __launch_bounds__(THREADS) void rownorm_bwd_kernel(RowNormBwdArgs a) {

@@ -270,7 +270,7 @@ struct RowNormBwdArgs {
     int site;
 };
 hipError_t launch_rownorm_bwd(const RowNormBwdArgs& a, hipStream_t st);
-constexpr int ROWNORM_BWD_ROWS = 64;   // rows per partial-sum block
+constexpr int ROWNORM_BWD_ROWS = 8;    // rows per partial-sum block (2 per wave: B = 256 rows fill 32 workgroups)
 // GCN layer (train mode) backward, everything but the two GEMMs: from dy (w.r.t. the layer's
 // dropout output) to dZ (w.r.t. Z = x W^T), with per-sample partials of dgamma, dbeta, dbias
 struct GcnBwdArgs {

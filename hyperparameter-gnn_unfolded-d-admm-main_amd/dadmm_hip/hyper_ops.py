@@ -170,8 +170,9 @@ def _update_running_stats(bn, mean, var, P):
     m = bn.momentum
     w = _rs_weights(T, m, mean.device)
     decay = (1.0 - m) ** T
-    bn.running_mean.copy_((decay * bn.running_mean.double() + w @ mean.double()).float())
-    bn.running_var.copy_((decay * bn.running_var.double() + w @ (var.double() * (P / (P - 1)))).float())
+    w = w[:, None]   # weighted sums over the calls as multiply + reduce (a float64 GEMV is slow)
+    bn.running_mean.copy_((decay * bn.running_mean.double() + (w * mean.double()).sum(0)).float())
+    bn.running_var.copy_((decay * bn.running_var.double() + (w * (var.double() * (P / (P - 1)))).sum(0)).float())
     bn.num_batches_tracked += T
 
 
@@ -314,7 +315,7 @@ class HyperTrainFn(torch.autograd.Function):
                     B, N, _ptr(dx.contiguous()), _ptr(ctx.dec_xd[blk]), _ptr(lnd.weight), _ptr(lnd.bias),
                     float(lnd.eps), 1, float(model.decoder[4 * blk + 3].negative_slope),
                     float(model.decoder[4 * blk + 1].p), ctx.seed, 4 + blk, _ptr(dv), _ptr(part), stream))
-                pw = part[:(B + 63) // 64 * 2 * N].view(-1, 2, N).sum(0)
+                pw = part[:L.dadmm_hyper_rownorm_bwd_part_bytes(B, N) // 4].view(-1, 2, N).sum(0)
                 g[f"ln{blk}.w"], g[f"ln{blk}.b"] = pw[0], pw[1]
                 g[f"lin{blk}.w"] = dv.t() @ ctx.dec_in[blk]
                 g[f"lin{blk}.b"] = dv.sum(0)
@@ -328,7 +329,7 @@ class HyperTrainFn(torch.autograd.Function):
             _lib.check("dadmm_hyper_rownorm_bwd", L.dadmm_hyper_rownorm_bwd(
                 rows, C, _ptr(dx), _ptr(ctx.x5), _ptr(ln.weight), _ptr(ln.bias), float(ln.eps), 0, 0.0,
                 0.0, ctx.seed, 99, _ptr(de), _ptr(part), stream))
-            pw = part[:(rows + 63) // 64 * 2 * C].view(-1, 2, C).sum(0)
+            pw = part[:L.dadmm_hyper_rownorm_bwd_part_bytes(rows, C) // 4].view(-1, 2, C).sum(0)
             g["norm.w"], g["norm.b"] = pw[0], pw[1]
             dx = de
             for i in (4, 3, 2, 1, 0):

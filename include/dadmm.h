@@ -372,7 +372,7 @@ int dadmm_hyper_linear_ln(int32_t rows, int32_t K, int32_t N, const float* x, in
  *   (:94-105) in train mode; xd [rows][N] = the LayerNorm input (post-dropout), for the backward.
  * dadmm_hyper_rownorm_bwd: backward of LayerNorm (+ LeakyReLU when act) rows from their input xd:
  *   dx w.r.t. the pre-dropout values when drop_p > 0 (same seed / site as the forward), part =
- *   [ceil(rows / 64)][2][C] block partial sums of dweight, dbias (dadmm_hyper_rownorm_bwd_part_bytes).
+ *   [ceil(rows / 8)][2][C] block partial sums of dweight, dbias (dadmm_hyper_rownorm_bwd_part_bytes).
  * dadmm_hyper_head_act: mode 0: hyp [B][4H] = head(z) for the fc logits z (sigmoid, clamp
  *   [1e-4, 0.9999], * max_c, clamp <= 0.9999 for tau / rho / eta: :167-196); mode 1: out = dz =
  *   dhyp * head'(z). */
