@@ -392,9 +392,11 @@ __global__ __launch_bounds__(THREADS) void finish_kernel(GnnArgs a) {
 }
 
 // ---- adjoint of one iteration (no guard fired) ---------------------------------------------------
-// One wave per sample (lanes = columns, all P agents per lane: the consensus and its adjoint are
-// lane-local); the per-sample hyper-parameter gradients reduce over the sample's columns (wave
-// shuffles per 64-column chunk, accumulated in LDS in chunk order: deterministic).
+// One workgroup per sample, its 4 waves on the sample's 64-column chunks w, w + 4, ... (lanes =
+// columns, all P agents per lane: the consensus and its adjoint are lane-local); the per-sample
+// hyper-parameter gradients reduce over the columns: wave shuffles per chunk, accumulated per wave
+// in LDS in chunk order, then the 4 waves' sums in wave order (deterministic). (One wave per sample
+// left most CUs idle at training batch sizes: B = 256 samples filled 64 workgroups.)
 __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k, GnnGrads gg) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int P = a.P, n = a.n, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -407,8 +409,7 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
     float* red = sl + 3 * P * 64;              // [4][H] per-sample hyp gradient
     int32_t* vpl = (int32_t*)(red + 4 * P);    // the sample's visit lists: starts [P + 1], entries
     uint8_t* vql = (uint8_t*)(vpl + P + 1);
-    const int s = blockIdx.x * WAVES + wv;
-    if (s >= a.B) return;                      // whole waves only: no block barrier below
+    const int s = blockIdx.x;
     float gclip, vclip;
     clips(a, k, gclip, vclip);
     const float* ys = a.yk;
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
         for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0) red[c * H + (H == 1 ? 0 : p)] += v;
     };
-    for (int c0 = 0; c0 < n; c0 += 64) {
+    for (int c0 = 64 * wv; c0 < n; c0 += 64 * WAVES) {
         const int c = c0 + lane;
         const bool cv = c < n;
         const size_t base = (size_t)s * P * n + c;
@@ -505,7 +506,12 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
             accum(2, p, pr);
         }
     }
-    for (int i = lane; i < 4 * H; i += 64) gg.ghyp[(size_t)s * 4 * H + i] = red[i];
+    __syncthreads();
+    const int SW = 3 * P * 64 + 4 * P + VW;     // floats per wave slice
+    for (int i = threadIdx.x; i < 4 * H; i += THREADS) {
+        const float* r0 = lds + 3 * P * 64 + i;
+        gg.ghyp[(size_t)s * 4 * H + i] = ((r0[0] + r0[SW]) + r0[2 * SW]) + r0[3 * SW];
+    }
 }
 
 }  // namespace gnn
@@ -568,7 +574,7 @@ hipError_t gnn_launch_step_backward(const GnnArgs& a, int k, const GnnGrads& gg,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(gnn::step_backward_kernel, dim3((a.B + gnn::WAVES - 1) / gnn::WAVES),
+    hipLaunchKernelGGL(gnn::step_backward_kernel, dim3(a.B),
                        dim3(gnn::THREADS), lds, st, a, k, gg);
     return hipGetLastError();
 }
