@@ -538,7 +538,9 @@ int dadmm_graph_generate(int32_t B, int32_t P, float prob, uint64_t seed, int32_
 
 size_t dadmm_tiled_scratch_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;
-    return 3 * align256(sizeof(float) * (size_t)d->B * d->P * d->n);   // U ping-pong, delta
+    // U ping-pong, delta; R_k of the column-split path
+    return 3 * align256(sizeof(float) * (size_t)d->B * d->P * d->n) +
+           align256(sizeof(float) * (size_t)d->B * d->P * m_pad_of(d));
 }
 
 int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
@@ -579,6 +581,7 @@ int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
     a.Ubuf[0] = (float*)scratch;
     a.Ubuf[1] = (float*)((char*)scratch + state);
     a.delta = (float*)((char*)scratch + 2 * state);
+    a.R = (float*)((char*)scratch + 3 * state);
     a.U_out = U_out;
     a.status = status;
     a.B = d->B;

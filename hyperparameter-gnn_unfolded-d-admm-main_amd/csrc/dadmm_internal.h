@@ -162,6 +162,7 @@ struct TiledArgs {
     float* Y;               // [K][B][P][n]
     float* Ubuf[2];         // ping-pong U_k buffers [B][P][n] (scratch)
     float* delta;           // delta_k [B][P][n] (scratch, consensus_kernel)
+    float* R;               // R_k = A_p y_k - b_p [B][P][m_pad] (scratch, the column-split path)
     float* U_out;           // [B][P][n] or nullptr
     int32_t* status;        // or nullptr (OR-ed DADMM_STATUS_* bits)
     int B, P, m, m_pad, n, n_pad, K, hyp_rows, variant, graph_shared;

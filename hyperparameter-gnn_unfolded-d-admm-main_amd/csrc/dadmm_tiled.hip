@@ -23,6 +23,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "dadmm_internal.h"
 
@@ -101,7 +102,9 @@ constexpr int STAGE_NP_MAX = 512;
 // Workgroup = (32-sample tile, agent p).
 // amdgpu_waves_per_eu(2): keeps VGPRs + AGPRs <= 256 (two workgroups per CU); without it the
 // allocator lands at 249 + 8 and the kernel runs at one wave per SIMD (0.40 -> 0.53 ms/iteration)
-template <bool STAGE, int MB>
+// RONLY (the column-split path): GEMM1 only, R_k -> a.R [B][P][m_pad]; the update runs in
+// colupdate_kernel
+template <bool STAGE, int MB, bool RONLY = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) void iter_kernel(TiledArgs a, int k) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int MP = 64 * MB;                      // padded rows per agent (a.m_pad)
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
         }
     };
     Chunk<MB> cA;
-    if (ntw > 0) load_chunk(0, cA);
+    if (!RONLY && ntw > 0) load_chunk(0, cA);
 
     if constexpr (STAGE) {
         if (!final_only) {
@@ -272,9 +275,24 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
                 for (int u = 0; u < D; ++u) step(u);   // the last D steps (T % D == 0)
             }
 #pragma unroll
-            for (int hh = 0; hh < HALVES; ++hh)
-                *(f32x4*)(Rlds + (hh * BT + j) * RS + 16 * mq + 4 * h) = acc[hh];
+            for (int hh = 0; hh < HALVES; ++hh) {
+                if constexpr (RONLY) {
+                    const int s = tile * ST + hh * BT + j;
+                    if (s < B) *(f32x4*)(a.R + ((size_t)s * P + p) * MP + 16 * mq + 4 * h) = acc[hh];
+                } else {
+                    *(f32x4*)(Rlds + (hh * BT + j) * RS + 16 * mq + 4 * h) = acc[hh];
+                }
+            }
         }
+    }
+    if constexpr (RONLY) {
+        if (a.status != nullptr) {
+            uint32_t ws = status;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) ws |= __shfl_xor(ws, o);
+            if (lane == 0 && ws) atomicOr((unsigned int*)a.status, ws);
+        }
+        return;
     }
     __syncthreads();
 
@@ -441,6 +459,230 @@ __global__ __launch_bounds__(THREADS) void consensus_kernel(TiledArgs a, const f
     }
 }
 
+
+// ---- column-split path: GEMM1 per (tile, agent), then one update kernel per (tile, column block)
+// that holds every agent of its samples, so the consensus is formed in LDS and neither delta_k
+// nor a second copy of y_k goes through HBM. Per iteration: iter_kernel<., ., RONLY> reads y_k and
+// b and writes R_k (m_pad floats per sample-agent), colupdate_kernel reads y_k, U_{k-1} and R_k
+// and writes y_{k+1} and U_k: the algorithmic streams plus R.
+//
+// Workgroup = (ST2 = 32 samples, CW columns) x all P agents. y_k[s][*][c0, c0 + CW) is copied
+// HBM -> LDS by LDS-DMA (row sl = one sample, P CW floats, 16-byte chunk c stored at chunk
+// c ^ (sl & 15) of its row: the 16 lanes of an MFMA column block read 16 distinct chunks of an
+// aligned 256 B run). Wave w takes agents w, w + 4, ...; per agent it holds R_p of both 16-sample
+// halves (GEMM2's B operand) and per 16-column n-tile A_p^T's rows (its A operand). A lane
+// (j, h) owns columns c0 + 16 nt + 4h .. + 3 of sample j of each half: delta_k by the sample's
+// visit list over the LDS rows (the consensus kernel's order), the deferred dual update, the
+// GEMM2 chain and the primal update, exactly as iter_kernel.
+constexpr int ST2 = 2 * BT;
+// DADMM_CS_ABL (timing builds only, wrong results): 1 = no consensus walk, 2 = no R / A^T loads,
+// 4 = no y-block DMA
+#ifndef DADMM_CS_ABL
+#define DADMM_CS_ABL 0
+#endif
+size_t colsplit_lds_bytes(int P, int CW, int vcap) {
+    return 4 * (size_t)ST2 * P * CW + 4 * (size_t)(ST2 * P + 1) + (size_t)vcap;
+}
+constexpr int AMAX = 4;     // agents per wave of the column-split path (P <= 16)
+template <int MB, int NT>   // NT = CW / 16 n-tiles per column block
+__global__ __launch_bounds__(THREADS) void colupdate_kernel(TiledArgs a, int k, int vcap) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int MP = 64 * MB, TM = MP / 16;
+    constexpr int CW = 16 * NT;
+    const int P = a.P, n = a.n, B = a.B, NP = a.n_pad, H = a.hyp_rows;
+    const int ncb = (n + CW - 1) / CW;
+    const int wg = xcd_swizzle(blockIdx.x, gridDim.x);   // a tile's column blocks on one XCD
+    const int tile = wg / ncb, c0 = (wg % ncb) * CW;
+    const int s0 = tile * ST2, ns = min(ST2, B - s0);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = lane & 15, h = lane >> 4;
+    const int CQ = CW / 4, RC = P * CQ;                  // 16-byte chunks per agent / per LDS row
+    float* ys = lds;                                     // [ST2][RC] chunks, swizzled
+    int32_t* vp = (int32_t*)(ys + (size_t)ST2 * RC * 4); // visit-list starts, local
+    uint8_t* vql = (uint8_t*)(vp + ST2 * P + 1);
+    const size_t S = (size_t)B * P * n;
+    const float* yk = k == 0 ? a.y0 : a.Y + (size_t)(k - 1) * S;
+    const bool final_only = k == a.K;
+
+    {   // y_k block -> LDS (no VGPRs held; past-the-range offsets return zeros)
+        const rsrc_t ry = make_rsrc(yk, (uint32_t)(S * 4));
+        for (int base = w * 64; base < ST2 * RC; base += WAVES * 64) {
+            const int lc = base + lane;
+            const int sl = lc / RC, cs = (lc % RC) ^ (sl & 15);
+            const int p = cs / CQ, c = c0 + 4 * (cs % CQ);
+            const uint32_t off = (sl < ns && c < n)
+                                     ? (uint32_t)((((size_t)(s0 + sl) * P + p) * n + c) * 4)
+                                     : 0x80000000u;
+            if (!(DADMM_CS_ABL & 4))
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (lds_void*)(ys + 4 * base), 16, off, 0, 0, 0);
+        }
+    }
+    // visit lists of the tile's samples (one list for a shared graph)
+    const int nl = a.graph_shared ? P : ns * P;
+    const int g0 = a.graph_shared ? 0 : s0 * P;
+    const int vbase = a.vptr[g0];
+    const int nent = a.vptr[g0 + nl] - vbase;
+    const bool vin = nent <= vcap;
+    for (int i = threadIdx.x; i <= nl; i += THREADS) vp[i] = a.vptr[g0 + i] - vbase;
+    if (vin)
+        for (int i = threadIdx.x; i < nent; i += THREADS) vql[i] = a.vq[vbase + i];
+    const uint8_t* vq = vin ? (const uint8_t*)vql : a.vq + vbase;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    auto yl = [&](int sl, int p, int g) -> f32x4 {   // columns c0 + 4g .. of agent p, sample row sl
+        return *(const f32x4*)(ys + 4 * ((size_t)sl * RC + ((p * CQ + g) ^ (sl & 15))));
+    };
+    float vclip_prev = 0.0f, gtmp;
+    if (k > 0) clips(a.variant, k - 1, gtmp, vclip_prev);
+    float gclip = 0.0f, vclip = 0.0f;
+    if (!final_only) clips(a.variant, k, gclip, vclip);
+    const float* usrc = k == 0 ? a.U0 : a.Ubuf[0];
+    float* Ucur = final_only ? a.U_out : a.Ubuf[0];       // in place: U_{k-1} -> U_k
+    float* Yk = a.Y + (size_t)k * S;
+    uint32_t status = 0;
+    bool bad_u0 = false, bad_g = false, bad_y = false;
+
+#pragma unroll
+    for (int ai = 0; ai < AMAX; ++ai) {
+        const int p = w + WAVES * ai;
+        if (p >= P) break;
+        const int hp = H == 1 ? 0 : p;
+        float al = 0, ta = 0, rh = 0, et_prev = 0;
+        if (!final_only) {
+            const float* hk = a.hyp + ((size_t)k * H + hp) * 4;
+            al = hk[0]; ta = hk[1]; rh = hk[2];
+            const float et = hk[3];
+            status |= (finitef(al) && finitef(ta) && finitef(rh) && finitef(et)) ? 0u : 8u;
+        }
+        if (k > 0) et_prev = a.hyp[((size_t)(k - 1) * H + hp) * 4 + 3];
+        // every global operand of this agent is issued first (R_p, A_p^T rows, U_{k-1}, d0); the
+        // consensus over the LDS block runs under their latency
+        f32x4 rv[HALVES][TM], at[NT][TM], up[NT][HALVES], dv[NT][HALVES], yv[NT][HALVES];
+        float dg[HALVES];
+        bool okr[NT][HALVES];
+        size_t off[NT][HALVES];
+#pragma unroll
+        for (int hh = 0; hh < HALVES; ++hh) {
+            const int s = s0 + hh * BT + j;
+            dg[hh] = s < B ? a.deg[(a.graph_shared ? 0 : s * P) + p] : 0.0f;
+#pragma unroll
+            for (int t = 0; t < TM; ++t)
+                rv[hh][t] = (!final_only && s < B && !(DADMM_CS_ABL & 2))
+                                ? *(const f32x4*)(a.R + ((size_t)s * P + p) * MP + 16 * t + 4 * h)
+                                : (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int col = c0 + 16 * nt + 4 * h;
+            if (DADMM_CS_ABL & 2) {
+#pragma unroll
+                for (int t = 0; t < TM; ++t) at[nt][t] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+            } else if (!final_only) {
+                const float* atp = a.At + ((size_t)p * NP + c0 + 16 * nt + j) * MP + 4 * h;
+#pragma unroll
+                for (int t = 0; t < TM; ++t) at[nt][t] = *(const f32x4*)(atp + 16 * t);
+            }
+#pragma unroll
+            for (int hh = 0; hh < HALVES; ++hh) {
+                const int sl = hh * BT + j, s = s0 + sl;
+                okr[nt][hh] = s < B && col < n;
+                off[nt][hh] = ((size_t)(okr[nt][hh] ? s : 0) * P + p) * n + (okr[nt][hh] ? col : 0);
+                up[nt][hh] = dv[nt][hh] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+                if (okr[nt][hh]) {
+                    up[nt][hh] = *(const f32x4*)(usrc + off[nt][hh]);
+                    if (k == 0) dv[nt][hh] = *(const f32x4*)(a.d0 + off[nt][hh]);
+                }
+                yv[nt][hh] = yl(sl, p, 4 * nt + h);
+            }
+        }
+        if (k > 0 && !(DADMM_CS_ABL & 1)) {   // delta_k = compute_delta(y_k) (unfolded_DLASSO.py:127-140), both halves'
+                       // lists walked together, each element's chain in its list's order
+            int v0[HALVES], len[HALVES], lmax = 0;
+#pragma unroll
+            for (int hh = 0; hh < HALVES; ++hh) {
+                const int sl = hh * BT + j;
+                const int li = a.graph_shared ? p : sl * P + p;
+                v0[hh] = vp[li];
+                len[hh] = s0 + sl < B ? vp[li + 1] - v0[hh] : 0;
+                lmax = max(lmax, len[hh]);
+            }
+            for (int t = 0; t < lmax; ++t) {
+#pragma unroll
+                for (int hh = 0; hh < HALVES; ++hh) {
+                    if (t < len[hh]) {
+                        const int q = (int)vq[v0[hh] + t];
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) {
+                            const f32x4 yq = yl(hh * BT + j, q, 4 * nt + h);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                dv[nt][hh][r] = dv[nt][hh][r] + (yv[nt][hh][r] - yq[r]);
+                        }
+                    }
+                }
+            }
+            if (a.variant != 0) {
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            dv[nt][hh][r] = tclamp(dv[nt][hh][r], -20.0f, 20.0f);   // :229
+            }
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+            for (int hh = 0; hh < HALVES; ++hh) {
+                const bool ok = okr[nt][hh];
+                f32x4 uv;
+                if (k == 0) {
+                    uv = up[nt][hh];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) bad_u0 |= ok && !finitef(uv[r]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        uv[r] = tclamp(up[nt][hh][r] + dv[nt][hh][r] * et_prev, -vclip_prev, vclip_prev);
+                }
+                if (ok) *(f32x4*)(Ucur + off[nt][hh]) = uv;           // U_k
+                if (final_only) continue;
+                f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};                  // GEMM2 rows of this n-tile
+#pragma unroll
+                for (int t = 0; t < TM; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) gc = mfma4(at[nt][t][r], rv[hh][t][r], gc);
+                if (ok) {
+                    f32x4 yn;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float y = yv[nt][hh][r];
+                        const float st = sign_times(y, ta);
+                        float gr = gc[r] + st;
+                        gr = gr + uv[r] * dg[hh];
+                        gr = gr + dv[nt][hh][r] * rh;
+                        bad_g |= gr != gr;
+                        gr = tclamp(gr, -gclip, gclip);
+                        const float v = tclamp(y - al * gr, -vclip, vclip);
+                        bad_y |= !finitef(v);
+                        yn[r] = v;
+                    }
+                    *(f32x4*)(Yk + off[nt][hh]) = yn;
+                }
+            }
+        }
+    }
+    status |= (bad_u0 ? 2u : 0u) | (bad_g ? 4u : 0u) | (bad_y ? 8u : 0u);
+    if (a.status != nullptr) {
+        uint32_t ws = status;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) ws |= __shfl_xor(ws, o);
+        if (lane == 0 && ws) atomicOr((unsigned int*)a.status, ws);
+    }
+}
+
 }  // namespace tiled
 
 size_t tiled_lds_bytes(int n_pad, int m_pad) {
@@ -448,8 +690,69 @@ size_t tiled_lds_bytes(int n_pad, int m_pad) {
     return stage + 4 * (size_t)(tiled::ST * (m_pad + 4));
 }
 
+// DADMM_TILED_SPLIT=1 builds the column-split form (iter_kernel<., ., RONLY> + colupdate_kernel)
+// instead of the two-launch (consensus + iteration kernel) form. Bit-identical; measured slower at
+// configs[2] (7.4 vs 6.9 ms per forward), so off by default.
+#ifndef DADMM_TILED_SPLIT
+#define DADMM_TILED_SPLIT 0
+#endif
+// the column block of the split path: the widest of 64 / 32 / 16 columns whose LDS (y block of
+// 32 samples x P agents + visit lists) keeps two workgroups per CU, else the narrowest that fits
+// one; 0 = the split path does not apply. The swizzle needs P CW / 4 to be a multiple of 16.
+static int colsplit_width(int P, int vcap) {
+#ifdef DADMM_CS_CW   // timing builds: a fixed column block
+    if (tiled::colsplit_lds_bytes(P, DADMM_CS_CW, vcap) <= 160 * 1024) return DADMM_CS_CW;
+#endif
+    int best = 0;
+    for (int cw : {64, 32, 16}) {
+        if ((P * cw / 4) % 16 != 0) continue;
+        const size_t l = tiled::colsplit_lds_bytes(P, cw, vcap);
+        if (l <= 80 * 1024) return cw;
+        if (l <= 160 * 1024) best = cw;
+    }
+    return best;
+}
+
+static hipError_t launch_colsplit(const TiledArgs& a, int CW, int vcap, hipStream_t stream) {
+    const size_t lds = tiled_lds_bytes(a.n_pad, a.m_pad);
+    const bool stage = a.n_pad <= tiled::STAGE_NP_MAX;
+    auto gk = a.m_pad == 64 ? (stage ? tiled::iter_kernel<true, 1, true> : tiled::iter_kernel<false, 1, true>)
+                            : (stage ? tiled::iter_kernel<true, 2, true> : tiled::iter_kernel<false, 2, true>);
+    decltype(&tiled::colupdate_kernel<1, 1>) uk;
+    if (a.m_pad == 64)
+        uk = CW == 64 ? tiled::colupdate_kernel<1, 4> : CW == 32 ? tiled::colupdate_kernel<1, 2> : tiled::colupdate_kernel<1, 1>;
+    else
+        uk = CW == 64 ? tiled::colupdate_kernel<2, 4> : CW == 32 ? tiled::colupdate_kernel<2, 2> : tiled::colupdate_kernel<2, 1>;
+    const size_t ulds = tiled::colsplit_lds_bytes(a.P, CW, vcap);
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)gk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    if (ulds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)uk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ulds);
+        if (e != hipSuccess) return e;
+    }
+    const int gitems = ((a.B + tiled::ST - 1) / tiled::ST) * a.P;
+    const int uitems = ((a.B + tiled::ST2 - 1) / tiled::ST2) * ((a.n + CW - 1) / CW);
+    for (int k = 0; k <= a.K; ++k) {
+        if (k == a.K && a.U_out == nullptr) break;   // k == K: the final dual update (U_out)
+        if (k < a.K)
+            hipLaunchKernelGGL(gk, dim3(gitems), dim3(tiled::THREADS), lds, stream, a, k);
+        hipLaunchKernelGGL(uk, dim3(uitems), dim3(tiled::THREADS), ulds, stream, a, k, vcap);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream) {
     const size_t lds = tiled_lds_bytes(a.n_pad, a.m_pad);
+    const char* env = getenv("DADMM_TILED_SPLIT");   // runtime override of the build default
+    const bool split = env != nullptr ? atoi(env) != 0 : DADMM_TILED_SPLIT != 0;
+    if (split && a.R != nullptr && a.n_pad % 64 == 0 && (a.m_pad == 64 || a.m_pad == 128) &&
+        lds <= 160 * 1024) {
+        const int vcap = 8192;
+        const int CW = a.P <= tiled::AMAX * tiled::WAVES ? colsplit_width(a.P, vcap) : 0;
+        if (CW > 0) return launch_colsplit(a, CW, vcap, stream);
+    }
     if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
     if (a.n_pad % 64 != 0) return hipErrorInvalidValue;   // the swizzle and GEMM ring assume it
     if (a.m_pad != 64 && a.m_pad != 128) return hipErrorInvalidValue;   // MB in {1, 2}

@@ -45,7 +45,7 @@ for it in range(12):
     Y = out[0] if isinstance(out, tuple) else out
     if ref is None:
         ref = Y.clone()
-    elif not torch.equal(ref, Y):
+    elif not torch.equal(ref, Y) and not os.environ.get("DADMM_ABLATION"):
         raise SystemExit("nondeterministic output")
 print(json.dumps({"lib": os.path.basename(os.environ.get("DADMM_LIB_VARIANT", "libdadmm.so")),
                   "cfg": [P, n, m, B, K, prob, per_sample, path], "median_ms": float(np.median(ts)),

@@ -195,6 +195,30 @@ def test_configs2_full_depth_bit_exact(cuda):
     assert np.array_equal(U, Uo)
 
 
+@pytest.mark.parametrize("shape", [
+    (16, 64, 512, 40, 6, 0.3, False, 0),   # configs[2] agents and size, per-sample graphs
+    (16, 100, 500, 33, 4, 0.3, True, 0),    # two m-groups, ragged n and B, shared graph
+    (9, 64, 320, 20, 5, 0.5, False, 1),     # odd P, the GNN variant's clamps
+])
+def test_tiled_column_split_bit_exact(cuda, shape, monkeypatch):
+    """The column-split form of the tiled path (DADMM_TILED_SPLIT=1: GEMM1 per (tile, agent),
+    then one update kernel per (tile, column block) that forms delta_k in LDS) against the
+    oracle, U_K included (the final dual update launch)."""
+    P, m, n, B, K, prob, shared, variant = shape
+    monkeypatch.setenv("DADMM_TILED_SPLIT", "1")
+    A, b, _ = O.make_problem(P, m, n, B, seed=900 + P)
+    graphs = ([O.er_graph(P, prob, seed=5)] * B if shared
+              else [O.connected_er_graph(P, prob, seed=100 + s) for s in range(B)])
+    y0, U0, d0 = _inits(B, P, n, seed=P)
+    rng = np.random.default_rng(K)
+    hyp = O.hyp_table((0.4 * rng.standard_normal((K, P, 4))).astype(np.float32), MAXP)
+    Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0, path="tiled", variant=variant)
+    Yo, Uo, sto = O.forward_f32(A, b, graphs, hyp, y0, U0, d0, variant=variant)
+    assert st == sto == 0
+    assert np.array_equal(Y, Yo), f"max |diff| {np.abs(Y - Yo).max()}"
+    assert np.array_equal(U, Uo)
+
+
 @pytest.mark.parametrize("path", ["auto", "stepwise", "tiled"])
 def test_same_mode_and_gnn_variant(cuda, path):
     """'same' hyper-parameters (H = 1) and the GNN variant's fixed clamps / delta clamp."""
