@@ -165,7 +165,10 @@ size_t dadmm_tiled_scratch_bytes(const dadmm_dims* d);
  * delta_k for every agent of a sample from y_k (visit lists, the reference's order; scratch), then
  * each (32-sample tile, agent) workgroup applies the deferred dual update, the factored gradient
  * GEMM pair and the primal update; Y is bit-identical to dadmm_forward_stepwise's on guard-free
- * inputs. Scratch: the U_k ping-pong pair and delta_k (dadmm_tiled_scratch_bytes).
+ * inputs. Scratch: the U_k ping-pong pair, delta_k and R_k (dadmm_tiled_scratch_bytes).
+ * Environment DADMM_TILED_SPLIT=1 selects the column-split form instead (P <= 16): a GEMM1 launch
+ * writes R_k = A_p y_k - b_p, then one launch per iteration takes a (32-sample, column block) x all
+ * agents, forms delta_k in LDS and applies the updates; bit-identical, slower at configs[2].
  * Replaces: the same loop as dadmm_forward (unfolded_DLASSO.py:45, 53-109).
  * Like dadmm_forward it only FLAGS the reference's guards in `status` (OR-ed; caller zeroes it):
  * enqueue dadmm_forward_stepwise with DADMM_GATE_ON behind it for the exact guarded result.
