@@ -481,7 +481,7 @@ constexpr int ST2 = 2 * BT;
 #define DADMM_CS_ABL 0
 #endif
 size_t colsplit_lds_bytes(int P, int CW, int vcap) {
-    return 4 * (size_t)ST2 * P * CW + 4 * (size_t)(ST2 * P + 1) + (size_t)vcap;
+    return 4 * (size_t)ST2 * P * CW + 4 * (size_t)(ST2 * P + 1) + (size_t)vcap + 4;
 }
 constexpr int AMAX = 4;     // agents per wave of the column-split path (P <= 16)
 template <int MB, int NT>   // NT = CW / 16 n-tiles per column block
@@ -522,11 +522,38 @@ __global__ __launch_bounds__(THREADS) void colupdate_kernel(TiledArgs a, int k, 
     const int g0 = a.graph_shared ? 0 : s0 * P;
     const int vbase = a.vptr[g0];
     const int nent = a.vptr[g0 + nl] - vbase;
-    const bool vin = nent <= vcap;
-    for (int i = threadIdx.x; i <= nl; i += THREADS) vp[i] = a.vptr[g0 + i] - vbase;
-    if (vin)
-        for (int i = threadIdx.x; i < nent; i += THREADS) vql[i] = a.vq[vbase + i];
-    const uint8_t* vq = vin ? (const uint8_t*)vql : a.vq + vbase;
+    // (vcap + 4 <= 8 KB: every thread's loads are issued before its LDS stores, one round trip)
+    const int vsh = vbase & 3;                           // lists copied as aligned 32-bit words
+    const bool vin = nent + vsh <= vcap;
+    {
+        constexpr int VPW = (ST2 * 16 + 1 + THREADS - 1) / THREADS;   // list starts per thread
+        constexpr int VQW = 8192 / 4 / THREADS;                       // list words per thread
+        int pv[VPW];
+        uint32_t qv[VQW];
+        const uint32_t* vq32 = (const uint32_t*)(a.vq + (vbase - vsh));
+        const int nw = vin ? (nent + vsh + 3) / 4 : 0;
+#pragma unroll
+        for (int u = 0; u < VPW; ++u) {
+            const int i = threadIdx.x + u * THREADS;
+            pv[u] = i <= nl ? a.vptr[g0 + i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < VQW; ++u) {
+            const int i = threadIdx.x + u * THREADS;
+            qv[u] = i < nw ? vq32[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < VPW; ++u) {
+            const int i = threadIdx.x + u * THREADS;
+            if (i <= nl) vp[i] = pv[u] - vbase;
+        }
+#pragma unroll
+        for (int u = 0; u < VQW; ++u) {
+            const int i = threadIdx.x + u * THREADS;
+            if (i < nw) ((uint32_t*)vql)[i] = qv[u];
+        }
+    }
+    const uint8_t* vq = vin ? (const uint8_t*)vql + vsh : a.vq + vbase;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
