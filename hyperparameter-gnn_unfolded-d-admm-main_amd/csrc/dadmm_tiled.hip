@@ -435,7 +435,26 @@ __global__ __launch_bounds__(THREADS) void consensus_kernel(TiledArgs a, const f
     const int s = blockIdx.x / ncb, c0 = (blockIdx.x % ncb) * CB;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const float* ys_g = y + (size_t)s * P * n;
-    for (int idx = threadIdx.x; idx < P * (CB / 4); idx += THREADS) {
+    // the sample's rows: up to 4 chunks per thread loaded before any is stored (one round trip
+    // for P <= 16), then the rest if P is larger
+    constexpr int CPT = 4;
+    {
+        f32x4 v[CPT];
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const int idx = threadIdx.x + u * THREADS;
+            const int p = idx / (CB / 4), c = c0 + 4 * (idx % (CB / 4));
+            v[u] = (p < P && c < n) ? *(const f32x4*)(ys_g + (size_t)p * n + c)
+                                    : (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const int idx = threadIdx.x + u * THREADS;
+            const int p = idx / (CB / 4), c = c0 + 4 * (idx % (CB / 4));
+            if (p < P && c < n) *(f32x4*)(ys + p * CB + (c - c0)) = v[u];
+        }
+    }
+    for (int idx = threadIdx.x + CPT * THREADS; idx < P * (CB / 4); idx += THREADS) {
         const int p = idx / (CB / 4), c = c0 + 4 * (idx % (CB / 4));
         if (c < n) *(f32x4*)(ys + p * CB + (c - c0)) = *(const f32x4*)(ys_g + (size_t)p * n + c);
     }
