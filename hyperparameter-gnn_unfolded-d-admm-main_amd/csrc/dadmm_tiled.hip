@@ -793,7 +793,10 @@ hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream) {
     const size_t lds = tiled_lds_bytes(a.n_pad, a.m_pad);
     const char* env = getenv("DADMM_TILED_SPLIT");   // runtime override of the build default
     const bool split = env != nullptr ? atoi(env) != 0 : DADMM_TILED_SPLIT != 0;
-    if (split && a.R != nullptr && a.n_pad % 64 == 0 && (a.m_pad == 64 || a.m_pad == 128) &&
+    // the column-split update reads the visit lists as 32-bit words: a word-aligned base only
+    // (a sharded view gb.vq[base:] may start anywhere; it takes the two-launch form)
+    const bool vq_words = ((uintptr_t)a.vq & 3u) == 0;
+    if (split && vq_words && a.R != nullptr && a.n_pad % 64 == 0 && (a.m_pad == 64 || a.m_pad == 128) &&
         lds <= 160 * 1024) {
         const int vcap = 8192;
         const int CW = a.P <= tiled::AMAX * tiled::WAVES ? colsplit_width(a.P, vcap) : 0;

@@ -63,6 +63,22 @@ class _UnfoldedFn(torch.autograd.Function):
         return dtable, None, None, None, None, None, None, None
 
 
+def tag_status(Y: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
+    """Attach the forward's device status word to the returned iterates, so that the next
+    consumer that synchronises anyway (compute_loss) can raise GuardTimeoutError instead of
+    silently taking the reference's NaN fallback on a poisoned Y."""
+    Y._dadmm_status = status
+    return Y
+
+
+def raise_if_timed_out(Y: torch.Tensor) -> None:
+    """GuardTimeoutError if ``Y`` came from a forward whose guarded recomputation could not
+    synchronise its grid (one host synchronisation; nothing when Y carries no status)."""
+    status = getattr(Y, "_dadmm_status", None)
+    if status is not None:
+        check_status(status)
+
+
 def dadmm_unfolded_apply(op, b, graphs, table, y0, U0, d0, variant=_lib.VARIANT_UNFOLDED):
     """(Y [K,B,P,n], status [1] int32 device tensor) = the K-step recurrence with the reference's
     guards; Y is differentiable w.r.t. ``table`` (adjoint kernel)."""

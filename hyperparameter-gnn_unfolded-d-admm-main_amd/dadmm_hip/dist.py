@@ -100,3 +100,12 @@ def init_from_env(backend: str = None):
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(backend, **kw)
     return rank, ws, local
+
+
+def seed_rank_streams(seed: int, rank: int) -> None:
+    """Give every rank its own random streams after the replicated model init: torch's CPU
+    generator (the HIP training hypernetwork draws its dropout seed from it,
+    hyper_ops.draw_dropout_seed) and the device generators (the random inits y0, U0, delta0).
+    Without it, local sample i of every rank would draw the same dropout masks."""
+    torch.manual_seed(int(seed) * 1009 + int(rank))
+

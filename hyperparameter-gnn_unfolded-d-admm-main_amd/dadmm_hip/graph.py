@@ -117,8 +117,12 @@ def _to_device(arrays, device):
     return [t.to(device, non_blocking=True) for t in ts]
 
 
+VQ_TAIL = 4   # zero bytes after the visit lists: kernels that read them as 32-bit words stay in bounds
+
+
 def _vq_nonempty(vq):
-    return vq if vq.size else np.zeros(1, np.uint8)   # the ABI wants a valid pointer
+    """The visit lists plus VQ_TAIL zero bytes (never empty: the ABI wants a valid pointer)."""
+    return np.concatenate([vq, np.zeros(VQ_TAIL, np.uint8)])
 
 
 def _batch(infos, P: int, device) -> GraphBatch:
@@ -317,7 +321,7 @@ def generate_er(B: int, P: int, prob: float, seed: int, device, connect: bool = 
         _lib.check("dadmm_graph_generate", L.dadmm_graph_generate(
             *args, vp(nbr), vp(deg), vp(order), vp(vptr), None, vp(scratch), stream))
         total = int(vptr[-1].item()) if B > 0 else 0      # sizes the visit lists (one sync)
-        vq = torch.empty(max(total, 1), dtype=torch.uint8, device=device)
+        vq = torch.zeros(total + VQ_TAIL, dtype=torch.uint8, device=device)
         if B > 0:
             _lib.check("dadmm_graph_generate", L.dadmm_graph_generate(
                 *args, vp(nbr), vp(deg), vp(order), vp(vptr), vp(vq), vp(scratch), stream))

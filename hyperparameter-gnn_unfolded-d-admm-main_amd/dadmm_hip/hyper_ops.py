@@ -1,5 +1,5 @@
-"""Inference-mode hypernetwork of DLASSO_GNNHyp3_Progressive on the HIP library (the
-``dadmm_hyper_*`` entry points of include/dadmm.h).
+"""The hypernetwork of DLASSO_GNNHyp3_Progressive on the HIP library (the ``dadmm_hyper_*``
+entry points of include/dadmm.h), in inference and in training mode.
 
 ``model.eval()`` under ``torch.no_grad()`` (the drivers' validation loop,
 gnn_dlasso_progressive.py:240-265): Dropout is the identity and BatchNorm uses its running
@@ -7,8 +7,14 @@ statistics, so the whole GNNHypernetwork3 -> decoder -> fc -> head chain of one 
 (gnn_dlasso_models_progressive.py:165-196) is 5 GCN-layer launches (f32 MFMA GEMM + normalised
 adjacency mix + bias + leaky_relu + BatchNorm), one LayerNorm, three (split-K linear, LayerNorm +
 LeakyReLU) pairs and one head launch that writes hyp_k [B, 4, H] — 13 launches for all B samples.
-Training (autograd, Dropout draws, per-sample BatchNorm statistics) stays on the torch
-composition in gnn_dlasso_models_progressive.py.
+
+``model.train()`` (the drivers' training loop, gnn_dlasso_progressive.py:193-214): HyperTrainFn
+(``hypernetwork_train``) runs the same GEMMs with training epilogues (per-sample BatchNorm batch
+statistics, Dropout) and HIP backward kernels. Dropout is counter-based: element (row, col) of
+site s is kept iff hash(seed, s, row, col) >= p 2^32, with one 62-bit seed per hypernetwork call
+drawn from torch's CPU generator (``draw_dropout_seed``; torch.manual_seed fixes it, and
+dist.seed_rank_streams gives every data-parallel rank its own). The backward regenerates the
+masks from the seed instead of storing them.
 """
 from __future__ import annotations
 
@@ -362,11 +368,16 @@ class HyperTrainFn(torch.autograd.Function):
         return (dAtAy, None, None, None, None, None, None, None, *grads)
 
 
+def draw_dropout_seed() -> int:
+    """The dropout stream of one training-mode hypernetwork call, from torch's CPU generator."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
 def hypernetwork_train(model, AtAy, Atb, n, ahat, per_sample, seed=None, defer=False):
     """hyp_k [B, 4, H] of one iteration in training mode (HyperTrainFn); ``seed`` names the
     dropout stream (default: drawn from torch's CPU generator, so torch.manual_seed fixes it).
     defer: queue the BatchNorm running-statistics update on ``model`` for flush_running_stats
     (the model's forward flushes once after its K iterations)."""
     if seed is None:
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        seed = draw_dropout_seed()
     return HyperTrainFn.apply(AtAy, Atb, ahat, model, n, per_sample, seed, defer, *_hyper_params(model))

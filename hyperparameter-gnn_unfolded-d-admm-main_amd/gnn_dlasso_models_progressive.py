@@ -28,12 +28,15 @@ every iteration); Dropout(0.1) draws from torch's generator (not the reference's
 """
 from __future__ import annotations
 
+import warnings
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from dadmm_hip import _lib
 from dadmm_hip import hyper_ops
+from dadmm_hip.autograd import tag_status
 from dadmm_hip.gnn_ops import GnnRun, GramFn, StepFn
 from dadmm_hip.graph import ingest, n_graphs
 from dadmm_hip.ops import PreparedOperator, draw_inits
@@ -185,6 +188,9 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         self._graph_plans = {}
         # optional observer, called every iteration with (AtAy_k, Atb, (alpha, tau, rho, eta))
         self.on_hyp = None
+        # which hypernetwork implementation the last forward ran: "hip-eval-graph", "hip-eval",
+        # "hip-train" or "torch"
+        self.last_backend = None
 
     @property
     def AtA(self):
@@ -243,18 +249,20 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
             y0, U0, d0 = (x.reshape(batch_size, self.P, self.n) for x in inits)
         H = 1 if self.DADMM_mode == 'same' else self.P
         grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
-        run = GnnRun(self.operator(), bb, graphs, K, H, _lib.VARIANT_GNN, y0, U0, d0, grad)
         n = self.n
-        Atb = run.Atb[..., :n]
-        y, U, D = run.ys[0], run.U0, run.d0
-        ys = []
         # inference (model.eval() under no_grad): the hypernetwork runs on the fused HIP kernels
         fused = self.hyper_backend == "auto" and not grad and hyper_ops.supported(self, n)
         # training (model.train()): the HIP training-mode hypernetwork (dropout, batch statistics,
         # its backward) — HyperTrainFn
         train_hip = self.hyper_backend == "auto" and hyper_ops.supported_train(self, n)
+        self.last_backend = self._backend_name(fused, train_hip)
         if fused and self.use_hip_graph and self.on_hyp is None:
+            # the plan owns its device state: no per-forward GnnRun (its Y, Atb, G) is built
             return self._forward_graphed(bb, graphs, a_hat.contiguous(), y0, U0, d0, K, H)
+        run = GnnRun(self.operator(), bb, graphs, K, H, _lib.VARIANT_GNN, y0, U0, d0, grad)
+        Atb = run.Atb[..., :n]
+        y, U, D = run.ys[0], run.U0, run.d0
+        ys = []
         if fused or train_hip:
             a_hat = a_hat.contiguous()
         if fused:
@@ -285,7 +293,7 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         self.last_status = run.finish()
         Y = torch.stack(ys) if run.Y is None else run.Y
         Y = Y[..., :n].unsqueeze(-1)
-        return Y, (alpha_k, tau_k, rho_k, eta_k)
+        return tag_status(Y, self.last_status), (alpha_k, tau_k, rho_k, eta_k)
 
     def _forward_graphed(self, bb, graphs, a_hat, y0, U0, d0, K, H):
         """The inference forward as one replay of a captured HIP graph (_EvalGraphPlan); the
@@ -301,7 +309,24 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
             plan = _EvalGraphPlan(self, bb, graphs, a_hat, K, H)
             self._graph_plans[key] = plan
         Y, hyp, self.last_status = plan.run(bb, graphs, a_hat, y0, U0, d0)
-        return Y[..., :self.n].unsqueeze(-1), hyp
+        return tag_status(Y[..., :self.n].unsqueeze(-1), self.last_status), hyp
+
+    _warned_torch = False
+
+    def _backend_name(self, fused, train_hip):
+        """Which hypernetwork implementation this forward runs (``model.last_backend``); the torch
+        composition outside an explicit ``hyper_backend = "torch"`` is reported once."""
+        if fused:
+            return "hip-eval-graph" if self.use_hip_graph and self.on_hyp is None else "hip-eval"
+        if train_hip:
+            return "hip-train"
+        if self.hyper_backend != "torch" and not DLASSO_GNNHyp3_Progressive._warned_torch:
+            DLASSO_GNNHyp3_Progressive._warned_torch = True
+            why = ("eval mode with autograd enabled" if not self.training else
+                   "a module or width the HIP kernels do not cover")
+            warnings.warn(f"DLASSO_GNNHyp3_Progressive: hypernetwork on the torch composition ({why}); "
+                          f"the D-ADMM iterations still run on HIP", RuntimeWarning, stacklevel=3)
+        return "torch"
 
     # kept for API parity with the reference (:245-276); not used by the HIP forward
     def compute_sum_neighbors(self, graph_list):
@@ -369,6 +394,11 @@ class _EvalGraphPlan:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             body()
+        # the kernels reach the iterates only through the device table yptr, which every replay
+        # re-points at the caller's fresh Y: the capture-time Y (K B P n_store floats) is dead
+        cur.synchronize()
+        self.run_.Y = None
+        self.run_.ys = self.run_.ys[:1]
 
     def _load(self, bb, graphs, a_hat, y0, U0, d0):
         self.b.copy_(bb)

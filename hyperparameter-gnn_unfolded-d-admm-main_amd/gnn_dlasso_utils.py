@@ -42,8 +42,14 @@ def compute_loss(Y, label):
     Returns (1.0, 1.0) if Y, the label or any layer loss is non-finite (reference :36-43,
     :69-71, :83-86). Iterates in the HIP forward's layout go through the fused loss kernels
     (dadmm_hip.loss: one pass forward, one pass for dL/dY); anything else (e.g. CPU tensors)
-    through the same formula in torch."""
+    through the same formula in torch.
+
+    Iterates returned by the HIP forwards carry their status word: if the forward's guarded
+    recomputation timed out (its Y is NaN-poisoned) this raises
+    dadmm_hip.autograd.GuardTimeoutError rather than returning the fallback (1, 1)."""
+    from dadmm_hip.autograd import raise_if_timed_out
     from dadmm_hip.loss import fused_compute_loss
+    raise_if_timed_out(Y)
     fused = fused_compute_loss(Y, label)
     if fused is not None:
         return fused

@@ -132,6 +132,10 @@ def main(argv=None):
     # the reference's parser reads --GHyp_hidden as float (configurations.py:118), which only
     # works at its int default: a value given on the command line would reach nn.Linear as 16.0
     args.GHyp_hidden = int(args.GHyp_hidden)
+    if args.train_size < args.batch_size or args.test_size < args.batch_size:
+        # drop_last batching (gnn_data.py:15) would leave an epoch without a single batch
+        raise SystemExit(f"--train_size ({args.train_size}) and --test_size ({args.test_size}) must "
+                         f"be at least --batch_size ({args.batch_size})")
     rank, world, local = D.init_from_env()
     if not (torch.cuda.is_available() and args.device.startswith("cuda")):
         raise SystemExit("train_gnn.py runs the HIP forward: it needs a ROCm GPU (--device cuda:N)")
@@ -149,7 +153,7 @@ def main(argv=None):
     b_tr, x_tr, b_va, x_va = (t.to(device) for t in (b_tr, x_tr, b_va, x_va))
     torch.manual_seed(seed)            # model init identical on every rank
     model = gnn_dlasso_models_progressive.DLASSO_GNNHyp3_Progressive(A=A, args=args).to(device)
-    torch.cuda.manual_seed(seed * 1009 + rank)   # dropout / random inits: a stream per rank
+    D.seed_rank_streams(seed, rank)     # dropout seeds and random inits: a stream per rank
     optimizer = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=1e-5,
                                   betas=(0.9, 0.999))
     scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode="min", factor=0.7,
@@ -162,6 +166,7 @@ def main(argv=None):
     out = args.out or os.path.join("checkpoints", time.strftime("progressive_hip_%Y%m%d_%H%M%S"))
     t0 = time.time()
     batch_id = 0
+    hyp = None
     for epoch in range(E):
         K = iterations_for_epoch(epoch, E, Kmax)
         f = lr_factor(K, epoch, E, Kmax)
@@ -209,7 +214,7 @@ def main(argv=None):
         hist["iterations"].append(K)
         scheduler.step(valid)
         if rank == 0:
-            a0 = hyp[0][0, 0].item()
+            a0 = hyp[0][0, 0].item() if hyp is not None else float("nan")   # last training batch
             print(f"epoch {epoch + 1}/{E} iterations {K} lr x{f:.3f} train {hist['train_final'][-1]:.5f} "
                   f"valid {valid:.5f} alpha[0,0] {a0:.5f} ({time.time() - t0:.1f} s)", flush=True)
         if valid < best:

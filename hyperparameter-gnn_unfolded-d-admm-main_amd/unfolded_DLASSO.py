@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from dadmm_hip import _lib
-from dadmm_hip.autograd import check_status, dadmm_unfolded_apply
+from dadmm_hip.autograd import check_status, dadmm_unfolded_apply, tag_status
 from dadmm_hip.ops import describe_status
 from dadmm_hip.graph import ingest, n_graphs
 from dadmm_hip.ops import PreparedOperator
@@ -112,7 +112,7 @@ class DLASSO_unfolded(nn.Module):
         Y, self.last_status = dadmm_unfolded_apply(self.operator(), bb, graphs, table, y0, U0,
                                                    d0, _lib.VARIANT_UNFOLDED)
         hyp = table[K - 1].unsqueeze(-1)                # seq_hyp(K-1): [H, 4, 1]
-        return Y.unsqueeze(-1), hyp
+        return tag_status(Y.unsqueeze(-1), self.last_status), hyp
 
     def guard_warnings(self):
         """The reference's NaN/Inf warnings (unfolded_DLASSO.py:56-104) for the last forward

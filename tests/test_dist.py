@@ -102,6 +102,40 @@ def test_sharded_loss_and_gradient_equal_full_batch(tmp_path, world):
                                atol=1e-12 * np.abs(p.grad.numpy()).max())
 
 
+def _seed_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    r, w, _ = D.init_from_env("gloo")
+    from dadmm_hip import hyper_ops
+    # train_gnn.main: the model init is replicated (same seed everywhere), then every rank
+    # re-seeds its own streams; the HIP training hypernetwork draws its dropout seeds from them
+    torch.manual_seed(5)
+    init = torch.randn(4)
+    D.seed_rank_streams(5, r)
+    seeds = torch.tensor([hyper_ops.draw_dropout_seed() for _ in range(3)], dtype=torch.int64)
+    gi = [torch.empty_like(init) for _ in range(w)]
+    gs = [torch.empty_like(seeds) for _ in range(w)]
+    torch.distributed.all_gather(gi, init)
+    torch.distributed.all_gather(gs, seeds)
+    if r == 0:
+        np.savez(out_path, init=torch.stack(gi).numpy(), seeds=torch.stack(gs).numpy())
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_dropout_seeds_differ_between_ranks(tmp_path):
+    """each rank's dropout masks must come from its own stream (hash(seed, site, local
+    row, col) with a shared seed would give local sample i the same masks on every rank)."""
+    out = str(tmp_path / "seeds.npz")
+    mp.start_processes(_seed_worker, args=(2, _free_port(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    assert np.array_equal(got["init"][0], got["init"][1])          # replicated model init
+    s0, s1 = got["seeds"]
+    assert not set(s0.tolist()) & set(s1.tolist())                 # disjoint dropout seeds
+
+
 def test_single_process_is_identity():
     p = torch.nn.Parameter(torch.ones(3))
     p.grad = torch.full((3,), 2.0)

@@ -219,6 +219,24 @@ def test_compute_loss_matches_oracle_and_nan_fallback():
     assert mean.item() == 1.0 and final.item() == 1.0
 
 
+def test_compute_loss_raises_on_timed_out_forward():
+    """a forward whose guarded recomputation timed out poisons Y with NaN;
+    compute_loss (the next consumer that synchronises) raises instead of returning (1, 1)."""
+    import gnn_dlasso_utils
+    from dadmm_hip import _lib
+    from dadmm_hip.autograd import GuardTimeoutError, tag_status
+    Y = torch.full((3, 2, 2, 5, 1), float("nan"))
+    x = torch.zeros(2, 5, 1)
+    tag_status(Y, torch.tensor([_lib.STATUS_BARRIER_TIMEOUT | _lib.STATUS_GRAD_NAN], dtype=torch.int32))
+    with pytest.raises(GuardTimeoutError):
+        gnn_dlasso_utils.compute_loss(Y, x)
+    # a guard that fired normally is the reference's own behaviour: the fallback stands
+    Y2 = tag_status(torch.full((3, 2, 2, 5, 1), float("nan")),
+                    torch.tensor([_lib.STATUS_GRAD_NAN], dtype=torch.int32))
+    mean, final = gnn_dlasso_utils.compute_loss(Y2, x)
+    assert mean.item() == 1.0 and final.item() == 1.0
+
+
 @pytest.mark.parametrize("P,B,prob,loops", [(5, 200, 0.5, False), (16, 150, 0.3, False),
                                            (9, 120, 0.4, True), (50, 80, 0.5, False)])
 def test_vectorized_ingestion_equals_per_graph_path(P, B, prob, loops):
