@@ -64,6 +64,50 @@ __device__ __forceinline__ void consensus(const float (&yy)[P][E], float (&dl)[P
         for (int e = 0; e < E; ++e) dl[p][e] = acc[p][e];
 }
 
+// The shared-graph form without branches or selects, for a symmetric adjacency (an undirected
+// graph: p in N(q) <=> q in N(p)): mf[a][b] (a < b) = 1.0f for an edge, else 0.0f, a uniform
+// value held in an SGPR. Every update of delta[p] is acc + fl(y_p - y_q) (see above), written as
+// fma(d, mf, acc): with mf = 1 that is exactly fl(acc + d); with mf = 0 it is acc + (+-0) = acc,
+// because acc starts at +0 and a round-to-nearest sum is -0 only when both addends are -0, so acc
+// is never -0. A self-loop's pair of updates, (acc + 0) - 0, leaves acc unchanged and is skipped.
+// One subtraction per unordered pair, one v_fma_f32 per candidate visit, for finite y (a
+// non-finite y is flagged before it can reach here).
+__device__ __forceinline__ float fma_s(float d, float m, float acc) {   // d * m + acc, m in an SGPR
+    float r;
+    asm("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(d), "s"(m), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ float fma_sn(float d, float m, float acc) {  // -d * m + acc
+    float r;
+    asm("v_fma_f32 %0, -%1, %2, %3" : "=v"(r) : "v"(d), "s"(m), "v"(acc));
+    return r;
+}
+template <int P>
+__device__ __forceinline__ void consensus_fma(const float (&yy)[P][1], float (&dl)[P][1],
+                                              const float (&mf)[P][P]) {
+    float d[P][P];   // d[a][b] = fl(y_a - y_b) for a < b
+#pragma unroll
+    for (int a2 = 0; a2 < P; ++a2)
+#pragma unroll
+        for (int b2 = a2 + 1; b2 < P; ++b2) d[a2][b2] = yy[a2][0] - yy[b2][0];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        float acc = 0.0f;
+        // the sequence of delta[p]: q < p (q's loop), then p's own loop (ascending), then q > p
+        // (q's loop); d(p, q) = fl(y_p - y_q) = -d[q][p] for q < p (exact negation)
+#pragma unroll
+        for (int q = 0; q < p; ++q) acc = fma_sn(d[q][p], mf[q][p], acc);
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            if (q < p) acc = fma_sn(d[q][p], mf[q][p], acc);
+            else if (q > p) acc = fma_s(d[p][q], mf[p][q], acc);
+        }
+#pragma unroll
+        for (int q = p + 1; q < P; ++q) acc = fma_s(d[p][q], mf[p][q], acc);
+        dl[p][0] = acc;
+    }
+}
+
 // Per-lane (per-sample graph) form: the conditional adds become selects; pair differences are
 // shared as above (the compiler CSEs yy[a] - yy[b] across the four uses).
 template <int P, int E>

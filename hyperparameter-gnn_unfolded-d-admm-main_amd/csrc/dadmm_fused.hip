@@ -44,8 +44,14 @@
 #ifndef DADMM_A_RING
 #define DADMM_A_RING 3
 #endif
+// GEMM2 as paired chains: each agent's T2 n-tiles run as T2 interleaved accumulator chains that
+// share the R_p operand (independent MFMAs back to back instead of one dependent chain), with
+// the agent's primal update under the next agent's MFMAs
+#ifndef DADMM_G2_PAIR
+#define DADMM_G2_PAIR 1
+#endif
 #ifndef DADMM_AT_QD
-#define DADMM_AT_QD 5
+#define DADMM_AT_QD (DADMM_G2_PAIR ? 6 : 5)
 #endif
 
 namespace dadmm {
@@ -80,7 +86,11 @@ __device__ __forceinline__ void wait_vm(int n) {
         case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
         case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
         case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+        case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+        case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;   // (over-waits: safe)
     }
 }
 __device__ __forceinline__ void bstore4(f32x4 v, rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -104,6 +114,15 @@ __device__ __forceinline__ float tclamp(float x, float lo, float hi) {
 }
 // torch.sign for float: (0 < x) - (x < 0)
 __device__ __forceinline__ float tsign(float x) { return (float)((0.0f < x) - (x < 0.0f)); }
+// tclamp as one v_med3_f32: equal to min(max(x, lo), hi) for every non-NaN x when lo <= hi
+// (-0 stays -0: the median of {lo, -0, hi}); NaN cases are flagged like tclamp's
+__device__ __forceinline__ float mclamp(float x, float lo, float hi) {
+    return __builtin_amdgcn_fmed3f(x, lo, hi);
+}
+// The hyper-parameter table through the scalar cache (s_load): it is read-only for the whole
+// launch, so a constant-address-space view lets the uniform per-iteration reads bypass the vector
+// memory queue (no vmcnt wait at the top of an iteration)
+typedef const __attribute__((address_space(4))) float cfloat;
 __device__ __forceinline__ bool finitef(float x) { return __builtin_isfinite(x); }
 // Ablation knobs (timing builds only, never shipped): replace operand loads by register values.
 #ifdef DADMM_ABL_A_CONST
@@ -149,6 +168,34 @@ __device__ __forceinline__ unsigned long long stamp() {
 #define STAMP(i) do {} while (0)
 #define STAMP_FLUSH(w) do {} while (0)
 #endif
+
+// The paired-chain GEMM2's A^T ring, simulated at compile time: quarter q = (4 p + t) T2 + tt is
+// A^T_p rows of n-tile tt, m-block t. PRE quarters are issued before the phase (under GEMM1's
+// last step, across the barrier); each step (p, t) first issues every quarter up to q0 + QD - 1
+// (q0 = (4 p + t) T2: reusing only slots of quarters read before the previous step's MFMAs),
+// then waits for its T2 quarters; after the MFMAs of agent p >= 1 the primal update of agent
+// p - 1 issues T2 * SPQ stores. younger[q] = the VMEM ops issued after quarter q's DMA and
+// before its wait, i.e. the exact s_waitcnt vmcnt(younger[q]) that guarantees it has landed.
+template <int P, int T2, int QD, int SPQ>
+struct G2Plan {
+    static constexpr int NQ = P * 4 * T2;
+    static constexpr int PRE = QD < NQ ? QD : NQ;
+    int younger[NQ];
+    constexpr G2Plan() : younger{} {
+        int pos[NQ] = {};
+        int op = 0, issued = 0;
+        for (; issued < PRE; ++issued) pos[issued] = op++;
+        for (int p = 0; p < P; ++p) {
+            for (int t = 0; t < 4; ++t) {
+                const int q0 = (4 * p + t) * T2;
+                const int lim = q0 + QD - 1 < NQ - 1 ? q0 + QD - 1 : NQ - 1;
+                for (; issued <= lim; ++issued) pos[issued] = op++;
+                for (int tt = 0; tt < T2; ++tt) younger[q0 + tt] = op - 1 - pos[q0 + tt];
+            }
+            if (p > 0) op += T2 * SPQ;
+        }
+    }
+};
 
 // Compiler-only memory barrier: bounds how far the scheduler hoists operand loads.
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
@@ -216,8 +263,15 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     }
 
     // ---- state: this wave owns n-tiles nb = w*T2 + tt; element e = 4*tt + r is row
-    //      nb*16 + 4h + r. D holds delta_k = 2 L y_k (k = 0: the caller's d0). -------------------
-    float y[P][E], U[P][E], D[P][E];
+    //      nb*16 + 4h + r. D holds delta_k = 2 L y_k (k = 0: the caller's d0). y_k itself is not
+    //      held in registers: it lives in the LDS tile Ylds (GEMM1's B operand), from which the
+    //      lane reads its own rows back when the updates need them (40 VGPRs freed at H). ------
+    float U[P][E], D[P][E];
+    bool bad_y = false;
+    // the lane's rows of y (row e of agent p) in the LDS tile
+    auto ylds_at = [&](int p, int e) -> float* {
+        return Ylds + (p * BT + j) * YS + (w * T2 + e / 4) * 16 + 4 * h + (e & 3);
+    };
     {
         const rsrc_t ry = make_rsrc(a.y0, state_bytes);
         const rsrc_t ru = make_rsrc(a.U0, state_bytes);
@@ -238,7 +292,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    y[p][4 * tt + r] = vy[r];
+                    bad_y |= !finitef(vy[r]);
                     U[p][4 * tt + r] = vu[r];
                     D[p][4 * tt + r] = vd[r];
                 }
@@ -268,15 +322,41 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     // terms are clamped), and a NaN gradient is flagged where it arises.
     uint32_t status = 0;
     {
-        bool bad_y = false, bad_u = false;
+        bool bad_u = false;
 #pragma unroll
         for (int p = 0; p < P; ++p)
 #pragma unroll
-            for (int e = 0; e < E; ++e) {
-                bad_y |= !finitef(y[p][e]);
-                bad_u |= !finitef(U[p][e]);
-            }
+            for (int e = 0; e < E; ++e) bad_u |= !finitef(U[p][e]);
         status |= (bad_y ? 1u : 0u) | (bad_u ? 2u : 0u);
+    }
+
+    // A non-finite hyper-parameter makes y_next NaN (reference guard :102): flag it once for the
+    // whole table (the bit only triggers the exact guarded recomputation of the batch)
+    {
+        bool bad_h = false;
+        const int nh = a.K * a.hyp_rows * 4;
+        for (int i = threadIdx.x; i < nh; i += WAVES * 64) bad_h |= !finitef(a.hyp[i]);
+        status |= bad_h ? 8u : 0u;
+    }
+    // the shared graph's edges as float 0/1 multipliers, mf[a][b] = (b in N(a)), a < b (uniform);
+    // consensus_fma needs a symmetric adjacency: an asymmetric one (a directed graph's successor
+    // lists) raises status bit 16, which sends the batch through the exact guarded path
+    float mf[P][P];
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int p = 0; p < P; ++p) mf[q][p] = 0.0f;
+    if constexpr (SHARED_GRAPH) {
+        bool asym = false;
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+#pragma unroll
+            for (int p = q + 1; p < P; ++p) {
+                const bool e1 = (msk[q] >> p) & 1u, e2 = (msk[p] >> q) & 1u;
+                asym |= e1 != e2;
+                mf[q][p] = e1 ? 1.0f : 0.0f;
+            }
+        status |= asym ? 16u : 0u;
     }
 
     // per-lane byte offsets into the operator and the output
@@ -291,8 +371,12 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     // ring slot q % QD of this wave (lane-linear: lane l's 16 bytes at l * 16, which is exactly the
     // MFMA A-operand fragment lane l reads back)
     auto dma_quarter = [&](const uint32_t (&vAt)[T2], int q) {
+#if DADMM_G2_PAIR
+        const int tt = q % T2, t = (q / T2) & 3, p = q / (4 * T2);   // see G2Plan
+#else
         const int c = q >> 2, t = q & 3;
         const int p = c / T2, tt = c % T2;
+#endif
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rAt, (lds_void*)(Qlds + (w * QD + q % QD) * 256), 16,
                                                  vAt[tt] + 64 * t, (uint32_t)(p * NP * MP * 4), 0, 0);
     };
@@ -311,7 +395,10 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     };
 #pragma unroll
     for (int t = 0; t + 1 < RING; ++t) load_a(aring[t], t);
-    if (HALF == 1) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half loses arbitration
+#ifndef DADMM_HALF_PRIO
+#define DADMM_HALF_PRIO 1
+#endif
+    if (HALF == 1 && DADMM_HALF_PRIO) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half loses arbitration
     __syncthreads();
     STAMP_DECL
 
@@ -321,22 +408,26 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     float vclip_prev = 0.0f;
 #pragma unroll
     for (int p = 0; p < P; ++p) et_prev[p] = 0.0f;
-    auto dual_update_row = [&](int e, const uint32_t (&mk)[P]) {
+    // GNN variant: delta clamped to +-20 (:229); the unfolded variant: +-inf (a no-op on finite d)
+    const float dlim = a.variant != 0 ? 20.0f : __builtin_inff();
+    auto dual_update_row = [&](int e, const uint32_t (&mk)[P], bool live) {
         float yy[P][1], dd[P][1];
 #pragma unroll
-        for (int p = 0; p < P; ++p) yy[p][0] = y[p][e];
+        for (int p = 0; p < P; ++p) yy[p][0] = *ylds_at(p, e);   // y_{k+1}, this lane's row e
         if constexpr (GRAPH == GRAPH_SHARED)
-            consensus<P, 1>(yy, dd, [&](int q, int p) { return ((mk[q] >> p) & 1u) != 0; });
+            consensus_fma<P>(yy, dd, mf);
         else if constexpr (GRAPH == GRAPH_LANE)
             consensus_lane<P, 1>(yy, dd, mk);
         else
             consensus_ordered<P, 1>(yy, dd, mk, ord);
 #pragma unroll
         for (int p = 0; p < P; ++p) {
-            float d = dd[p][0];
-            if (a.variant != 0) d = tclamp(d, -20.0f, 20.0f);             // GNN :229
-            D[p][e] = d;
-            U[p][e] = tclamp(U[p][e] + d * et_prev[p], -vclip_prev, vclip_prev);
+            const float d = mclamp(dd[p][0], -dlim, dlim);
+            const float un = mclamp(U[p][e] + d * et_prev[p], -vclip_prev, vclip_prev);
+            // k = 0 keeps the caller's U0, delta0 (a select, not a branch: the row stays one
+            // basic block, interleavable with the GEMM1 MFMAs)
+            D[p][e] = live ? d : D[p][e];
+            U[p][e] = live ? un : U[p][e];
         }
     };
 
@@ -357,7 +448,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
         float al[P], ta[P], rh[P], et[P];
 #pragma unroll
         for (int p = 0; p < P; ++p) {
-            const float* hp = a.hyp + ((size_t)k * a.hyp_rows + (a.hyp_rows == 1 ? 0 : p)) * 4;
+            const cfloat* hp = (const cfloat*)a.hyp + ((size_t)k * a.hyp_rows + (a.hyp_rows == 1 ? 0 : p)) * 4;
             al[p] = hp[0]; ta[p] = hp[1]; rh[p] = hp[2]; et[p] = hp[3];
         }
         float gclip, vclip;
@@ -368,15 +459,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
             gclip = 10.0f;                                   // gnn_dlasso_models_progressive.py:212
             vclip = 100.0f;                                  // :224, :232
         }
-        // A non-finite hyper-parameter makes y_next NaN (reference guard :102); flag it.
-        {
-            bool bad_h = false;
-#pragma unroll
-            for (int p = 0; p < P; ++p)
-                bad_h |= !(finitef(al[p]) && finitef(ta[p]) && finitef(rh[p]) && finitef(et[p]));
-            status |= bad_h ? 8u : 0u;
-        }
-        const bool deferred = k > 0 && has_tiles;
+        const bool deferred = k > 0;
 
         // ---- GEMM1: R_p = A_p y_p - b_p for this wave's TH tiles, with the previous
         //      iteration's dual update interleaved (VALU under the MFMA chains) ------------------
@@ -410,13 +493,13 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                     // GEMM2's first quarters, in flight across the barrier
                     if (t == NB - 1 && has_tiles) {
 #pragma unroll
-                        for (int q = 0; q + 1 < QD && q < P * T2 * 4; ++q) dma_quarter(vAt, q);
+                        for (int q = 0; q + 1 - DADMM_G2_PAIR < QD && q < P * T2 * 4; ++q) dma_quarter(vAt, q);
                     }
                 }
                 // rows e with e * NB / E == t
 #pragma unroll
                 for (int e = 0; e < E; ++e)
-                    if ((e * NB) / E == t && deferred) dual_update_row(e, mk);
+                    if ((e * NB) / E == t && has_tiles) dual_update_row(e, mk, deferred);
             }
 #pragma unroll
             for (int i = 0; i < TH; ++i)
@@ -455,16 +538,17 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 const int nb = w * T2 + tt;
                 const int n0 = nb * 16 + 4 * h;
                 f32x4 yn, grv, urv;
+                const f32x4 yk = *(const f32x4*)(Ylds + (p * BT + j) * YS + n0);   // y_k, 4 rows
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int e = 4 * tt + r;
-                    const float yv = y[p][e];
+                    const float yv = yk[r];
                     // grad = (AtAy - Atb) + sign(y)*tau + U*deg + delta*rho, left to right;
                     // sign(y)*tau is exactly +-tau or +0
                     // (the nested ternary compiles to short divergent branches here; the branch-free
                     // sign_times() costs 46 spilled VGPRs in this register-bound kernel and measured
                     // 0.64 vs 0.59 ms at the headline shape)
-                    const float st = yv > 0.0f ? ta[p] : (yv < 0.0f ? -ta[p] : 0.0f);
+                    const float st = sign_times(yv, ta[p]);
                     float gr = gp[r];
                     gr = gr + st;
                     gr = gr + U[p][e] * dg[p];
@@ -472,10 +556,9 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                     grv[r] = gr;
                     urv[r] = U[p][e];
                     bad_g |= (gr != gr);                            // :84 guard (flag only)
-                    gr = tclamp(gr, -gclip, gclip);                 // :80-81
+                    gr = mclamp(gr, -gclip, gclip);                 // :80-81
                     float v = yv - al[p] * gr;                      // :89
-                    v = tclamp(v, -vclip, vclip);                   // :92-93
-                    y[p][e] = v;
+                    v = mclamp(v, -vclip, vclip);                   // :92-93
                     yn[r] = v;
                 }
                 *(f32x4*)(Ylds + (p * BT + j) * YS + n0) = yn;
@@ -489,7 +572,54 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                     bstore4_stream(urv, rUr, o);
                 }
             };
-#if DADMM_AT_DMA
+#if DADMM_AT_DMA && DADMM_G2_PAIR
+            // stores of one primal update (Y[k], and Grec / Urec when recording)
+            constexpr int SPQ = REC ? 3 : 1;
+            constexpr G2Plan<P, T2, QD, SPQ> plan{};
+            f32x4 gp[2][T2];
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                compiler_fence();
+#pragma unroll
+                for (int t = 0; t < MP / 16; ++t)
+                    rv[t] = *(const f32x4*)(Rlds + (p * BT + j) * RS + 4 * h + 16 * t);
+                f32x4 gc[T2];
+#pragma unroll
+                for (int tt = 0; tt < T2; ++tt) gc[tt] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int t = 0; t < MP / 16; ++t) {
+                    const int q0 = (4 * p + t) * T2;
+                    // every quarter up to q0 + QD - 1 (the slots of the quarters read before the
+                    // previous step's MFMAs), then this step's waits (exact counts: G2Plan)
+#pragma unroll
+                    for (int x = q0 + QD - T2; x < q0 + QD; ++x)
+                        if (q0 > 0 && x < G2Plan<P, T2, QD, SPQ>::NQ) dma_quarter(vAt, x);
+                    f32x4 av[T2];
+#pragma unroll
+                    for (int tt = 0; tt < T2; ++tt) {
+                        wait_vm(plan.younger[q0 + tt]);
+                        av[tt] = ABL_AT(*(const f32x4*)(Qlds + (w * QD + (q0 + tt) % QD) * 256 + lane * 4));
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int tt = 0; tt < T2; ++tt) gc[tt] = mfma4(av[tt][r], rv[t][r], gc[tt]);
+                }
+#pragma unroll
+                for (int tt = 0; tt < T2; ++tt) gp[p & 1][tt] = gc[tt];
+                if (p + 1 == P && k + 1 < a.K) {
+                    // next iteration's first GEMM1 steps, after every ring wait (so no wait has
+                    // to count them), before the last agent's Y stores
+                    for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
+                }
+                if (p > 0) {
+#pragma unroll
+                    for (int tt = 0; tt < T2; ++tt) primal_update((p - 1) * T2 + tt, gp[(p - 1) & 1][tt]);
+                }
+            }
+#pragma unroll
+            for (int tt = 0; tt < T2; ++tt) primal_update((P - 1) * T2 + tt, gp[(P - 1) & 1][tt]);
+#elif DADMM_AT_DMA
             constexpr int NQ = NS * 4;
             // stores of one primal update (Y[k], and Grec / Urec when recording)
             constexpr int SPQ = REC ? 3 : 1;
@@ -553,7 +683,9 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 if (s2 > 0) primal_update(s2 - 1, g[(s2 - 1) & 1]);
             }
 #endif
+#if !(DADMM_AT_DMA && DADMM_G2_PAIR)
             primal_update(NS - 1, g[(NS - 1) & 1]);
+#endif
             status |= bad_g ? 4u : 0u;
         } else if (k + 1 < a.K) {
             for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
@@ -575,7 +707,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
         for (int p = 0; p < P; ++p) mk[p] = msk[p];
         if (a.K > 0) {
 #pragma unroll
-            for (int e = 0; e < E; ++e) dual_update_row(e, mk);
+            for (int e = 0; e < E; ++e) dual_update_row(e, mk, true);
         }
         const rsrc_t rU = make_rsrc(a.U_out, state_bytes);
 #pragma unroll

@@ -18,6 +18,7 @@ DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
 STATUS_BARRIER_TIMEOUT = 0x100
+STATUS_RECOMPUTE = 16      # ungated fused kernel only: asymmetric shared adjacency
 GATE_ON, FLAGS_ZEROED = 1, 2
 
 # every symbol include/dadmm.h declares

@@ -230,6 +230,45 @@ def _batch_vectorized(graph_list, P: int, device) -> GraphBatch:
     return GraphBatch(t_[0], t_[1], False, t_[4] if ordered else None, t_[2], t_[3], fused_ok)
 
 
+def _native():
+    """dadmm_hip._ingest (csrc/dadmm_ingest.c), or None when the extension is not built."""
+    global _NATIVE
+    if _NATIVE is False:
+        try:
+            from . import _ingest
+            _NATIVE = _ingest
+        except ImportError:
+            _NATIVE = None
+    return _NATIVE
+
+
+_NATIVE = False
+
+
+def _batch_native(graph_list, P: int, device):
+    """Per-sample layouts for a list of networkx graphs in one C pass over their adjacency dicts
+    (dadmm_hip._ingest.batch: masks, degrees, order nibbles, reference-order visit lists; any
+    adjacency, directed included). None when the extension is missing or a graph is not a
+    dict-of-dicts networkx graph (the caller takes the Python path)."""
+    mod = _native()
+    if mod is None:
+        return None
+    try:
+        nbr, deg, order, vptr, vq, ascending, _ = mod.batch(graph_list, P)
+    except TypeError:
+        return None
+    B = len(graph_list)
+    ordered = not ascending
+    fused_ok = not (ordered and P > 8)
+    ordered &= fused_ok
+    arrays = [np.frombuffer(nbr, np.int64).reshape(B, P), np.frombuffer(deg, np.float32).reshape(B, P),
+              np.frombuffer(vptr, np.int32), _vq_nonempty(np.frombuffer(vq, np.uint8))]
+    if ordered:
+        arrays.append(np.frombuffer(order, np.int32).reshape(B, P))
+    t_ = _to_device(arrays, device)
+    return GraphBatch(t_[0], t_[1], False, t_[4] if ordered else None, t_[2], t_[3], fused_ok)
+
+
 def n_graphs(graph_list, batch_size: int) -> int:
     """len(graph_list) as the reference's forward sees it; an already ingested GraphBatch counts
     as one graph per sample."""
@@ -266,7 +305,10 @@ def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
     else:
         ids = {id(g) for g in graph_list}
         if len(ids) > 64 and G == batch_size:
-            gb = _batch_vectorized(graph_list, P, device)      # many distinct graphs
+            # many distinct graphs: one native pass (csrc/dadmm_ingest.c), else numpy
+            gb = _batch_native(graph_list, P, device)
+            if gb is None:
+                gb = _batch_vectorized(graph_list, P, device)
             if gb is not None:
                 return gb
         per = {}

@@ -276,6 +276,8 @@ def describe_status(st: int) -> list:
         out.append("NaN/Inf in gradient, update skipped")
     if st & _lib.STATUS_YNEXT_NAN:
         out.append("NaN/Inf in y_next, previous value kept")
+    if st & _lib.STATUS_RECOMPUTE:
+        out.append("fused kernel: asymmetric shared adjacency, batch needs the guarded recomputation")
     if st & _lib.STATUS_BARRIER_TIMEOUT:
         out.append("stepwise grid barrier timed out: Y is invalid (device shared with other work)")
     return out

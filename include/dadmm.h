@@ -80,6 +80,10 @@ enum {
     DADMM_STATUS_U_NONFINITE = 2,    /* U_k had NaN/Inf at the top of an iteration   (:59)   */
     DADMM_STATUS_GRAD_NAN = 4,       /* clamped gradient had NaN                     (:84)   */
     DADMM_STATUS_YNEXT_NAN = 8,      /* y_next had NaN/Inf                           (:102)  */
+    DADMM_STATUS_RECOMPUTE = 16,     /* dadmm_forward only: the shared adjacency is not
+                                      * symmetric, so the fused consensus cannot follow it; the
+                                      * gated stepwise run recomputes the batch (never set after
+                                      * a gated run)                                          */
     DADMM_STATUS_BARRIER_TIMEOUT = 0x100 /* gated stepwise run could not synchronise its grid
                                           * (device shared with other work): Y is invalid    */
 };

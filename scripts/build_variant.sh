@@ -9,7 +9,7 @@ NAME=$1; EXTRA=${2:-}; SRC=${3:-dadmm_fused.hip}
 C=hyperparameter-gnn_unfolded-d-admm-main_amd/csrc
 make -s -C $C >/dev/null
 mkdir -p build/var
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -mllvm -pragma-unroll-threshold=1000000 -Wall -Wno-unused-function"
 /opt/rocm/bin/hipcc $FLAGS $EXTRA -x hip -c $C/$SRC -o build/var/${NAME}_$SRC.o
 OBJS=""
 for o in $C/build/*.o; do

@@ -259,6 +259,46 @@ def test_vectorized_ingestion_equals_per_graph_path(P, B, prob, loops):
     assert Gm.ingest(graphs, P, B, "cpu").vq.numel() == ref.vq.numel()
 
 
+@pytest.mark.parametrize("P,B,prob,loops,directed", [(5, 200, 0.5, False, False), (16, 150, 0.3, False, False),
+                                                    (9, 120, 0.4, True, False), (50, 80, 0.5, True, False),
+                                                    (7, 90, 0.4, True, True), (64, 20, 0.2, False, False)])
+def test_native_ingestion_equals_per_graph_path(P, B, prob, loops, directed):
+    """csrc/dadmm_ingest.c (the C pass over the networkx adjacency dicts) gives exactly the
+    per-graph Python layouts, including self-loops, non-ascending adjacency (the connectivity
+    patch) and directed graphs (successor lists: asymmetric masks)."""
+    import networkx as nx
+    from dadmm_hip import graph as Gm
+    assert Gm._native() is not None, "dadmm_hip._ingest not built (csrc/Makefile)"
+    graphs = []
+    for s in range(B):
+        g = O.connected_er_graph(P, prob, seed=s)
+        if directed:
+            d = nx.DiGraph()
+            d.add_nodes_from(range(P))
+            d.add_edges_from((u, v) if (u + v + s) % 2 else (v, u) for u, v in g.edges())
+            g = d
+        if loops and s % 3 == 0:
+            g.add_edge(s % P, s % P)
+        graphs.append(g)
+    fast = Gm._batch_native(graphs, P, "cpu")
+    ref = Gm._batch([Gm._info(g, P) for g in graphs], P, "cpu")
+    for k in ("nbr", "deg", "vptr", "vq"):
+        np.testing.assert_array_equal(getattr(fast, k).numpy(), getattr(ref, k).numpy(), err_msg=k)
+    assert (fast.order is None) == (ref.order is None) and fast.fused_ok == ref.fused_ok
+    if fast.order is not None:
+        np.testing.assert_array_equal(fast.order.numpy(), ref.order.numpy())
+
+
+def test_native_ingestion_errors():
+    import networkx as nx
+    from dadmm_hip import graph as Gm
+    g = nx.Graph([(0, 5)])
+    g.add_nodes_from(range(4))
+    with pytest.raises(ValueError, match="neighbour id 5"):
+        Gm._batch_native([g] * 3, 4, "cpu")
+    assert Gm._batch_native([object()] * 3, 4, "cpu") is None       # not networkx: Python path
+
+
 def test_vectorized_ingestion_rejects_asymmetric_graphs():
     from dadmm_hip import graph as Gm
     P = 4
