@@ -53,6 +53,17 @@
 #ifndef DADMM_AT_QD
 #define DADMM_AT_QD (DADMM_G2_PAIR ? 6 : 5)
 #endif
+// DADMM_AT_DMA = 0 with DADMM_G2_PAIR: GEMM2's A^T through a register ring of DADMM_AT_RS steps
+// (one step = the T2 fragments of (agent, m-block)), the first steps issued under GEMM1
+#ifndef DADMM_AT_RS
+#define DADMM_AT_RS 3
+#endif
+// Per-agent-group synchronisation instead of the two workgroup barriers per iteration (8-wave
+// workgroups, DMA paired GEMM2): LDS arrival counters let a half of the waves run GEMM2 of the
+// agents whose R is complete while the other half still runs GEMM1 (see fused_body)
+#ifndef DADMM_AGENT_SYNC
+#define DADMM_AGENT_SYNC 0
+#endif
 
 namespace dadmm {
 
@@ -176,7 +187,9 @@ __device__ __forceinline__ unsigned long long stamp() {
 // then waits for its T2 quarters; after the MFMAs of agent p >= 1 the primal update of agent
 // p - 1 issues T2 * SPQ stores. younger[q] = the VMEM ops issued after quarter q's DMA and
 // before its wait, i.e. the exact s_waitcnt vmcnt(younger[q]) that guarantees it has landed.
-template <int P, int T2, int QD, int SPQ>
+// FLUSH (agent sync): the stores of position FLUSH - 1 are issued before position FLUSH's steps
+// instead of after them (-1: none).
+template <int P, int T2, int QD, int SPQ, int FLUSH = -1>
 struct G2Plan {
     static constexpr int NQ = P * 4 * T2;
     static constexpr int PRE = QD < NQ ? QD : NQ;
@@ -186,16 +199,29 @@ struct G2Plan {
         int op = 0, issued = 0;
         for (; issued < PRE; ++issued) pos[issued] = op++;
         for (int p = 0; p < P; ++p) {
+            if (p == FLUSH && p > 0) op += T2 * SPQ;
             for (int t = 0; t < 4; ++t) {
                 const int q0 = (4 * p + t) * T2;
                 const int lim = q0 + QD - 1 < NQ - 1 ? q0 + QD - 1 : NQ - 1;
                 for (; issued <= lim; ++issued) pos[issued] = op++;
                 for (int tt = 0; tt < T2; ++tt) younger[q0 + tt] = op - 1 - pos[q0 + tt];
             }
-            if (p > 0) op += T2 * SPQ;
+            if (p > 0 && p != FLUSH) op += T2 * SPQ;
         }
     }
 };
+
+// LDS arrival counters of the agent-group synchronisation (one lane adds; the spin reads with
+// s_sleep). The adder first waits for its own LDS writes (lgkmcnt(0)); LDS is coherent in the CU.
+__device__ __forceinline__ void lds_signal(uint32_t* c, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait(uint32_t* c, uint32_t target) {
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+        __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
 
 // Compiler-only memory barrier: bounds how far the scheduler hoists operand loads.
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
@@ -232,6 +258,16 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     float* __restrict__ Blds = Rlds + P * BT * RS;   // [P][BT][RS]   -b (not with DADMM_AT_DMA)
     constexpr int QD = DADMM_AT_QD;
     float* __restrict__ Qlds = Rlds + P * BT * RS;   // [WAVES][QD][256] A^T ring (DADMM_AT_DMA)
+
+    // agent-group sync (DADMM_AGENT_SYNC): Rrdy[h] counts the waves of half h that have stored
+    // their R tiles (4 per iteration), Ydone[h] the waves that have finished the primal updates
+    // of half h's agents (every wave with GEMM2 tiles, once per iteration). GEMM2 visits the
+    // agents of half 1 first (p odd), then half 0.
+    constexpr bool SYNC = DADMM_AGENT_SYNC && DADMM_AT_DMA && DADMM_G2_PAIR && WAVES == 8 && P > 1;
+    uint32_t* const cnt = (uint32_t*)(DADMM_AT_DMA ? Qlds + WAVES * QD * 256 : Blds + P * BT * RS);
+    constexpr int NODD = P / 2;                      // agents 1, 3, ...: the first GEMM2 positions
+    auto agent_at = [](int i) { return SYNC ? (i < NODD ? 2 * i + 1 : 2 * (i - NODD)) : i; };
+    constexpr int TILE_WAVES = (NB + T2 - 1) / T2;    // waves with GEMM2 tiles (has_tiles)
 
     const int lane = threadIdx.x & 63;
     const int j = lane & 15;             // sample within the tile (MFMA column)
@@ -372,7 +408,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     // MFMA A-operand fragment lane l reads back)
     auto dma_quarter = [&](const uint32_t (&vAt)[T2], int q) {
 #if DADMM_G2_PAIR
-        const int tt = q % T2, t = (q / T2) & 3, p = q / (4 * T2);   // see G2Plan
+        const int tt = q % T2, t = (q / T2) & 3, p = agent_at(q / (4 * T2));   // see G2Plan
 #else
         const int c = q >> 2, t = q & 3;
         const int p = c / T2, tt = c % T2;
@@ -381,6 +417,17 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                                                  vAt[tt] + 64 * t, (uint32_t)(p * NP * MP * 4), 0, 0);
     };
 
+#if !DADMM_AT_DMA && DADMM_G2_PAIR
+    // GEMM2 A^T register ring: slot st % DADMM_AT_RS holds step st = 4 p + t, the A^T_p rows of the
+    // wave's T2 n-tiles at m-block t
+    f32x4 tring2[DADMM_AT_RS][T2];
+    auto load_at_step = [&](f32x4 (&slot)[T2], const uint32_t (&vAt)[T2], int st) {
+        const int p = st / 4, t = st % 4;
+#pragma unroll
+        for (int tt = 0; tt < T2; ++tt)
+            slot[tt] = ABL_AT(bload4(rAt, vAt[tt] + 64 * t, (uint32_t)(p * NP * MP * 4)));
+    };
+#endif
     // GEMM1 A-operand ring: slot t % RING holds A rows of step t (16 columns) for the TH tiles.
     // The first step of every iteration is issued before the previous iteration's last Y stores,
     // so it is not queued behind them (vmcnt counts loads and stores in order).
@@ -399,6 +446,9 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
 #define DADMM_HALF_PRIO 1
 #endif
     if (HALF == 1 && DADMM_HALF_PRIO) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half loses arbitration
+    if constexpr (SYNC) {
+        if (w == 0 && lane < 4) cnt[lane] = 0u;
+    }
     __syncthreads();
     STAMP_DECL
 
@@ -432,6 +482,10 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     };
 
     for (int k = 0; k < a.K; ++k) {
+        if constexpr (SYNC) {
+            // y_k of this half's agents complete in Ylds (every tile wave's primal updates)
+            if (k > 0) lds_wait(cnt + 2 + HALF, (uint32_t)(TILE_WAVES * k));
+        }
         vA = fresh(voffA);
         // shared graph: re-launder the (uniform) masks so the neighbour tests are evaluated in the
         // loop (s_bitcmp + branch) instead of being hoisted as P*P 64-bit condition registers
@@ -496,6 +550,13 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                         for (int q = 0; q + 1 - DADMM_G2_PAIR < QD && q < P * T2 * 4; ++q) dma_quarter(vAt, q);
                     }
                 }
+#if !DADMM_AT_DMA && DADMM_G2_PAIR
+                // GEMM2's first A^T steps, in flight across the barrier
+                if (t == NB - 1 && has_tiles) {
+#pragma unroll
+                    for (int st = 0; st + 1 < DADMM_AT_RS && st < 4 * P; ++st) load_at_step(tring2[st], vAt, st);
+                }
+#endif
                 // rows e with e * NB / E == t
 #pragma unroll
                 for (int e = 0; e < E; ++e)
@@ -506,7 +567,8 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 *(f32x4*)(Rlds + ((HALF + AS * i) * BT + j) * RS + 16 * mb + 4 * h) = acc[i];
         }
         STAMP(0);
-        __syncthreads();
+        if constexpr (SYNC) lds_signal(cnt + HALF, lane);   // this wave's R tiles are in Rlds
+        else __syncthreads();
         STAMP(1);
 
         // ---- GEMM2 (G_p = A_p^T R_p) as a sequence of (agent, n-tile) chains of 16 MFMAs; the
@@ -518,13 +580,13 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
             const rsrc_t rG = make_rsrc(REC ? a.Grec + (size_t)k * B * P * n : a.Y, REC ? state_bytes : 0u);
             const rsrc_t rUr = make_rsrc(REC ? a.Urec + (size_t)k * B * P * n : a.Y, REC ? state_bytes : 0u);
             constexpr int NS = P * T2;                       // chains: s = p*T2 + tt
-#if !DADMM_AT_DMA
+#if !DADMM_AT_DMA && !DADMM_G2_PAIR
             f32x4 tring[2][MP / 16];
 #endif
             f32x4 g[2];
             f32x4 rv[MP / 16];
             bool bad_g = false;
-#if !DADMM_AT_DMA
+#if !DADMM_AT_DMA && !DADMM_G2_PAIR
             auto load_at = [&](f32x4 (&slot)[MP / 16], int s2) {
                 const int p = s2 / T2, tt = s2 % T2;
 #pragma unroll
@@ -575,10 +637,21 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
 #if DADMM_AT_DMA && DADMM_G2_PAIR
             // stores of one primal update (Y[k], and Grec / Urec when recording)
             constexpr int SPQ = REC ? 3 : 1;
-            constexpr G2Plan<P, T2, QD, SPQ> plan{};
+            constexpr int FL = SYNC ? NODD : -1;
+            constexpr G2Plan<P, T2, QD, SPQ, FL> plan{};
             f32x4 gp[2][T2];
 #pragma unroll
-            for (int p = 0; p < P; ++p) {
+            for (int i = 0; i < P; ++i) {
+                const int p = agent_at(i);
+                if constexpr (SYNC) {
+                    if (i == NODD) {
+                        // the odd agents' last primal update, then release them to GEMM1(k+1)
+#pragma unroll
+                        for (int tt = 0; tt < T2; ++tt) primal_update(agent_at(i - 1) * T2 + tt, gp[(i - 1) & 1][tt]);
+                        lds_signal(cnt + 2 + 1, lane);
+                    }
+                    if (i == 0 || i == NODD) lds_wait(cnt + (i == 0 ? 1 : 0), (uint32_t)(4 * (k + 1)));
+                }
                 compiler_fence();
 #pragma unroll
                 for (int t = 0; t < MP / 16; ++t)
@@ -588,7 +661,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 for (int tt = 0; tt < T2; ++tt) gc[tt] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
                 for (int t = 0; t < MP / 16; ++t) {
-                    const int q0 = (4 * p + t) * T2;
+                    const int q0 = (4 * i + t) * T2;
                     // every quarter up to q0 + QD - 1 (the slots of the quarters read before the
                     // previous step's MFMAs), then this step's waits (exact counts: G2Plan)
 #pragma unroll
@@ -606,10 +679,47 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                         for (int tt = 0; tt < T2; ++tt) gc[tt] = mfma4(av[tt][r], rv[t][r], gc[tt]);
                 }
 #pragma unroll
-                for (int tt = 0; tt < T2; ++tt) gp[p & 1][tt] = gc[tt];
-                if (p + 1 == P && k + 1 < a.K) {
+                for (int tt = 0; tt < T2; ++tt) gp[i & 1][tt] = gc[tt];
+                if (i + 1 == P && k + 1 < a.K) {
                     // next iteration's first GEMM1 steps, after every ring wait (so no wait has
                     // to count them), before the last agent's Y stores
+                    for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
+                }
+                if (i > 0 && i != FL) {
+#pragma unroll
+                    for (int tt = 0; tt < T2; ++tt) primal_update(agent_at(i - 1) * T2 + tt, gp[(i - 1) & 1][tt]);
+                }
+            }
+#pragma unroll
+            for (int tt = 0; tt < T2; ++tt) primal_update(agent_at(P - 1) * T2 + tt, gp[(P - 1) & 1][tt]);
+            if constexpr (SYNC) lds_signal(cnt + 2 + 0, lane);   // the even agents' y_{k+1}
+#elif DADMM_G2_PAIR
+            // paired chains, A^T from the register ring (compiler-counted vmcnt waits)
+            constexpr int NST = 4 * P;
+            f32x4 gp[2][T2];
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                compiler_fence();
+#pragma unroll
+                for (int t = 0; t < MP / 16; ++t)
+                    rv[t] = *(const f32x4*)(Rlds + (p * BT + j) * RS + 4 * h + 16 * t);
+                f32x4 gc[T2];
+#pragma unroll
+                for (int tt = 0; tt < T2; ++tt) gc[tt] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int t = 0; t < MP / 16; ++t) {
+                    const int st = 4 * p + t;
+                    if (st + DADMM_AT_RS - 1 < NST)
+                        load_at_step(tring2[(st + DADMM_AT_RS - 1) % DADMM_AT_RS], vAt, st + DADMM_AT_RS - 1);
+                    const f32x4(&av)[T2] = tring2[st % DADMM_AT_RS];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int tt = 0; tt < T2; ++tt) gc[tt] = mfma4(av[tt][r], rv[t][r], gc[tt]);
+                }
+#pragma unroll
+                for (int tt = 0; tt < T2; ++tt) gp[p & 1][tt] = gc[tt];
+                if (p + 1 == P && k + 1 < a.K) {
                     for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
                 }
                 if (p > 0) {
@@ -683,7 +793,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 if (s2 > 0) primal_update(s2 - 1, g[(s2 - 1) & 1]);
             }
 #endif
-#if !(DADMM_AT_DMA && DADMM_G2_PAIR)
+#if !DADMM_G2_PAIR
             primal_update(NS - 1, g[(NS - 1) & 1]);
 #endif
             status |= bad_g ? 4u : 0u;
@@ -695,7 +805,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
         vclip_prev = vclip;
         STAMP(2);
         STAMP(3);
-        __syncthreads();
+        if constexpr (!SYNC) __syncthreads();
         STAMP(4);
     }
     STAMP_FLUSH(w);
@@ -734,12 +844,21 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
 template <int P, int NT, int GRAPH, int WV, bool REC>
 __global__ __launch_bounds__(WV * 64) void fused_forward_kernel(FusedArgs a) {
     constexpr int NP = NT * 64;
-    __shared__ __attribute__((aligned(16))) float lds[DADMM_AT_DMA
+    __shared__ __attribute__((aligned(16))) float lds[(DADMM_AT_DMA
         ? P * BT * ((NP + 4) + (M_PAD + 4)) + WV * DADMM_AT_QD * 256
-        : P * BT * ((NP + 4) + 2 * (M_PAD + 4))];
+        : P * BT * ((NP + 4) + 2 * (M_PAD + 4))) + 4];   // + the agent-sync counters
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave id, in an SGPR
     if constexpr (WV == 4) {
         fused_body<P, NT, GRAPH, 4, 0, REC>(a, lds, w);
+    } else if constexpr (WV == 16) {   // 4 waves per SIMD (timing experiments)
+        if (w < 4)
+            fused_body<P, NT, GRAPH, 16, 0, REC>(a, lds, w);
+        else if (w < 8)
+            fused_body<P, NT, GRAPH, 16, 1, REC>(a, lds, w);
+        else if (w < 12)
+            fused_body<P, NT, GRAPH, 16, 2, REC>(a, lds, w);
+        else
+            fused_body<P, NT, GRAPH, 16, 3, REC>(a, lds, w);
     } else {
         if (w < 4)
             fused_body<P, NT, GRAPH, 8, 0, REC>(a, lds, w);
