@@ -907,6 +907,58 @@ int dadmm_hyper_head_act(int32_t mode, int32_t B, int32_t H, const float* z, con
     return ok();
 }
 
+size_t dadmm_hyper_wgrad_scratch_bytes(int32_t R, int32_t N, int32_t K) {
+    if (R < 0 || N < 1 || K < 1) return 0;
+    const int s = dadmm::wgrad_splits(R, N, K);
+    return s > 1 ? 4 * (size_t)s * N * (K + 1) : 0;
+}
+
+int dadmm_hyper_wgrad(int32_t R, int32_t N, int32_t K, const float* dz, int32_t ldz, const float* x1,
+                      int32_t ld1, int32_t K1, const float* x2, int32_t ld2, float* g, float* gbias,
+                      int32_t beta, void* scratch, void* stream) {
+    if (R < 0 || N < 1 || K < 1 || K1 < 1 || K1 > K) return fail(DADMM_EINVAL, "bad wgrad dims R=%d N=%d K=%d K1=%d", R, N, K, K1);
+    if (!dz || !x1 || !g || (K1 < K && !x2)) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (ldz < N || ld1 < K1 || (K1 < K && ld2 < K - K1)) return fail(DADMM_EINVAL, "leading dimension too small");
+    if ((int64_t)R * (ldz > ld1 ? ldz : ld1) >= ((int64_t)1 << 31) || (int64_t)N * K >= ((int64_t)1 << 31))
+        return fail(DADMM_EUNSUPPORTED, "operand larger than 2^31 floats");
+    const int splits = dadmm::wgrad_splits(R, N, K);
+    if (splits > 1 && (!scratch || !aligned16(scratch)))
+        return fail(DADMM_EINVAL, "scratch (dadmm_hyper_wgrad_scratch_bytes) is NULL or not 16-byte aligned");
+    if (R == 0) {
+        if (beta) return ok();
+        hipError_t e = hipMemsetAsync(g, 0, 4 * (size_t)N * K, (hipStream_t)stream);
+        if (e == hipSuccess && gbias) e = hipMemsetAsync(gbias, 0, 4 * (size_t)N, (hipStream_t)stream);
+        if (e != hipSuccess) return fail(DADMM_EHIP, "memset: %s", hipGetErrorString(e));
+        return ok();
+    }
+    dadmm::WgradArgs a{dz, x1, K1 < K ? x2 : x1, g, gbias, (float*)scratch,
+                       splits > 1 ? (float*)scratch + (size_t)splits * N * K : nullptr,
+                       R, N, K, K1, ldz, ld1, K1 < K ? ld2 : ld1, splits, beta ? 1 : 0};
+    hipError_t e = dadmm::launch_wgrad(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "wgrad launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_hyper_colsum(const float* part, int32_t G, int32_t R, int32_t C, float* out, int32_t beta,
+                       void* stream) {
+    if (G < 1 || R < 0 || C < 1) return fail(DADMM_EINVAL, "bad colsum dims G=%d R=%d C=%d", G, R, C);
+    if (!out || (R > 0 && !part)) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if ((int64_t)G * R * C >= ((int64_t)1 << 31)) return fail(DADMM_EUNSUPPORTED, "operand larger than 2^31 floats");
+    hipError_t e = dadmm::launch_colsum(part, G, R, C, out, beta ? 1 : 0, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "colsum launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_hyper_transpose(int32_t rows, int32_t cols, const float* in, float* out, void* stream) {
+    if (rows < 0 || cols < 0) return fail(DADMM_EINVAL, "bad transpose dims");
+    if (rows == 0 || cols == 0) return ok();
+    if (!in || !out) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if ((int64_t)rows * cols >= ((int64_t)1 << 31)) return fail(DADMM_EUNSUPPORTED, "operand larger than 2^31 floats");
+    hipError_t e = dadmm::launch_transpose(in, rows, cols, out, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "transpose launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;
     const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);

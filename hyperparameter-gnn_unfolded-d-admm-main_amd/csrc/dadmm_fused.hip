@@ -579,11 +579,11 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
             // REC (training): the adjoint's trajectory, Grec[k] = pre-clamp gradient, Urec[k] = U_k
             const rsrc_t rG = make_rsrc(REC ? a.Grec + (size_t)k * B * P * n : a.Y, REC ? state_bytes : 0u);
             const rsrc_t rUr = make_rsrc(REC ? a.Urec + (size_t)k * B * P * n : a.Y, REC ? state_bytes : 0u);
-            constexpr int NS = P * T2;                       // chains: s = p*T2 + tt
+            [[maybe_unused]] constexpr int NS = P * T2;      // chains: s = p*T2 + tt
 #if !DADMM_AT_DMA && !DADMM_G2_PAIR
             f32x4 tring[2][MP / 16];
 #endif
-            f32x4 g[2];
+            [[maybe_unused]] f32x4 g[2];
             f32x4 rv[MP / 16];
             bool bad_g = false;
 #if !DADMM_AT_DMA && !DADMM_G2_PAIR

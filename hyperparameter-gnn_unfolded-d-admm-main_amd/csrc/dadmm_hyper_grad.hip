@@ -1,0 +1,227 @@
+// dadmm_hyper_grad.hip — the parameter-gradient GEMMs and reductions of the training-mode GNN
+// hypernetwork (gnn_dlasso_models_progressive.py:9-72, :93-123; backward through them as the
+// reference's loss_final.backward(), gnn_dlasso_progressive.py:207-214), accumulated in place:
+//
+//   wgrad_kernel  : G[N][K] += dZ^T X  (the weight gradient of one nn.Linear / GCNConv.lin over R
+//                   rows: dZ [R][N] is the gradient of the linear's output, X [R][K] its input,
+//                   optionally read as two column segments, cat(AtAy, Atb) in place), and
+//                   g_bias[N] += sum_r dZ[r][n] (the bias gradient) from the same dZ reads.
+//                   f32 MFMA v_mfma_f32_16x16x4_f32 with the R rows as the reduction (k) dimension:
+//                   lane (i, h) feeds dZ[r + h][n0 + i] and X[r + h][k0 + i]. One workgroup per
+//                   64 x 64 output tile and R-split; splits > 1 write partial tiles to scratch that
+//                   reduce_kernel adds into G in split order.
+//   colsum_kernel : out[g][c] += sum_r part[g][r][c] — the per-block partial sums of the BatchNorm /
+//                   bias (dadmm_hyper_gcn_train_bwd) and LayerNorm (dadmm_hyper_rownorm_bwd) parameter
+//                   gradients, one thread per output column, rows in order.
+// Every sum runs in a fixed order: the gradients are deterministic run to run. They match torch's
+// autograd (hipBLASLt) to f32 rounding of a different summation order.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dadmm_internal.h"
+
+namespace dadmm {
+namespace hgrad {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int THREADS = 256;
+constexpr int TN = 64, TK = 64;   // output tile (n x k) per workgroup: 4 waves of 32 x 32
+constexpr int RING = 4;           // row steps (4 rows each) of operands in flight per wave
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// XCD-aware order: consecutive tiles (the k-tiles of one n-tile, which read the same dZ columns)
+// on blocks of one XCD (the dispatcher deals blocks round-robin over the 8 XCDs)
+__device__ __forceinline__ int xcd_tile(int bid, int G) {
+    constexpr int NX = 8;
+    const int xcd = bid % NX, i = bid / NX, q = G / NX, r = G % NX;
+    return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
+}
+
+__global__ __launch_bounds__(THREADS) void wgrad_kernel(WgradArgs a) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = lane & 15, h = lane >> 4;
+    const int wn = w >> 1, wk = w & 1;
+    const int gn = (a.N + TN - 1) / TN, gk = (a.K + TK - 1) / TK;
+    const int tl = xcd_tile(blockIdx.x, gridDim.x);
+    const int kt = tl % gk, nt = (tl / gk) % gn, split = tl / (gk * gn);
+    const int n0 = nt * TN + wn * 32, k0 = kt * TK + wk * 32;
+    const int steps = (a.R + 3) / 4;
+    const int per = (steps + a.splits - 1) / a.splits;
+    const int s_begin = split * per;
+    const int s_end = s_begin + per < steps ? s_begin + per : steps;
+
+    // operand columns of this lane (clamped: out-of-range columns compute garbage, never stored)
+    int nc[2];
+    const float* xs[2];
+    int ldx[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        int n = n0 + 16 * b + i;
+        nc[b] = n < a.N ? n : a.N - 1;
+        int k = k0 + 16 * b + i;
+        k = k < a.K ? k : a.K - 1;
+        if (k < a.K1) {
+            xs[b] = a.x1 + k;
+            ldx[b] = a.ld1;
+        } else {
+            xs[b] = a.x2 + (k - a.K1);
+            ldx[b] = a.ld2;
+        }
+    }
+    const bool do_bias = a.gbias != nullptr && kt == 0 && wk == 0;
+
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) acc[x][0] = acc[x][1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    float bsum[2] = {0.0f, 0.0f};
+
+    float ra[RING][2], rb[RING][2];
+    auto load = [&](int u, int st) {
+        const int r = 4 * st + h;
+        const bool ok = r < a.R && st < s_end;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            ra[u][b] = ok ? a.dz[(size_t)r * a.ldz + nc[b]] : 0.0f;
+            rb[u][b] = ok ? xs[b][(size_t)r * ldx[b]] : 0.0f;
+        }
+    };
+#pragma unroll
+    for (int u = 0; u < RING; ++u) load(u, s_begin + u);
+    for (int st = s_begin; st < s_end; st += RING) {
+#pragma unroll
+        for (int u = 0; u < RING; ++u) {
+            if (st + u < s_end) {
+#pragma unroll
+                for (int x = 0; x < 2; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y) acc[x][y] = mfma4(ra[u][x], rb[u][y], acc[x][y]);
+                if (do_bias) {
+                    bsum[0] += ra[u][0];
+                    bsum[1] += ra[u][1];
+                }
+            }
+            load(u, st + u + RING);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // acc[x][y]: lane (i, h) holds G rows n0 + 16 x + 4 h + q (q = 0..3), column k0 + 16 y + i
+    float* out = a.splits > 1 ? a.scratch + (size_t)split * a.N * a.K : a.g;
+    const bool accum = a.splits == 1 && a.beta != 0;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            const int k = k0 + 16 * y + i;
+            if (k >= a.K) continue;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = n0 + 16 * x + 4 * h + q;
+                if (n >= a.N) continue;
+                float* o = out + (size_t)n * a.K + k;
+                *o = accum ? *o + acc[x][y][q] : acc[x][y][q];
+            }
+        }
+    if (do_bias) {
+        // column sums of dZ over this split's rows: lanes (i, h) hold rows 4 st + h; the 4 groups
+        // h are added in order
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            float v = bsum[b];
+            const float v1 = __shfl_down(v, 16), v2 = __shfl_down(v, 32), v3 = __shfl_down(v, 48);
+            v = ((v + v1) + v2) + v3;
+            const int n = n0 + 16 * b + i;
+            if (h == 0 && n < a.N) {
+                if (a.splits > 1) a.scratch_bias[(size_t)split * a.N + n] = v;
+                else a.gbias[n] = a.beta != 0 ? a.gbias[n] + v : v;
+            }
+        }
+    }
+}
+
+// dst[i] (+)= sum_s src[s][i], s in order
+__global__ __launch_bounds__(THREADS) void reduce_kernel(const float* __restrict__ src, int splits, size_t count,
+                                                         float* __restrict__ dst, int beta) {
+    const size_t idx = (size_t)blockIdx.x * THREADS + threadIdx.x;
+    if (idx >= count) return;
+    float v = beta ? dst[idx] : 0.0f;
+    float s = 0.0f;
+    for (int k = 0; k < splits; ++k) s += src[(size_t)k * count + idx];
+    dst[idx] = v + s;
+}
+
+// out[g][c] (+)= sum_r part[g][r][c], r in order; one thread per (g, c)
+__global__ __launch_bounds__(THREADS) void colsum_kernel(const float* __restrict__ part, int G, int R, int C,
+                                                         float* __restrict__ out, int beta) {
+    const int idx = blockIdx.x * THREADS + threadIdx.x;
+    if (idx >= G * C) return;
+    const int g = idx / C, c = idx - g * C;
+    const float* p = part + (size_t)g * R * C + c;
+    float s = 0.0f;
+    for (int r = 0; r < R; ++r) s += p[(size_t)r * C];
+    out[idx] = beta ? out[idx] + s : s;
+}
+
+// out [cols][rows] = in [rows][cols], 32 x 32 tiles through LDS (the weight transposes the input
+// gradient GEMM dX = dZ W reads as the K-contiguous operand of dadmm_hyper_linear)
+__global__ __launch_bounds__(THREADS) void transpose_kernel(const float* __restrict__ in, int rows, int cols,
+                                                            float* __restrict__ out) {
+    __shared__ float t[32][33];
+    const int gc = (cols + 31) / 32;
+    const int r0 = (blockIdx.x / gc) * 32, c0 = (blockIdx.x % gc) * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 8 rows of 32 per pass
+    for (int y = ty; y < 32; y += 8) {
+        const int r = r0 + y, c = c0 + tx;
+        if (r < rows && c < cols) t[y][tx] = in[(size_t)r * cols + c];
+    }
+    __syncthreads();
+    for (int y = ty; y < 32; y += 8) {
+        const int c = c0 + y, r = r0 + tx;
+        if (r < rows && c < cols) out[(size_t)c * rows + r] = t[tx][y];
+    }
+}
+
+}  // namespace hgrad
+
+hipError_t launch_transpose(const float* in, int rows, int cols, float* out, hipStream_t st) {
+    const int g = ((rows + 31) / 32) * ((cols + 31) / 32);
+    hipLaunchKernelGGL(hgrad::transpose_kernel, dim3(g), dim3(hgrad::THREADS), 0, st, in, rows, cols, out);
+    return hipGetLastError();
+}
+
+int wgrad_splits(int R, int N, int K) {
+    const int tiles = ((N + hgrad::TN - 1) / hgrad::TN) * ((K + hgrad::TK - 1) / hgrad::TK);
+    const int steps = (R + 3) / 4;
+    int s = 1;
+    // split the rows while the grid is short of ~2 workgroups per CU and each split keeps >= 32
+    // row steps (128 rows)
+    while (tiles * s * 2 <= 512 && steps / (2 * s) >= 32) s *= 2;
+    return s;
+}
+
+hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st) {
+    const int tiles = ((a.N + hgrad::TN - 1) / hgrad::TN) * ((a.K + hgrad::TK - 1) / hgrad::TK);
+    hipLaunchKernelGGL(hgrad::wgrad_kernel, dim3(tiles * a.splits), dim3(hgrad::THREADS), 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || a.splits == 1) return e;
+    const size_t cnt = (size_t)a.N * a.K;
+    hipLaunchKernelGGL(hgrad::reduce_kernel, dim3((unsigned)((cnt + hgrad::THREADS - 1) / hgrad::THREADS)),
+                       dim3(hgrad::THREADS), 0, st, a.scratch, a.splits, cnt, a.g, a.beta);
+    e = hipGetLastError();
+    if (e != hipSuccess || a.gbias == nullptr) return e;
+    hipLaunchKernelGGL(hgrad::reduce_kernel, dim3((unsigned)((a.N + hgrad::THREADS - 1) / hgrad::THREADS)),
+                       dim3(hgrad::THREADS), 0, st, a.scratch_bias, a.splits, (size_t)a.N, a.gbias, a.beta);
+    return hipGetLastError();
+}
+
+hipError_t launch_colsum(const float* part, int G, int R, int C, float* out, int beta, hipStream_t st) {
+    const int n = G * C;
+    hipLaunchKernelGGL(hgrad::colsum_kernel, dim3((n + hgrad::THREADS - 1) / hgrad::THREADS), dim3(hgrad::THREADS),
+                       0, st, part, G, R, C, out, beta);
+    return hipGetLastError();
+}
+
+}  // namespace dadmm

@@ -13,8 +13,7 @@
  * exactly as dadmm_hip.graph._visit_lists does in Python. The Python per-graph loops were the
  * dominant host cost of a forward over thousands of distinct graphs (missing #4).
  *
- * batch(graph_list, P) -> (nbr bytes, deg bytes, order bytes, vptr bytes, vq bytes, ascending,
- *                          symmetric)
+ * batch(graph_list, P) -> (nbr, deg, order, vptr, vq as bytearrays, ascending, symmetric)
  * Raises ValueError for a neighbour id outside 0..P-1 (the reference would index past the
  * state), TypeError for a graph without a dict adjacency (the caller then takes the Python path).
  */
@@ -186,10 +185,13 @@ static PyObject* batch(PyObject* self, PyObject* args) {
                 *o++ = (uint8_t)__builtin_ctzll(m);
         }
         free(intos);
-        out = Py_BuildValue("(y#y#y#y#y#NN)", (const char*)nbr, (Py_ssize_t)(BP * 8), (const char*)deg,
-                            (Py_ssize_t)(BP * 4), (const char*)order, (Py_ssize_t)(BP * 4),
-                            (const char*)vptr, (Py_ssize_t)((BP + 1) * 4), (const char*)vq,
-                            (Py_ssize_t)total, PyBool_FromLong(ascending), PyBool_FromLong(symmetric));
+        /* bytearrays: numpy views of them are writable (torch.from_numpy warns on read-only ones) */
+        out = Py_BuildValue("(NNNNNNN)", PyByteArray_FromStringAndSize((const char*)nbr, (Py_ssize_t)(BP * 8)),
+                            PyByteArray_FromStringAndSize((const char*)deg, (Py_ssize_t)(BP * 4)),
+                            PyByteArray_FromStringAndSize((const char*)order, (Py_ssize_t)(BP * 4)),
+                            PyByteArray_FromStringAndSize((const char*)vptr, (Py_ssize_t)((BP + 1) * 4)),
+                            PyByteArray_FromStringAndSize((const char*)vq, (Py_ssize_t)total),
+                            PyBool_FromLong(ascending), PyBool_FromLong(symmetric));
     }
 
 done:
@@ -207,7 +209,7 @@ done:
 
 static PyMethodDef methods[] = {
     {"batch", batch, METH_VARARGS,
-     "batch(graph_list, P) -> (nbr, deg, order, vptr, vq, ascending, symmetric) as bytes / bools"},
+     "batch(graph_list, P) -> (nbr, deg, order, vptr, vq, ascending, symmetric) as bytearrays / bools"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_ingest",

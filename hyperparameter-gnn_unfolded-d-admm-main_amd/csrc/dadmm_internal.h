@@ -295,6 +295,26 @@ hipError_t launch_head_act(int mode, int B, int H, const float* z, const float* 
                            float* out, hipStream_t st);
 hipError_t launch_rownorm(const RowNormArgs& a, hipStream_t st);
 
+// ---- training-mode parameter gradients (dadmm_hyper_grad.hip) ----------------------------------
+// g [N][K] (+)= dZ^T X over R rows; X = cat of two column segments (x1: columns < K1, x2: the
+// rest); gbias [N] (+)= column sums of dZ (nullable); splits > 1: partial tiles in scratch
+struct WgradArgs {
+    const float* dz;        // [R][ldz]
+    const float* x1;        // [R][ld1]
+    const float* x2;        // [R][ld2] (K1 == K: unused)
+    float* g;               // [N][K]
+    float* gbias;           // [N] or nullptr
+    float* scratch;         // [splits][N][K] when splits > 1
+    float* scratch_bias;    // [splits][N] when splits > 1 and gbias
+    int R, N, K, K1, ldz, ld1, ld2, splits, beta;
+};
+int wgrad_splits(int R, int N, int K);
+hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st);
+// out [G][C] (+)= sum over r of part [G][R][C] (fixed order)
+hipError_t launch_colsum(const float* part, int G, int R, int C, float* out, int beta, hipStream_t st);
+// out [cols][rows] = in [rows][cols]
+hipError_t launch_transpose(const float* in, int rows, int cols, float* out, hipStream_t st);
+
 // ---- device-side ER graph generation (dadmm_graphgen.hip) ---------------------------------------
 struct GraphGenArgs {
     int B, P;

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -47,6 +47,13 @@ EXPORTED_SYMBOLS = (
     "dadmm_hyper_rownorm_bwd_part_bytes",
     "dadmm_hyper_rownorm_bwd",
     "dadmm_hyper_head_act",
+    "dadmm_hyper_wgrad_scratch_bytes",
+    "dadmm_hyper_wgrad",
+    "dadmm_hyper_colsum",
+    "dadmm_hyper_transpose",
+    "dadmm_hyper_train_work_bytes",
+    "dadmm_hyper_train_forward",
+    "dadmm_hyper_train_backward",
     "dadmm_gnn_flag_bytes",
     "dadmm_gnn_begin",
     "dadmm_gnn_gram",
@@ -82,6 +89,40 @@ class Dims(ctypes.Structure):
 
 _lib = None
 
+
+
+_fp = ctypes.POINTER(ctypes.c_float)
+_f5 = ctypes.c_float * 5
+_f3 = ctypes.c_float * 3
+
+
+class HyperNet(ctypes.Structure):
+    """dadmm_hyper_net (include/dadmm.h): the training hypernetwork's dimensions and parameters."""
+    _fields_ = [("P", ctypes.c_int32), ("n", ctypes.c_int32), ("ld", ctypes.c_int32),
+                ("width", ctypes.c_int32 * 5), ("dec_width", ctypes.c_int32 * 3), ("H", ctypes.c_int32),
+                ("conv_w", ctypes.c_void_p * 5), ("conv_b", ctypes.c_void_p * 5),
+                ("bn_w", ctypes.c_void_p * 5), ("bn_b", ctypes.c_void_p * 5), ("bn_eps", _f5),
+                ("norm_w", ctypes.c_void_p), ("norm_b", ctypes.c_void_p), ("norm_eps", ctypes.c_float),
+                ("dec_w", ctypes.c_void_p * 3), ("dec_b", ctypes.c_void_p * 3),
+                ("ln_w", ctypes.c_void_p * 3), ("ln_b", ctypes.c_void_p * 3),
+                ("ln_eps", _f3), ("dec_slope", _f3), ("dec_drop", _f3),
+                ("fc_w", ctypes.c_void_p), ("fc_b", ctypes.c_void_p),
+                ("drop_enc", ctypes.c_float), ("maxv", ctypes.c_float * 4)]
+
+
+class HyperSaved(ctypes.Structure):
+    """dadmm_hyper_saved: one iteration's saved activations."""
+    _fields_ = [("y", ctypes.c_void_p * 5), ("m", ctypes.c_void_p * 5), ("mean", ctypes.c_void_p * 5),
+                ("var", ctypes.c_void_p * 5), ("e", ctypes.c_void_p), ("dec_y", ctypes.c_void_p * 3),
+                ("dec_xd", ctypes.c_void_p * 3), ("z", ctypes.c_void_p), ("hyp", ctypes.c_void_p)]
+
+
+class HyperGrads(ctypes.Structure):
+    """dadmm_hyper_grads: gradient accumulators and transposed weights of one backward pass."""
+    _fields_ = [("conv_w", ctypes.c_void_p * 5), ("bn_wbc", ctypes.c_void_p * 5), ("norm_wb", ctypes.c_void_p),
+                ("dec_w", ctypes.c_void_p * 3), ("dec_b", ctypes.c_void_p * 3), ("ln_wb", ctypes.c_void_p * 3),
+                ("fc_w", ctypes.c_void_p), ("fc_b", ctypes.c_void_p),
+                ("conv_wt", ctypes.c_void_p * 5), ("dec_wt", ctypes.c_void_p * 3), ("fc_wt", ctypes.c_void_p)]
 
 def load() -> ctypes.CDLL:
     """Load libdadmm.so once; raises if it is absent (no silent fallback)."""
@@ -175,6 +216,26 @@ def load() -> ctypes.CDLL:
         f.argtypes = args
     L.dadmm_hyper_rownorm_bwd_part_bytes.restype = ctypes.c_size_t
     L.dadmm_hyper_rownorm_bwd_part_bytes.argtypes = [i32, i32]
+    # one call per iteration (csrc/dadmm_hyper_net.cpp)
+    L.dadmm_hyper_train_work_bytes.restype = ctypes.c_size_t
+    L.dadmm_hyper_train_work_bytes.argtypes = [ctypes.POINTER(HyperNet), i32]
+    L.dadmm_hyper_train_forward.restype = ctypes.c_int
+    L.dadmm_hyper_train_forward.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, vp, i32, u64,
+                                            ctypes.POINTER(HyperSaved), vp, vp]
+    L.dadmm_hyper_train_backward.restype = ctypes.c_int
+    L.dadmm_hyper_train_backward.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, vp, i32, u64,
+                                             ctypes.POINTER(HyperSaved), vp, ctypes.POINTER(HyperGrads),
+                                             vp, vp, vp]
+    # training-mode parameter gradients (csrc/dadmm_hyper_grad.hip)
+    L.dadmm_hyper_wgrad_scratch_bytes.restype = ctypes.c_size_t
+    L.dadmm_hyper_wgrad_scratch_bytes.argtypes = [i32, i32, i32]
+    for name, args in (("dadmm_hyper_wgrad", [i32, i32, i32, vp, i32, vp, i32, i32, vp, i32, vp, vp, i32,
+                                              vp, vp]),
+                       ("dadmm_hyper_colsum", [vp, i32, i32, i32, vp, i32, vp]),
+                       ("dadmm_hyper_transpose", [i32, i32, vp, vp, vp])):
+        f = getattr(L, name)
+        f.restype = ctypes.c_int
+        f.argtypes = args
     v = L.dadmm_abi_version()
     if v != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {v}, expected {ABI_VERSION}")

@@ -18,6 +18,8 @@ masks from the seed instead of storing them.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.nn as nn
 
@@ -212,6 +214,9 @@ class HyperTrainFn(torch.autograd.Function):
     def forward(ctx, AtAy, Atb, ahat, model, n, per_sample, seed, defer, *params):
         L = _lib.load()
         B, P, ns = AtAy.shape
+        ctx.native = n % 16 == 0 and B > 0
+        if ctx.native:   # the whole call in one library entry point (csrc/dadmm_hyper_net.cpp)
+            return _native_forward(ctx, L, AtAy, Atb, ahat, model, n, per_sample, seed, defer)
         dev = AtAy.device
         stream = _stream(dev)
         enc = model.encoder
@@ -224,6 +229,7 @@ class HyperTrainFn(torch.autograd.Function):
         else:
             xc = torch.cat([AtAy[..., :n], Atb[..., :n]], dim=2).reshape(rows, 2 * n).contiguous()
             x1, ld1, K1, x2, ld2, K = xc, 2 * n, 2 * n, None, 0, 2 * n
+        x1in = (x1, ld1, K1, x2, ld2)   # layer 1's input, for its weight gradient
         saved = []          # per GCN layer: (M, mean, var)
         stats = []          # per GCN layer: (bn, mean, var) for the running statistics
         xs = []             # per GCN layer: its input rows (None for layer 1: rebuilt from AtAy / Atb)
@@ -284,6 +290,7 @@ class HyperTrainFn(torch.autograd.Function):
                 model._bn_pending = []
             model._bn_pending.append((stats, P))
         ctx.model, ctx.n, ctx.per_sample, ctx.seed, ctx.mx = model, n, per_sample, seed, mx
+        ctx.x1in = x1in
         ctx.saved = saved
         ctx.xs, ctx.x5, ctx.dec_in, ctx.dec_xd, ctx.x3, ctx.z = xs, x5, dec_in, dec_xd, x, z
         ctx.AtAy, ctx.Atb, ctx.ahat = AtAy, Atb, ahat
@@ -291,7 +298,15 @@ class HyperTrainFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dhyp):
+        """The reverse of forward on the HIP kernels: head, decoder and encoder backward kernels,
+        the parameter gradients of every linear by dadmm_hyper_wgrad (f32 MFMA, accumulated in
+        place) and the partial sums by dadmm_hyper_colsum, all into the backward pass's flat
+        gradient buffer (_GradAccumulator: one per loss.backward(), whose end callback hands the
+        sums to the parameters' .grad); the input gradients dX = dZ W by dadmm_hyper_linear with
+        the transposed weights. Returns only d AtAy: autograd adds nothing per call."""
         L = _lib.load()
+        if ctx.native:
+            return _native_backward(ctx, L, dhyp)
         model, n = ctx.model, ctx.n
         AtAy, Atb = ctx.AtAy, ctx.Atb
         B, P, ns = AtAy.shape
@@ -303,69 +318,314 @@ class HyperTrainFn(torch.autograd.Function):
         bns = (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)
         p_enc = float(enc.dropout.p)
         H = model.fc.out_features // 4
-        g = {}
+        acc = _GradAccumulator.current(model, dev)
+        chk = _lib.check
         with torch.cuda.device(dev):
             dhyp = dhyp.contiguous()
             dz = torch.empty((B, 4 * H), device=dev)
-            _lib.check("dadmm_hyper_head_act", L.dadmm_hyper_head_act(
+            chk("dadmm_hyper_head_act", L.dadmm_hyper_head_act(
                 1, B, H, _ptr(ctx.z), _ptr(dhyp), *ctx.mx, _ptr(dz), stream))
-            g["fc.w"] = dz.t() @ ctx.x3
-            g["fc.b"] = dz.sum(0)
-            dx = dz @ model.fc.weight
+            fc = model.fc
+            hid = fc.in_features
+            acc.wgrad(B, 4 * H, hid, dz, 4 * H, ctx.x3, hid, hid, None, 0, fc.weight, fc.bias)
+            dx = acc.input_grad(B, dz, 4 * H, fc.weight)            # [B, hid]
             for blk in (2, 1, 0):
                 lin, lnd = model.decoder[4 * blk], model.decoder[4 * blk + 2]
-                N = lin.out_features
+                N, Kin = lin.out_features, lin.in_features
                 dv = torch.empty((B, N), device=dev)
-                part = torch.empty(max(L.dadmm_hyper_rownorm_bwd_part_bytes(B, N), 16) // 4, device=dev)
-                _lib.check("dadmm_hyper_rownorm_bwd", L.dadmm_hyper_rownorm_bwd(
-                    B, N, _ptr(dx.contiguous()), _ptr(ctx.dec_xd[blk]), _ptr(lnd.weight), _ptr(lnd.bias),
+                nbytes = L.dadmm_hyper_rownorm_bwd_part_bytes(B, N)
+                part = torch.empty(max(nbytes, 16) // 4, device=dev)
+                chk("dadmm_hyper_rownorm_bwd", L.dadmm_hyper_rownorm_bwd(
+                    B, N, _ptr(dx), _ptr(ctx.dec_xd[blk]), _ptr(lnd.weight), _ptr(lnd.bias),
                     float(lnd.eps), 1, float(model.decoder[4 * blk + 3].negative_slope),
                     float(model.decoder[4 * blk + 1].p), ctx.seed, 4 + blk, _ptr(dv), _ptr(part), stream))
-                pw = part[:L.dadmm_hyper_rownorm_bwd_part_bytes(B, N) // 4].view(-1, 2, N).sum(0)
-                g[f"ln{blk}.w"], g[f"ln{blk}.b"] = pw[0], pw[1]
-                g[f"lin{blk}.w"] = dv.t() @ ctx.dec_in[blk]
-                g[f"lin{blk}.b"] = dv.sum(0)
-                dx = dv @ lin.weight
+                acc.colsum(part, 1, nbytes // (4 * 2 * N), 2 * N, lnd.weight)   # -> ln.weight, ln.bias
+                acc.wgrad(B, N, Kin, dv, N, ctx.dec_in[blk], Kin, Kin, None, 0, lin.weight, lin.bias)
+                dx = acc.input_grad(B, dv, N, lin.weight)           # [B, Kin]
             # self.norm backward (no dropout, no activation): input x5 [rows, 4h]
             C = ctx.x5.shape[1]
-            dx = dx.reshape(rows, C).contiguous()
             de = torch.empty((rows, C), device=dev)
-            part = torch.empty(max(L.dadmm_hyper_rownorm_bwd_part_bytes(rows, C), 16) // 4, device=dev)
+            nbytes = L.dadmm_hyper_rownorm_bwd_part_bytes(rows, C)
+            part = torch.empty(max(nbytes, 16) // 4, device=dev)
             ln = enc.norm
-            _lib.check("dadmm_hyper_rownorm_bwd", L.dadmm_hyper_rownorm_bwd(
+            chk("dadmm_hyper_rownorm_bwd", L.dadmm_hyper_rownorm_bwd(
                 rows, C, _ptr(dx), _ptr(ctx.x5), _ptr(ln.weight), _ptr(ln.bias), float(ln.eps), 0, 0.0,
                 0.0, ctx.seed, 99, _ptr(de), _ptr(part), stream))
-            pw = part[:L.dadmm_hyper_rownorm_bwd_part_bytes(rows, C) // 4].view(-1, 2, C).sum(0)
-            g["norm.w"], g["norm.b"] = pw[0], pw[1]
+            acc.colsum(part, 1, nbytes // (4 * 2 * C), 2 * C, ln.weight)        # -> norm.weight, .bias
             dx = de
+            dAtAy = torch.zeros_like(AtAy) if ns != n else torch.empty_like(AtAy)
             for i in (4, 3, 2, 1, 0):
                 conv, bn = convs[i], bns[i]
                 N = conv.lin.out_features
                 M, mean, var = ctx.saved[i]
                 dZ = torch.empty((rows, N), device=dev)
                 part = torch.empty((3, B, N), device=dev)
-                _lib.check("dadmm_hyper_gcn_train_bwd", L.dadmm_hyper_gcn_train_bwd(
-                    B, P, N, _ptr(dx.contiguous()), _ptr(M), _ptr(mean), _ptr(var), _ptr(bn.weight),
+                chk("dadmm_hyper_gcn_train_bwd", L.dadmm_hyper_gcn_train_bwd(
+                    B, P, N, _ptr(dx), _ptr(M), _ptr(mean), _ptr(var), _ptr(bn.weight),
                     float(bn.eps), _ptr(ctx.ahat), int(ctx.per_sample), LEAKY_SLOPE,
                     p_enc if i < 4 else 0.0, ctx.seed, i, _ptr(dZ), _ptr(part), stream))
-                ps = part.sum(1)
-                g[f"bn{i}.w"], g[f"bn{i}.b"], g[f"conv{i}.b"] = ps[0], ps[1], ps[2]
-                xin = ctx.xs[i]
-                if xin is None:
-                    xin = torch.cat([AtAy[..., :n], Atb[..., :n]], dim=2).reshape(rows, 2 * n)
-                g[f"conv{i}.w"] = dZ.t() @ xin
-                dx = dZ @ conv.lin.weight
-            dAtAy = torch.zeros_like(AtAy)
-            dAtAy[..., :n] = dx.reshape(B, P, 2 * n)[..., :n]
-        grads = []
-        for i in range(5):
-            grads += [g[f"conv{i}.w"], g[f"conv{i}.b"], g[f"bn{i}.w"], g[f"bn{i}.b"]]
-        grads += [g["norm.w"], g["norm.b"]]
-        for blk in range(3):
-            grads += [g[f"lin{blk}.w"], g[f"lin{blk}.b"], g[f"ln{blk}.w"], g[f"ln{blk}.b"]]
-        grads += [g["fc.w"], g["fc.b"]]
+                acc.colsum(part, 3, B, N, bn.weight)          # -> bn.weight, bn.bias, conv.bias
+                Kin = conv.lin.in_features
+                if i == 0:
+                    # layer 1's input cat(AtAy, Atb) read in place; only d AtAy is needed
+                    x1, ld1, K1, x2, ld2 = ctx.x1in
+                    acc.wgrad(rows, N, Kin, dZ, N, x1, ld1, K1, x2, ld2, conv.lin.weight, None)
+                    acc.input_grad(rows, dZ, N, conv.lin.weight, cols=n, out=dAtAy, ldo=ns)
+                else:
+                    acc.wgrad(rows, N, Kin, dZ, N, ctx.xs[i], Kin, Kin, None, 0, conv.lin.weight, None)
+                    dx = acc.input_grad(rows, dZ, N, conv.lin.weight)
         ctx.saved = ctx.xs = ctx.dec_in = ctx.dec_xd = None
-        return (dAtAy, None, None, None, None, None, None, None, *grads)
+        return (dAtAy, None, None, None, None, None, None, None) + (None,) * len(_hyper_params(model))
+
+
+# ---- one library call per iteration (dadmm_hyper_train_forward / _backward) -------------------
+
+def _native_net(model, P, n, ns, dev):
+    """The dadmm_hyper_net struct of ``model`` (parameter pointers, dimensions, constants), cached
+    on the model and rebuilt when a parameter's storage, a dropout p or a maximum changes."""
+    enc = model.encoder
+    convs = (enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5)
+    bns = (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)
+    params = _hyper_params(model)
+    key = (P, n, ns, str(dev), tuple(p.data_ptr() for p in params), float(enc.dropout.p),
+           tuple(float(model.decoder[4 * j + 1].p) for j in range(3)),
+           tuple(float(v) for v in (model.alpha_max, model.tau_max, model.rho_max, model.eta_max)))
+    hit = getattr(model, "_native_net", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    net = _lib.HyperNet()
+    net.P, net.n, net.ld = P, n, ns
+    for i, (conv, bn) in enumerate(zip(convs, bns)):
+        net.width[i] = conv.lin.out_features
+        net.conv_w[i], net.conv_b[i] = conv.lin.weight.data_ptr(), conv.bias.data_ptr()
+        net.bn_w[i], net.bn_b[i], net.bn_eps[i] = bn.weight.data_ptr(), bn.bias.data_ptr(), float(bn.eps)
+    net.norm_w, net.norm_b, net.norm_eps = enc.norm.weight.data_ptr(), enc.norm.bias.data_ptr(), float(enc.norm.eps)
+    for j in range(3):
+        lin, ln = model.decoder[4 * j], model.decoder[4 * j + 2]
+        net.dec_width[j] = lin.out_features
+        net.dec_w[j], net.dec_b[j] = lin.weight.data_ptr(), lin.bias.data_ptr()
+        net.ln_w[j], net.ln_b[j], net.ln_eps[j] = ln.weight.data_ptr(), ln.bias.data_ptr(), float(ln.eps)
+        net.dec_slope[j] = float(model.decoder[4 * j + 3].negative_slope)
+        net.dec_drop[j] = float(model.decoder[4 * j + 1].p)
+    net.H = model.fc.out_features // 4
+    net.fc_w, net.fc_b = model.fc.weight.data_ptr(), model.fc.bias.data_ptr()
+    net.drop_enc = float(enc.dropout.p)
+    for c, v in enumerate((model.alpha_max, model.tau_max, model.rho_max, model.eta_max)):
+        net.maxv[c] = float(v)
+    model._native_net = (key, net)
+    return net
+
+
+def _native_work(model, L, net, B, dev):
+    """The shared work buffer (dadmm_hyper_train_work_bytes) for batch B, cached on the model."""
+    nbytes = L.dadmm_hyper_train_work_bytes(ctypes.byref(net), B)
+    if nbytes == 0:
+        raise ValueError("dadmm_hyper_train_work_bytes: hypernetwork dimensions not supported")
+    w = getattr(model, "_native_work", None)
+    if w is None or w.numel() * 4 < nbytes or w.device != dev:
+        w = torch.empty(nbytes // 4 + 4, device=dev)
+        model._native_work = w
+    return w
+
+
+def _native_forward(ctx, L, AtAy, Atb, ahat, model, n, per_sample, seed, defer):
+    B, P, ns = AtAy.shape
+    dev = AtAy.device
+    net = _native_net(model, P, n, ns, dev)
+    rows = B * P
+    W = list(net.width)
+    DW = list(net.dec_width)
+    H = net.H
+    # one arena for the call's saved activations (16-byte aligned slices)
+    sizes = ([rows * w for w in W] + [rows * w for w in W] + [B * w for w in W] + [B * w for w in W]
+             + [rows * W[4]] + [B * d for d in DW] + [B * d for d in DW] + [B * 4 * H, B * 4 * H])
+    offs, o = [], 0
+    for sz in sizes:
+        offs.append(o)
+        o += (sz + 3) & ~3
+    arena = torch.empty(o, device=dev)
+    base = arena.data_ptr()
+    sv = _lib.HyperSaved()
+    it = iter(range(len(sizes)))
+    for field in ("y", "m", "mean", "var"):
+        arr = getattr(sv, field)
+        for i in range(5):
+            arr[i] = base + 4 * offs[next(it)]
+    sv.e = base + 4 * offs[next(it)]
+    for j in range(3):
+        sv.dec_y[j] = base + 4 * offs[next(it)]
+    for j in range(3):
+        sv.dec_xd[j] = base + 4 * offs[next(it)]
+    sv.z = base + 4 * offs[next(it)]
+    ih = next(it)
+    sv.hyp = base + 4 * offs[ih]
+    work = _native_work(model, L, net, B, dev)
+    with torch.cuda.device(dev):
+        _lib.check("dadmm_hyper_train_forward", L.dadmm_hyper_train_forward(
+            ctypes.byref(net), B, _ptr(AtAy), _ptr(Atb), _ptr(ahat), int(per_sample), seed,
+            ctypes.byref(sv), _ptr(work), _stream(dev)))
+    # the batch statistics of every GCN block, for the running-statistics updates
+    enc = model.encoder
+    stats = []
+    for i, bn in enumerate((enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)):
+        mean = arena[offs[10 + i]:offs[10 + i] + B * W[i]].view(B, W[i])
+        var = arena[offs[15 + i]:offs[15 + i] + B * W[i]].view(B, W[i])
+        stats.append((bn, mean, var))
+    if defer:
+        if not hasattr(model, "_bn_pending"):
+            model._bn_pending = []
+        model._bn_pending.append((stats, P))
+    else:
+        with torch.no_grad():
+            for bn, mean, var in stats:
+                _update_running_stats(bn, mean, var, P)
+    ctx.model, ctx.n, ctx.per_sample, ctx.seed = model, n, per_sample, seed
+    ctx.arena, ctx.sv, ctx.net = arena, sv, net
+    ctx.AtAy, ctx.Atb, ctx.ahat = AtAy, Atb, ahat
+    return arena[offs[ih]:offs[ih] + B * 4 * H].view(B, 4, H)
+
+
+def _native_backward(ctx, L, dhyp):
+    model, n = ctx.model, ctx.n
+    AtAy, Atb = ctx.AtAy, ctx.Atb
+    B, P, ns = AtAy.shape
+    dev = AtAy.device
+    acc = _GradAccumulator.current(model, dev)
+    g = acc.grads_struct()
+    net = ctx.net
+    work = _native_work(model, L, net, B, dev)
+    dAtAy = torch.zeros_like(AtAy) if ns != n else torch.empty_like(AtAy)
+    with torch.cuda.device(dev):
+        _lib.check("dadmm_hyper_train_backward", L.dadmm_hyper_train_backward(
+            ctypes.byref(net), B, _ptr(AtAy), _ptr(Atb), _ptr(ctx.ahat), int(ctx.per_sample), ctx.seed,
+            ctypes.byref(ctx.sv), _ptr(dhyp.contiguous()), ctypes.byref(g), _ptr(dAtAy), _ptr(work),
+            _stream(dev)))
+    ctx.arena = ctx.sv = None
+    return (dAtAy, None, None, None, None, None, None, None) + (None,) * len(_hyper_params(model))
+
+
+class _GradAccumulator:
+    """The hypernetwork's parameter gradients of ONE backward pass, in one flat float32 buffer laid
+    out so that every group the kernels produce together is contiguous: per GCN layer
+    [lin.weight | bn.weight | bn.bias | conv.bias] (dadmm_hyper_gcn_train_bwd's [3][B][N]
+    partials reduce in one dadmm_hyper_colsum), LayerNorm [weight | bias], Linear [weight | bias].
+    Created by the first HyperTrainFn.backward of a pass; the autograd engine's end-of-backward
+    callback adds the sums to the parameters' .grad (set when None, accumulated otherwise) — in
+    place of autograd's per-call, per-parameter accumulation kernels. Also caches the transposed
+    weights of the input-gradient GEMMs (the weights do not change during a backward pass)."""
+
+    def __init__(self, model, dev):
+        self.model = model
+        self.L = _lib.load()
+        self.stream = _stream(dev)
+        self.dev = dev
+        enc = model.encoder
+        order = []
+        for conv, bn in zip((enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5),
+                            (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)):
+            order += [conv.lin.weight, bn.weight, bn.bias, conv.bias]   # [3][N] partials: contiguous
+        order += [enc.norm.weight, enc.norm.bias]
+        for blk in range(3):
+            lin, ln = model.decoder[4 * blk], model.decoder[4 * blk + 2]
+            order += [lin.weight, lin.bias, ln.weight, ln.bias]
+        order += [model.fc.weight, model.fc.bias]
+        self.off = {}
+        o = 0
+        for p in order:
+            self.off[id(p)] = o
+            o += (p.numel() + 3) & ~3              # 16-byte aligned (widths are multiples of 4)
+        self.params = order
+        self.flat = torch.zeros(o, device=dev)
+        self.wt = {}
+        self.scratch = torch.empty(0, device=dev)
+
+    @staticmethod
+    def current(model, dev):
+        """The accumulator of the running backward pass (keyed by autograd's graph-task id, so a
+        pass that ended in an exception never leaks its partial sums into the next one)."""
+        task = torch._C._current_graph_task_id()
+        acc = getattr(model, "_grad_acc", None)
+        if acc is None or acc.task != task:
+            acc = _GradAccumulator(model, dev)
+            acc.task = task
+            model._grad_acc = acc
+            torch.autograd.Variable._execution_engine.queue_callback(acc.finalize)
+        return acc
+
+    def ptr(self, p):
+        return self.flat.data_ptr() + 4 * self.off[id(p)]
+
+    def view(self, p):
+        o = self.off[id(p)]
+        return self.flat[o:o + p.numel()].view_as(p)
+
+    def wgrad(self, R, N, K, dz, ldz, x1, ld1, K1, x2, ld2, weight, bias):
+        nb = self.L.dadmm_hyper_wgrad_scratch_bytes(R, N, K)
+        if nb > 4 * self.scratch.numel():
+            self.scratch = torch.empty(nb // 4 + 4, device=self.dev)
+        gb = ctypes.c_void_p(self.ptr(bias)) if bias is not None else None
+        _lib.check("dadmm_hyper_wgrad", self.L.dadmm_hyper_wgrad(
+            R, N, K, _ptr(dz), ldz, _ptr(x1), ld1, K1, _ptr(x2), ld2, ctypes.c_void_p(self.ptr(weight)),
+            gb, 1, _ptr(self.scratch), self.stream))
+
+    def colsum(self, part, G, R, C, first):
+        _lib.check("dadmm_hyper_colsum", self.L.dadmm_hyper_colsum(
+            _ptr(part), G, R, C, ctypes.c_void_p(self.ptr(first)), 1, self.stream))
+
+    def input_grad(self, R, dz, N, weight, cols=None, out=None, ldo=None):
+        """dX [R][cols] = dZ [R][N] W [N][cols] (the first ``cols`` input columns)."""
+        wt = self.transposed(weight)
+        cols = wt.shape[0] if cols is None else cols
+        if out is None:
+            out = torch.empty((R, cols), device=self.dev)
+            ldo = cols
+        _lib.check("dadmm_hyper_linear", self.L.dadmm_hyper_linear(
+            R, N, cols, _ptr(dz), N, N, None, 0, _ptr(wt), None, _ptr(out), ldo, self.stream))
+        return out
+
+    def transposed(self, weight):
+        wt = self.wt.get(id(weight))
+        if wt is None:
+            Nw, Kw = weight.shape
+            wt = torch.empty((Kw, Nw), device=self.dev)
+            _lib.check("dadmm_hyper_transpose", self.L.dadmm_hyper_transpose(
+                Nw, Kw, _ptr(weight), _ptr(wt), self.stream))
+            self.wt[id(weight)] = wt
+        return wt
+
+    def grads_struct(self):
+        """dadmm_hyper_grads: this pass's accumulators and the transposed weights (built once)."""
+        g = getattr(self, "_gstruct", None)
+        if g is not None:
+            return g
+        model = self.model
+        enc = model.encoder
+        g = _lib.HyperGrads()
+        for i, (conv, bn) in enumerate(zip((enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5),
+                                           (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5))):
+            g.conv_w[i] = self.ptr(conv.lin.weight)
+            g.bn_wbc[i] = self.ptr(bn.weight)
+            g.conv_wt[i] = self.transposed(conv.lin.weight).data_ptr()
+        g.norm_wb = self.ptr(enc.norm.weight)
+        for j in range(3):
+            lin, ln = model.decoder[4 * j], model.decoder[4 * j + 2]
+            g.dec_w[j], g.dec_b[j], g.ln_wb[j] = self.ptr(lin.weight), self.ptr(lin.bias), self.ptr(ln.weight)
+            g.dec_wt[j] = self.transposed(lin.weight).data_ptr()
+        g.fc_w, g.fc_b = self.ptr(model.fc.weight), self.ptr(model.fc.bias)
+        g.fc_wt = self.transposed(model.fc.weight).data_ptr()
+        self._gstruct = g
+        return g
+
+    def finalize(self):
+        if getattr(self.model, "_grad_acc", None) is self:
+            self.model._grad_acc = None
+        with torch.no_grad():
+            for p in self.params:
+                g = self.view(p)
+                if p.grad is None:
+                    p.grad = g
+                else:
+                    p.grad.add_(g)
 
 
 def draw_dropout_seed() -> int:

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 11
+#define DADMM_ABI_VERSION 12
 
 enum {
     DADMM_OK = 0,
@@ -407,6 +407,92 @@ int dadmm_hyper_rownorm_bwd(int32_t rows, int32_t C, const float* dy, const floa
 int dadmm_hyper_head_act(int32_t mode, int32_t B, int32_t H, const float* z, const float* dhyp,
                          float alpha_max, float tau_max, float rho_max, float eta_max, float* out,
                          void* stream);
+
+/* ---- GNN hypernetwork training: parameter gradients on hand-written kernels ------------------
+ * Replace the weight / bias gradients torch's autograd computes through hipBLASLt and its sums
+ * (gnn_dlasso_progressive.py:207-214 loss_final.backward() through the hypernetwork of
+ * gnn_dlasso_models_progressive.py:9-72, :93-123), accumulated in place in a fixed order.
+ * dadmm_hyper_wgrad: g [N][K] (+)= dZ^T X over R rows (f32 MFMA); X = cat of x1 (columns < K1,
+ *   leading dimension ld1) and x2 (the other K - K1 columns, ld2); gbias [N] (+)= column sums of dZ
+ *   (nullable); beta = 1 accumulates. scratch: dadmm_hyper_wgrad_scratch_bytes (0: none needed).
+ * dadmm_hyper_colsum: out [G][C] (+)= sum_r part [G][R][C] (the per-block partials of
+ *   dadmm_hyper_gcn_train_bwd / dadmm_hyper_rownorm_bwd), rows in order.
+ * dadmm_hyper_transpose: out [cols][rows] = in [rows][cols] (the weights of the input-gradient
+ *   GEMMs dX = dZ W, run as dadmm_hyper_linear with W^T). */
+size_t dadmm_hyper_wgrad_scratch_bytes(int32_t R, int32_t N, int32_t K);
+int dadmm_hyper_wgrad(int32_t R, int32_t N, int32_t K, const float* dz, int32_t ldz, const float* x1,
+                      int32_t ld1, int32_t K1, const float* x2, int32_t ld2, float* g, float* gbias,
+                      int32_t beta, void* scratch, void* stream);
+int dadmm_hyper_colsum(const float* part, int32_t G, int32_t R, int32_t C, float* out, int32_t beta,
+                       void* stream);
+int dadmm_hyper_transpose(int32_t rows, int32_t cols, const float* in, float* out, void* stream);
+
+/* ---- GNN hypernetwork training: one call per iteration (host orchestration in the library) ----
+ * dadmm_hyper_train_forward runs the whole training-mode hypernetwork of one iteration
+ * (gnn_dlasso_models_progressive.py:165-196 with :52-72 in train mode: 5 GCN blocks, LayerNorm,
+ * 3 decoder blocks, fc, head) and stores its activations in `sv` (caller-allocated, 16-byte
+ * aligned); dadmm_hyper_train_backward runs its backward from d hyp, ACCUMULATES (+=) every
+ * parameter gradient into `g` (contiguous groups as the partial sums come: [bn.weight | bn.bias |
+ * conv.bias], [LayerNorm weight | bias]) and writes the first n columns of d AtAy (row stride
+ * net->ld). `work`: dadmm_hyper_train_work_bytes (16-byte aligned), shared by both. The dropout
+ * masks of both come from `seed` (the same value for an iteration's forward and backward).
+ * Requires P >= 2, n % 16 == 0 and widths that are multiples of 4 (else DADMM_EINVAL /
+ * DADMM_EUNSUPPORTED: the caller runs the per-kernel entry points above). */
+typedef struct dadmm_hyper_net {
+    int32_t P, n, ld;           /* agents; signal length; row stride of AtAy / Atb / dAtAy       */
+    int32_t width[5];           /* GCNConv output widths (h, 2h, 4h, 4h, 4h)                     */
+    int32_t dec_width[3];       /* decoder Linear output widths (4h, 2h, h)                      */
+    int32_t H;                  /* P ('diff') or 1 ('same'): fc outputs 4H                       */
+    const float* conv_w[5];     /* [width_i][width_{i-1}] (layer 1: [width_0][2n])               */
+    const float* conv_b[5];
+    const float* bn_w[5];
+    const float* bn_b[5];
+    float bn_eps[5];
+    const float* norm_w;
+    const float* norm_b;
+    float norm_eps;
+    const float* dec_w[3];
+    const float* dec_b[3];
+    const float* ln_w[3];
+    const float* ln_b[3];
+    float ln_eps[3], dec_slope[3], dec_drop[3];
+    const float* fc_w;
+    const float* fc_b;
+    float drop_enc;             /* the encoder's Dropout p                                        */
+    float maxv[4];              /* alpha_max, tau_max, rho_max, eta_max                           */
+} dadmm_hyper_net;
+typedef struct dadmm_hyper_saved {
+    float* y[5];                /* [B*P][width_i] block outputs                                   */
+    float* m[5];                /* [B*P][width_i] pre-activation mixes                            */
+    float* mean[5];             /* [B][width_i] batch statistics                                  */
+    float* var[5];
+    float* e;                   /* [B*P][width_4] LayerNorm output = decoder input                */
+    float* dec_y[3];            /* [B][dec_width_j] block outputs                                 */
+    float* dec_xd[3];           /* [B][dec_width_j] LayerNorm inputs (after Dropout)              */
+    float* z;                   /* [B][4H] fc logits                                              */
+    float* hyp;                 /* [B][4][H] the iteration's (alpha, tau, rho, eta)               */
+} dadmm_hyper_saved;
+typedef struct dadmm_hyper_grads {
+    float* conv_w[5];
+    float* bn_wbc[5];           /* [3][width_i]: bn.weight, bn.bias, conv.bias                    */
+    float* norm_wb;             /* [2][width_4]                                                   */
+    float* dec_w[3];
+    float* dec_b[3];
+    float* ln_wb[3];            /* [2][dec_width_j]                                               */
+    float* fc_w;
+    float* fc_b;
+    const float* conv_wt[5];    /* transposed weights (dadmm_hyper_transpose) for dX = dZ W       */
+    const float* dec_wt[3];
+    const float* fc_wt;
+} dadmm_hyper_grads;
+size_t dadmm_hyper_train_work_bytes(const dadmm_hyper_net* net, int32_t B);
+int dadmm_hyper_train_forward(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
+                              const float* ahat, int32_t ahat_per_sample, uint64_t seed,
+                              const dadmm_hyper_saved* sv, void* work, void* stream);
+int dadmm_hyper_train_backward(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
+                               const float* ahat, int32_t ahat_per_sample, uint64_t seed,
+                               const dadmm_hyper_saved* sv, const float* dhyp, const dadmm_hyper_grads* g,
+                               float* dAtAy, void* work, void* stream);
 
 #ifdef __cplusplus
 }

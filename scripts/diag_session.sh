@@ -1,13 +1,15 @@
 #!/bin/bash
 # Diagnostics of the fused kernel at the headline shape: per-phase stamps (diagnostic build
 # build/ablate/libdadmm_stamps.so) and the two SQ counter groups of scripts/pmc.sh on the
-# in-tree library. Each GPU step has its own time limit; the first failure ends the script.
+# in-tree library (or the build/var variant named by LIBV, e.g. LIBV=sync). Each GPU step has
+# its own time limit; the first failure ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-diag}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-if [ -f build/ablate/libdadmm_stamps.so ]; then
+[ -n "${LIBV:-}" ] && export DADMM_LIB_VARIANT=$PWD/build/var/libdadmm_$LIBV.so
+if [ -z "${LIBV:-}" ] && [ -f build/ablate/libdadmm_stamps.so ]; then
   timeout -k 10 120 python3 scripts/stamps.py > "$OUT/stamps.json" 2> "$OUT/stamps.err"
   rc=$?; echo "stamps rc=$rc"; cat "$OUT/stamps.json"; [ $rc -eq 0 ] || exit $rc
 fi

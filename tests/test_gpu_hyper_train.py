@@ -265,3 +265,48 @@ def test_model_train_step_uses_hip_hypernetwork(cuda):
     for (name, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
         assert p1.grad is not None and torch.isfinite(p1.grad).all(), name
         _close(p1.grad, p2.grad, rel=5e-3, name=name)
+
+
+@pytest.mark.parametrize("R,N,K,K1,beta", [(1280, 400, 400, 400, 1), (1280, 100, 512, 256, 0),
+                                           (256, 400, 2000, 2000, 1), (256, 20, 100, 100, 1),
+                                           (37, 13, 70, 70, 0), (51200, 100, 2048, 1024, 1)])
+def test_wgrad_colsum_transpose_kernels(cuda, R, N, K, K1, beta):
+    """dadmm_hyper_wgrad (G (+)= dZ^T X with the bias column sums, X read as two segments),
+    dadmm_hyper_colsum and dadmm_hyper_transpose against fp64 references; deterministic."""
+    import ctypes
+    from dadmm_hip import _lib
+    from dadmm_hip.ops import _ptr, _stream
+    L = _lib.load()
+    g = torch.Generator(device=cuda).manual_seed(R + N + K)
+    dz = torch.randn(R, N, device=cuda, generator=g)
+    x1 = torch.randn(R, K1 + 8, device=cuda, generator=g)     # padded rows: ld1 > K1
+    x2 = torch.randn(R, K - K1 + 4, device=cuda, generator=g) if K1 < K else None
+    G0 = torch.randn(N, K, device=cuda, generator=g)
+    b0 = torch.randn(N, device=cuda, generator=g)
+    nb = L.dadmm_hyper_wgrad_scratch_bytes(R, N, K)
+    scratch = torch.empty(max(nb, 16) // 4 + 4, device=cuda)
+    outs = []
+    for _ in range(2):
+        Gm, bm = G0.clone(), b0.clone()
+        _lib.check("dadmm_hyper_wgrad", L.dadmm_hyper_wgrad(
+            R, N, K, _ptr(dz), N, _ptr(x1), K1 + 8, K1, _ptr(x2), (K - K1 + 4) if x2 is not None else 0,
+            _ptr(Gm), _ptr(bm), beta, _ptr(scratch), _stream(cuda)))
+        outs.append((Gm, bm))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    X = x1[:, :K1].double() if x2 is None else torch.cat([x1[:, :K1], x2[:, :K - K1]], 1).double()
+    want = dz.double().t() @ X + (G0.double() if beta else 0)
+    wantb = dz.double().sum(0) + (b0.double() if beta else 0)
+    scale = float((dz.double().abs().t() @ X.abs()).max())
+    assert float((outs[0][0].double() - want).abs().max()) <= 2e-6 * scale + 1e-6
+    assert float((outs[0][1].double() - wantb).abs().max()) <= 2e-6 * float(dz.abs().sum(0).max()) + 1e-6
+    # colsum: out [G][C] (+)= sum_r part [G][R][C]
+    part = torch.randn(3, min(R, 300), N, device=cuda, generator=g)
+    out = torch.randn(3, N, device=cuda, generator=g)
+    ref = out.double() + part.double().sum(1)
+    _lib.check("dadmm_hyper_colsum", L.dadmm_hyper_colsum(_ptr(part), 3, part.shape[1], N, _ptr(out), 1,
+                                                          _stream(cuda)))
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4)
+    # transpose
+    t = torch.empty(K, N, device=cuda)
+    _lib.check("dadmm_hyper_transpose", L.dadmm_hyper_transpose(N, K, _ptr(G0), _ptr(t), _stream(cuda)))
+    assert torch.equal(t, G0.t())
