@@ -931,8 +931,10 @@ int dadmm_hyper_wgrad(int32_t R, int32_t N, int32_t K, const float* dz, int32_t 
         if (e != hipSuccess) return fail(DADMM_EHIP, "memset: %s", hipGetErrorString(e));
         return ok();
     }
-    dadmm::WgradArgs a{dz, x1, K1 < K ? x2 : x1, g, gbias, (float*)scratch,
-                       splits > 1 ? (float*)scratch + (size_t)splits * N * K : nullptr,
+    // scratch: [splits][N][K] partial tiles, [splits][N] partial bias sums
+    float* part = splits > 1 ? (float*)scratch : nullptr;
+    dadmm::WgradArgs a{dz, x1, K1 < K ? x2 : x1, g, gbias, part,
+                       splits > 1 ? part + (size_t)splits * N * K : nullptr,
                        R, N, K, K1, ldz, ld1, K1 < K ? ld2 : ld1, splits, beta ? 1 : 0};
     hipError_t e = dadmm::launch_wgrad(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(DADMM_EHIP, "wgrad launch: %s", hipGetErrorString(e));

@@ -8,11 +8,13 @@
 //                   g_bias[N] += sum_r dZ[r][n] (the bias gradient) from the same dZ reads.
 //                   f32 MFMA v_mfma_f32_16x16x4_f32 with the R rows as the reduction (k) dimension:
 //                   lane (i, h) feeds dZ[r + h][n0 + i] and X[r + h][k0 + i]. One workgroup per
-//                   64 x 64 output tile and R-split; splits > 1 write partial tiles to scratch that
-//                   reduce_kernel adds into G in split order.
+//                   32 x 32 output tile (and R-split): its 4 waves take interleaved 4-row steps
+//                   (RING in flight each) and add their partial tiles through LDS in wave order.
+//                   Splits > 1 (short grids) write partial tiles that reduce_kernel adds into G in
+//                   split order.
 //   colsum_kernel : out[g][c] += sum_r part[g][r][c] — the per-block partial sums of the BatchNorm /
 //                   bias (dadmm_hyper_gcn_train_bwd) and LayerNorm (dadmm_hyper_rownorm_bwd) parameter
-//                   gradients, one thread per output column, rows in order.
+//                   gradients: 16 columns x 16 row slices per workgroup, slices added in order.
 // Every sum runs in a fixed order: the gradients are deterministic run to run. They match torch's
 // autograd (hipBLASLt) to f32 rounding of a different summation order.
 
@@ -26,8 +28,9 @@ namespace hgrad {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int THREADS = 256;
-constexpr int TN = 64, TK = 64;   // output tile (n x k) per workgroup: 4 waves of 32 x 32
-constexpr int RING = 4;           // row steps (4 rows each) of operands in flight per wave
+constexpr int TN = 32, TK = 32;   // output tile (n x k) per workgroup; 4 waves split its rows
+constexpr int WAVES = THREADS / 64;
+constexpr int RING = 8;           // row steps (4 rows each) of operands in flight per wave
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -42,13 +45,14 @@ __device__ __forceinline__ int xcd_tile(int bid, int G) {
 }
 
 __global__ __launch_bounds__(THREADS) void wgrad_kernel(WgradArgs a) {
+    __shared__ float red[WAVES - 1][16][64];    // waves 1..3's partial tiles (16 floats per lane)
+    __shared__ float redb[WAVES - 1][2][16];    // and their bias column sums
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = lane & 15, h = lane >> 4;
-    const int wn = w >> 1, wk = w & 1;
     const int gn = (a.N + TN - 1) / TN, gk = (a.K + TK - 1) / TK;
     const int tl = xcd_tile(blockIdx.x, gridDim.x);
     const int kt = tl % gk, nt = (tl / gk) % gn, split = tl / (gk * gn);
-    const int n0 = nt * TN + wn * 32, k0 = kt * TK + wk * 32;
+    const int n0 = nt * TN, k0 = kt * TK;
     const int steps = (a.R + 3) / 4;
     const int per = (steps + a.splits - 1) / a.splits;
     const int s_begin = split * per;
@@ -72,29 +76,31 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(WgradArgs a) {
             ldx[b] = a.ld2;
         }
     }
-    const bool do_bias = a.gbias != nullptr && kt == 0 && wk == 0;
+    const bool do_bias = a.gbias != nullptr && kt == 0;
 
     f32x4 acc[2][2];
 #pragma unroll
     for (int x = 0; x < 2; ++x) acc[x][0] = acc[x][1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
     float bsum[2] = {0.0f, 0.0f};
 
+    // wave w: steps s_begin + w, + WAVES, ...
     float ra[RING][2], rb[RING][2];
     auto load = [&](int u, int st) {
         const int r = 4 * st + h;
-        const bool ok = r < a.R && st < s_end;
+        const bool ok = st < s_end && r < a.R;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             ra[u][b] = ok ? a.dz[(size_t)r * a.ldz + nc[b]] : 0.0f;
             rb[u][b] = ok ? xs[b][(size_t)r * ldx[b]] : 0.0f;
         }
     };
+    const int first = s_begin + w;
 #pragma unroll
-    for (int u = 0; u < RING; ++u) load(u, s_begin + u);
-    for (int st = s_begin; st < s_end; st += RING) {
+    for (int u = 0; u < RING; ++u) load(u, first + WAVES * u);
+    for (int st = first; st < s_end; st += WAVES * RING) {
 #pragma unroll
         for (int u = 0; u < RING; ++u) {
-            if (st + u < s_end) {
+            if (st + WAVES * u < s_end) {
 #pragma unroll
                 for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -104,8 +110,42 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(WgradArgs a) {
                     bsum[1] += ra[u][1];
                 }
             }
-            load(u, st + u + RING);
+            load(u, st + WAVES * (u + RING));
             __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // bias: the 4 row groups h of the wave, in order
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const float v1 = __shfl_down(bsum[b], 16), v2 = __shfl_down(bsum[b], 32), v3 = __shfl_down(bsum[b], 48);
+        bsum[b] = ((bsum[b] + v1) + v2) + v3;
+    }
+    // waves 1..3 hand their partials to wave 0, which adds them in wave order
+    if (w > 0) {
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) red[w - 1][8 * x + 4 * y + q][lane] = acc[x][y][q];
+        if (do_bias && h == 0) {
+            redb[w - 1][0][i] = bsum[0];
+            redb[w - 1][1][i] = bsum[1];
+        }
+    }
+    __syncthreads();
+    if (w > 0) return;
+#pragma unroll
+    for (int v = 0; v < WAVES - 1; ++v) {
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[x][y][q] += red[v][8 * x + 4 * y + q][lane];
+        if (do_bias && h == 0) {
+            bsum[0] += redb[v][0][i];
+            bsum[1] += redb[v][1][i];
         }
     }
     // acc[x][y]: lane (i, h) holds G rows n0 + 16 x + 4 h + q (q = 0..3), column k0 + 16 y + i
@@ -125,19 +165,13 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(WgradArgs a) {
                 *o = accum ? *o + acc[x][y][q] : acc[x][y][q];
             }
         }
-    if (do_bias) {
-        // column sums of dZ over this split's rows: lanes (i, h) hold rows 4 st + h; the 4 groups
-        // h are added in order
+    if (do_bias && h == 0) {
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            float v = bsum[b];
-            const float v1 = __shfl_down(v, 16), v2 = __shfl_down(v, 32), v3 = __shfl_down(v, 48);
-            v = ((v + v1) + v2) + v3;
             const int n = n0 + 16 * b + i;
-            if (h == 0 && n < a.N) {
-                if (a.splits > 1) a.scratch_bias[(size_t)split * a.N + n] = v;
-                else a.gbias[n] = a.beta != 0 ? a.gbias[n] + v : v;
-            }
+            if (n >= a.N) continue;
+            if (a.splits > 1) a.scratch_bias[(size_t)split * a.N + n] = bsum[b];
+            else a.gbias[n] = a.beta != 0 ? a.gbias[n] + bsum[b] : bsum[b];
         }
     }
 }
@@ -153,16 +187,38 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(const float* __restrict
     dst[idx] = v + s;
 }
 
-// out[g][c] (+)= sum_r part[g][r][c], r in order; one thread per (g, c)
+// out[g][c] (+)= sum_r part[g][r][c]. The partial rows are few columns wide and short (a few
+// hundred rows), so the sum is latency-bound: each workgroup takes CS_C = 16 columns of one g and
+// splits the rows over CS_S = 16 slices (slice s: rows s, s + 16, ..., 8 loads in flight), then
+// adds the 16 slice sums in slice order through LDS — a fixed order, deterministic run to run.
+constexpr int CS_C = 16, CS_S = THREADS / CS_C;
 __global__ __launch_bounds__(THREADS) void colsum_kernel(const float* __restrict__ part, int G, int R, int C,
                                                          float* __restrict__ out, int beta) {
-    const int idx = blockIdx.x * THREADS + threadIdx.x;
-    if (idx >= G * C) return;
-    const int g = idx / C, c = idx - g * C;
+    __shared__ float red[CS_S][CS_C + 1];
+    const int cb = (C + CS_C - 1) / CS_C;
+    const int g = blockIdx.x / cb, c0 = (blockIdx.x % cb) * CS_C;
+    const int cl = threadIdx.x % CS_C, sl = threadIdx.x / CS_C;
+    const int c = c0 + cl < C ? c0 + cl : C - 1;
     const float* p = part + (size_t)g * R * C + c;
     float s = 0.0f;
-    for (int r = 0; r < R; ++r) s += p[(size_t)r * C];
-    out[idx] = beta ? out[idx] + s : s;
+    int r = sl;
+    for (; r + 7 * CS_S < R; r += 8 * CS_S) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(r + u * CS_S) * C];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; r < R; r += CS_S) s += p[(size_t)r * C];
+    red[sl][cl] = s;
+    __syncthreads();
+    if (sl == 0 && c0 + cl < C) {
+        float t = 0.0f;
+#pragma unroll
+        for (int k = 0; k < CS_S; ++k) t += red[k][cl];
+        float* o = out + (size_t)g * C + c0 + cl;
+        *o = beta ? *o + t : t;
+    }
 }
 
 // out [cols][rows] = in [rows][cols], 32 x 32 tiles through LDS (the weight transposes the input
@@ -196,9 +252,9 @@ int wgrad_splits(int R, int N, int K) {
     const int tiles = ((N + hgrad::TN - 1) / hgrad::TN) * ((K + hgrad::TK - 1) / hgrad::TK);
     const int steps = (R + 3) / 4;
     int s = 1;
-    // split the rows while the grid is short of ~2 workgroups per CU and each split keeps >= 32
-    // row steps (128 rows)
-    while (tiles * s * 2 <= 512 && steps / (2 * s) >= 32) s *= 2;
+    // split the rows while the grid is short of one workgroup per CU and every wave of a split
+    // keeps >= 8 row steps
+    while (tiles * s * 2 <= 256 && steps / (2 * s) >= 8 * hgrad::WAVES) s *= 2;
     return s;
 }
 
@@ -218,9 +274,8 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_colsum(const float* part, int G, int R, int C, float* out, int beta, hipStream_t st) {
-    const int n = G * C;
-    hipLaunchKernelGGL(hgrad::colsum_kernel, dim3((n + hgrad::THREADS - 1) / hgrad::THREADS), dim3(hgrad::THREADS),
-                       0, st, part, G, R, C, out, beta);
+    const int blocks = G * ((C + hgrad::CS_C - 1) / hgrad::CS_C);
+    hipLaunchKernelGGL(hgrad::colsum_kernel, dim3(blocks), dim3(hgrad::THREADS), 0, st, part, G, R, C, out, beta);
     return hipGetLastError();
 }
 

@@ -31,7 +31,8 @@ struct Work {   // carve of the caller's work buffer (dadmm_hyper_train_work_byt
     float* dx[2];   // [rows][max width] ping-pong
     float* dv;      // [B][max decoder width]
     float* part;    // max(3 B N, rownorm partials)
-    float* wscr;    // wgrad split partials / linear_ln split-K partials
+    float* wscr;    // dadmm_hyper_wgrad split partials
+    float* lscr;    // dadmm_hyper_linear_ln_train split-K partials
 };
 
 int max_width(const dadmm_hyper_net* net) {
@@ -52,8 +53,8 @@ size_t layout(const dadmm_hyper_net* net, int B, Work* w, char* base) {
         const size_t r = dadmm_hyper_rownorm_bwd_part_bytes(B, net->dec_width[j]) / 4;
         part = part > r ? part : r;
     }
-    // scratch: the largest split partials of any weight gradient or decoder linear
-    size_t scr = 0;
+    // scratch: the largest split partials of any weight gradient; of any decoder linear
+    size_t scr = 0, lscr = 0;
     int kin = 2 * net->n;
     for (int i = 0; i < 5; ++i) {
         const size_t s = dadmm_hyper_wgrad_scratch_bytes(rows, net->width[i], kin);
@@ -65,18 +66,18 @@ size_t layout(const dadmm_hyper_net* net, int B, Work* w, char* base) {
         size_t s = dadmm_hyper_wgrad_scratch_bytes(B, net->dec_width[j], din);
         scr = scr > s ? scr : s;
         s = dadmm_hyper_linear_ln_scratch_bytes(B, din, net->dec_width[j]);
-        scr = scr > s ? scr : s;
+        lscr = lscr > s ? lscr : s;
         din = net->dec_width[j];
     }
     {
         const size_t s = dadmm_hyper_wgrad_scratch_bytes(B, 4 * net->H, din);
         scr = scr > s ? scr : s;
     }
-    const size_t sizes[6] = {up16(4 * (size_t)B * 4 * net->H), up16(4 * (size_t)rows * mw),
-                             up16(4 * (size_t)rows * mw), up16(4 * (size_t)B * md), up16(4 * part), up16(scr + 16)};
+    const size_t sizes[7] = {up16(scr + 16), up16(4 * (size_t)B * 4 * net->H), up16(4 * (size_t)rows * mw),
+                             up16(4 * (size_t)rows * mw), up16(4 * (size_t)B * md), up16(4 * part), up16(lscr + 16)};
     size_t off = 0;
-    float** slots[6] = {&w->dz, &w->dx[0], &w->dx[1], &w->dv, &w->part, &w->wscr};
-    for (int i = 0; i < 6; ++i) {
+    float** slots[7] = {&w->wscr, &w->dz, &w->dx[0], &w->dx[1], &w->dv, &w->part, &w->lscr};
+    for (int i = 0; i < 7; ++i) {
         if (base) *slots[i] = (float*)(base + off);
         off += sizes[i];
     }
@@ -149,7 +150,7 @@ int dadmm_hyper_train_forward(const dadmm_hyper_net* net, int32_t B, const float
         const int N = net->dec_width[j];
         TRY(dadmm_hyper_linear_ln_train(B, width, N, x, width, net->dec_w[j], net->dec_b[j], net->ln_w[j],
                                         net->ln_b[j], net->ln_eps[j], 1, net->dec_slope[j], net->dec_drop[j],
-                                        seed, 4 + j, sv->dec_y[j], sv->dec_xd[j], w.wscr, stream));
+                                        seed, 4 + j, sv->dec_y[j], sv->dec_xd[j], w.lscr, stream));
         x = sv->dec_y[j];
         width = N;
     }

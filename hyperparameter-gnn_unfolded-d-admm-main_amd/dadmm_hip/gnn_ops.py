@@ -1,9 +1,10 @@
 """Per-iteration HIP path of the GNN-hypernetwork model (C ABI: the dadmm_gnn_* entry points of
 include/dadmm.h) and its autograd plumbing.
 
-The hypernetwork between iterations is torch (its linears run on hipBLASLt MFMA GEMMs); every
-D-ADMM operation — A^T A y, A^T b, the gradient assembly and clamps, the primal / consensus / dual
-updates and the reference's batch-global guards — runs in libdadmm.so.
+Every D-ADMM operation — A^T A y, A^T b, the gradient assembly and clamps, the primal / consensus /
+dual updates and the reference's batch-global guards — runs in libdadmm.so; so does the
+hypernetwork between iterations (dadmm_hip.hyper_ops). GnnTrainFn runs a whole training-mode
+forward (K iterations) as one autograd node.
 """
 from __future__ import annotations
 
@@ -145,3 +146,75 @@ class StepFn(torch.autograd.Function):
         y_k, U, D, AtAy, hyp_k = ctx.saved_tensors
         gy, gU, gd, gA, ghyp = ctx.run.step_backward(ctx.k, y_k, AtAy, hyp_k, U, D, gy1, gU1, gd1)
         return gy, gU, gd, gA, ghyp, None, None
+
+
+class GnnTrainFn(torch.autograd.Function):
+    """The K iterations of a training-mode forward of DLASSO_GNNHyp3_Progressive
+    (gnn_dlasso_models_progressive.py:227-243 with the hypernetwork of :165-196 in train mode) as
+    ONE autograd node: per iteration A^T A y_k (dadmm_gnn_gram), the hypernetwork
+    (dadmm_hyper_train_forward, one library call) and the D-ADMM step (dadmm_gnn_step); the
+    backward walks the iterations in reverse with dadmm_gnn_step_backward,
+    dadmm_hyper_train_backward (parameter gradients added in place into the pass's flat buffer,
+    hyper_ops._GradAccumulator) and A^T A for the gram's input gradient. Replaces K x (GramFn,
+    HyperTrainFn, StepFn) nodes and the engine's per-iteration gradient sums — the training step
+    is then bound by the GPU, not by the host.
+
+    Inputs: ``marker`` (a parameter that requires grad, or None: the node's outputs require grad
+    through it), the GnnRun (iterate table Y [K, B, P, ns] layout), the model, its
+    hyper_ops.NativeHyperPlan, a_hat, per-sample flag and the K dropout seeds.
+    Outputs: Y [K, B, P, ns] and hyp_{K-1} [B, 4, H]. The BatchNorm running statistics of the K
+    iterations are updated in the forward, in call order."""
+
+    @staticmethod
+    def forward(ctx, marker, run, model, plan, a_hat, per_sample, seeds):
+        from . import hyper_ops
+        K, dev = run.K, run.dev
+        stream = _stream(dev)
+        arena = torch.empty(K * plan.per, device=dev)
+        svs = [plan.saved(arena, k) for k in range(K)]
+        U, D = run.U0, run.d0
+        Us, Ds, As = [U], [D], []
+        with torch.cuda.device(dev):
+            for k in range(K):
+                AtAy = run.gram(k)
+                plan.forward(AtAy, run.Atb, a_hat, per_sample, seeds[k], svs[k], stream)
+                _, U, D = run.step(k, AtAy, plan.hyp(arena, k), U, D)
+                As.append(AtAy)
+                Us.append(U)
+                Ds.append(D)
+        run.finish()
+        hyper_ops.queue_running_stats(model, plan.stats(arena, K), run.P, defer=False)
+        ctx.run, ctx.model, ctx.plan, ctx.a_hat, ctx.per_sample, ctx.seeds = run, model, plan, a_hat, per_sample, seeds
+        ctx.arena, ctx.svs, ctx.As, ctx.Us, ctx.Ds = arena, svs, As, Us, Ds
+        return run.Y, plan.hyp(arena, K - 1)
+
+    @staticmethod
+    def backward(ctx, gY, ghyp_last):
+        from . import hyper_ops
+        run, plan = ctx.run, ctx.plan
+        _check_guards(run)
+        K, dev = run.K, run.dev
+        stream = _stream(dev)
+        acc = hyper_ops._GradAccumulator.current(ctx.model, dev)
+        g = acc.grads_struct()
+        gY = gY.contiguous() if gY is not None else None
+        gy1 = gY[K - 1] if gY is not None else None
+        gU1 = gd1 = None
+        with torch.cuda.device(dev):
+            for k in range(K - 1, -1, -1):
+                hyp_k = plan.hyp(ctx.arena, k)
+                gy, gU, gd, gA, ghyp = run.step_backward(k, run.ys[k], ctx.As[k], hyp_k, ctx.Us[k], ctx.Ds[k],
+                                                         gy1, gU1, gd1)
+                if k == K - 1 and ghyp_last is not None:
+                    ghyp.add_(ghyp_last)
+                dA = plan.backward(ctx.As[k], run.Atb, ctx.a_hat, ctx.per_sample, ctx.seeds[k], ctx.svs[k], ghyp,
+                                   g, stream)
+                if k == 0:   # y_0, U_0, delta_0 are the random inits: no gradient
+                    break
+                gA.add_(dA)
+                gy.add_(run.gram(0, x=gA))
+                if gY is not None:
+                    gy.add_(gY[k - 1])
+                gy1, gU1, gd1 = gy, gU, gd
+        ctx.arena = ctx.svs = ctx.As = ctx.Us = ctx.Ds = None
+        return (None,) * 7

@@ -174,6 +174,8 @@ def _update_running_stats(bn, mean, var, P):
     """bn's running statistics after the reference's sequential per-sample calls (train mode),
     in closed form: r <- (1 - m) r + m s_t for t = 0 .. T-1 (unbiased variance). mean / var are
     [T, N]: the B samples of one call, or those of several calls stacked in call order."""
+    if mean.dim() == 3:   # [iterations, B, N] blocks of a whole forward: the calls in order
+        mean, var = mean.reshape(-1, mean.shape[2]), var.reshape(-1, var.shape[2])
     T = mean.shape[0]
     m = bn.momentum
     w = _rs_weights(T, m, mean.device)
@@ -196,8 +198,8 @@ def flush_running_stats(model):
         for i in range(len(pending[0][0])):
             bn = pending[0][0][i][0]
             P = pending[0][1]
-            mean = torch.cat([call[0][i][1] for call in pending])
-            var = torch.cat([call[0][i][2] for call in pending])
+            mean = torch.cat([call[0][i][1].reshape(-1, call[0][i][1].shape[-1]) for call in pending])
+            var = torch.cat([call[0][i][2].reshape(-1, call[0][i][2].shape[-1]) for call in pending])
             _update_running_stats(bn, mean, var, P)
 
 
@@ -214,6 +216,7 @@ class HyperTrainFn(torch.autograd.Function):
     def forward(ctx, AtAy, Atb, ahat, model, n, per_sample, seed, defer, *params):
         L = _lib.load()
         B, P, ns = AtAy.shape
+        ctx.n_params = len(params)
         ctx.native = n % 16 == 0 and B > 0
         if ctx.native:   # the whole call in one library entry point (csrc/dadmm_hyper_net.cpp)
             return _native_forward(ctx, L, AtAy, Atb, ahat, model, n, per_sample, seed, defer)
@@ -375,102 +378,164 @@ class HyperTrainFn(torch.autograd.Function):
                     acc.wgrad(rows, N, Kin, dZ, N, ctx.xs[i], Kin, Kin, None, 0, conv.lin.weight, None)
                     dx = acc.input_grad(rows, dZ, N, conv.lin.weight)
         ctx.saved = ctx.xs = ctx.dec_in = ctx.dec_xd = None
-        return (dAtAy, None, None, None, None, None, None, None) + (None,) * len(_hyper_params(model))
+        return (dAtAy, None, None, None, None, None, None, None) + (None,) * ctx.n_params
 
 
 # ---- one library call per iteration (dadmm_hyper_train_forward / _backward) -------------------
 
-def _native_net(model, P, n, ns, dev):
-    """The dadmm_hyper_net struct of ``model`` (parameter pointers, dimensions, constants), cached
-    on the model and rebuilt when a parameter's storage, a dropout p or a maximum changes."""
-    enc = model.encoder
-    convs = (enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5)
-    bns = (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)
-    params = _hyper_params(model)
-    key = (P, n, ns, str(dev), tuple(p.data_ptr() for p in params), float(enc.dropout.p),
-           tuple(float(model.decoder[4 * j + 1].p) for j in range(3)),
-           tuple(float(v) for v in (model.alpha_max, model.tau_max, model.rho_max, model.eta_max)))
-    hit = getattr(model, "_native_net", None)
-    if hit is not None and hit[0] == key:
-        return hit[1]
-    net = _lib.HyperNet()
-    net.P, net.n, net.ld = P, n, ns
-    for i, (conv, bn) in enumerate(zip(convs, bns)):
-        net.width[i] = conv.lin.out_features
-        net.conv_w[i], net.conv_b[i] = conv.lin.weight.data_ptr(), conv.bias.data_ptr()
-        net.bn_w[i], net.bn_b[i], net.bn_eps[i] = bn.weight.data_ptr(), bn.bias.data_ptr(), float(bn.eps)
-    net.norm_w, net.norm_b, net.norm_eps = enc.norm.weight.data_ptr(), enc.norm.bias.data_ptr(), float(enc.norm.eps)
-    for j in range(3):
-        lin, ln = model.decoder[4 * j], model.decoder[4 * j + 2]
-        net.dec_width[j] = lin.out_features
-        net.dec_w[j], net.dec_b[j] = lin.weight.data_ptr(), lin.bias.data_ptr()
-        net.ln_w[j], net.ln_b[j], net.ln_eps[j] = ln.weight.data_ptr(), ln.bias.data_ptr(), float(ln.eps)
-        net.dec_slope[j] = float(model.decoder[4 * j + 3].negative_slope)
-        net.dec_drop[j] = float(model.decoder[4 * j + 1].p)
-    net.H = model.fc.out_features // 4
-    net.fc_w, net.fc_b = model.fc.weight.data_ptr(), model.fc.bias.data_ptr()
-    net.drop_enc = float(enc.dropout.p)
-    for c, v in enumerate((model.alpha_max, model.tau_max, model.rho_max, model.eta_max)):
-        net.maxv[c] = float(v)
-    model._native_net = (key, net)
-    return net
+_N_SAVED = 29   # pointers in dadmm_hyper_saved: y, m, mean, var [5] each, e, dec_y [3], dec_xd [3], z, hyp
 
 
-def _native_work(model, L, net, B, dev):
-    """The shared work buffer (dadmm_hyper_train_work_bytes) for batch B, cached on the model."""
-    nbytes = L.dadmm_hyper_train_work_bytes(ctypes.byref(net), B)
-    if nbytes == 0:
-        raise ValueError("dadmm_hyper_train_work_bytes: hypernetwork dimensions not supported")
-    w = getattr(model, "_native_work", None)
-    if w is None or w.numel() * 4 < nbytes or w.device != dev:
-        w = torch.empty(nbytes // 4 + 4, device=dev)
-        model._native_work = w
-    return w
+def _modules(model):
+    """(convs, bns, decoder linears, decoder layernorms, decoder dropouts, decoder activations),
+    cached on the model (nn.Module attribute lookups dominate the per-iteration host cost)."""
+    mods = model.__dict__.get("_hyper_modules")
+    if mods is None:
+        enc = model.encoder
+        dec = model.decoder
+        mods = ((enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5),
+                (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5),
+                tuple(dec[4 * j] for j in range(3)), tuple(dec[4 * j + 2] for j in range(3)),
+                tuple(dec[4 * j + 1] for j in range(3)), tuple(dec[4 * j + 3] for j in range(3)))
+        model.__dict__["_hyper_modules"] = mods
+    return mods
+
+
+class NativeHyperPlan:
+    """The training hypernetwork of ``model`` for batches of B samples on one device, as the
+    dadmm_hyper_net struct (parameter pointers, dimensions, constants), the layout of one
+    iteration's saved activations (``per`` floats: the dadmm_hyper_saved slices, 16-byte aligned)
+    and the shared work buffer. ``NativeHyperPlan.get`` rebuilds it when a parameter's storage, a
+    dropout p or a maximum changes."""
+
+    def __init__(self, model, B, P, n, ns, dev, key):
+        self.L = L = _lib.load()
+        self.key = key
+        self.B, self.P, self.n, self.ns, self.dev = B, P, n, ns, dev
+        convs, bns, lins, lns, drops, acts = _modules(model)
+        enc = model.encoder
+        net = _lib.HyperNet()
+        net.P, net.n, net.ld = P, n, ns
+        for i, (conv, bn) in enumerate(zip(convs, bns)):
+            net.width[i] = conv.lin.out_features
+            net.conv_w[i], net.conv_b[i] = conv.lin.weight.data_ptr(), conv.bias.data_ptr()
+            net.bn_w[i], net.bn_b[i], net.bn_eps[i] = bn.weight.data_ptr(), bn.bias.data_ptr(), float(bn.eps)
+        net.norm_w, net.norm_b, net.norm_eps = enc.norm.weight.data_ptr(), enc.norm.bias.data_ptr(), float(enc.norm.eps)
+        for j in range(3):
+            net.dec_width[j] = lins[j].out_features
+            net.dec_w[j], net.dec_b[j] = lins[j].weight.data_ptr(), lins[j].bias.data_ptr()
+            net.ln_w[j], net.ln_b[j], net.ln_eps[j] = lns[j].weight.data_ptr(), lns[j].bias.data_ptr(), float(lns[j].eps)
+            net.dec_slope[j] = float(acts[j].negative_slope)
+            net.dec_drop[j] = float(drops[j].p)
+        net.H = model.fc.out_features // 4
+        net.fc_w, net.fc_b = model.fc.weight.data_ptr(), model.fc.bias.data_ptr()
+        net.drop_enc = float(enc.dropout.p)
+        for c, v in enumerate((model.alpha_max, model.tau_max, model.rho_max, model.eta_max)):
+            net.maxv[c] = float(v)
+        self.net = net
+        self.bns = bns
+        self.H = H = net.H
+        rows = B * P
+        W = [net.width[i] for i in range(5)]
+        DW = [net.dec_width[j] for j in range(3)]
+        self.W = W
+        sizes = ([rows * w for w in W] * 2 + [B * w for w in W] * 2 + [rows * W[4]] + [B * d for d in DW] * 2
+                 + [B * 4 * H, B * 4 * H])
+        assert len(sizes) == _N_SAVED
+        offs, o = [], 0
+        for sz in sizes:
+            offs.append(o)
+            o += (sz + 3) & ~3
+        self.offs = offs            # float offsets of the 29 slices in one iteration's block
+        self.per = o                # floats per iteration
+        self.offs_b = torch.tensor(offs, dtype=torch.int64) * 4
+        nbytes = L.dadmm_hyper_train_work_bytes(ctypes.byref(net), B)
+        if nbytes == 0:
+            raise ValueError("dadmm_hyper_train_work_bytes: hypernetwork dimensions not supported")
+        self.work = torch.empty(nbytes // 4 + 4, device=dev)
+        self.dAtAy = None
+
+    @staticmethod
+    def get(model, B, P, n, ns, dev):
+        convs, bns, lins, lns, drops, _ = _modules(model)
+        params = param_list(model)
+        key = (B, P, n, ns, dev, tuple(p.data_ptr() for p in params), float(model.encoder.dropout.p),
+               tuple(float(d.p) for d in drops),
+               (float(model.alpha_max), float(model.tau_max), float(model.rho_max), float(model.eta_max)))
+        plans = model.__dict__.setdefault("_native_plans", {})
+        plan = plans.get((B, dev))
+        if plan is None or plan.key != key:
+            if len(plans) > 8:
+                plans.clear()
+            plan = NativeHyperPlan(model, B, P, n, ns, dev, key)
+            plans[(B, dev)] = plan
+        return plan
+
+    def saved(self, arena, k=0):
+        """dadmm_hyper_saved of iteration block k of ``arena`` (blocks of ``per`` floats)."""
+        ptrs = self.offs_b + (arena.data_ptr() + 4 * k * self.per)
+        return _lib.HyperSaved.from_buffer_copy(ptrs.numpy().tobytes())
+
+    def hyp(self, arena, k=0):
+        o = k * self.per + self.offs[28]
+        return arena[o:o + self.B * 4 * self.H].view(self.B, 4, self.H)
+
+    def stats(self, arena, iters):
+        """[(bn, mean [iters, B, N], var [iters, B, N])] of the GCN blocks over ``iters`` blocks."""
+        blocks = arena[:iters * self.per].view(iters, self.per)
+        out = []
+        for i, bn in enumerate(self.bns):
+            n = self.B * self.W[i]
+            mean = blocks[:, self.offs[10 + i]:self.offs[10 + i] + n].view(iters, self.B, self.W[i])
+            var = blocks[:, self.offs[15 + i]:self.offs[15 + i] + n].view(iters, self.B, self.W[i])
+            out.append((bn, mean, var))
+        return out
+
+    def forward(self, AtAy, Atb, ahat, per_sample, seed, sv, stream):
+        _lib.check("dadmm_hyper_train_forward", self.L.dadmm_hyper_train_forward(
+            ctypes.byref(self.net), self.B, _ptr(AtAy), _ptr(Atb), _ptr(ahat), int(per_sample), seed,
+            ctypes.byref(sv), _ptr(self.work), stream))
+
+    def backward(self, AtAy, Atb, ahat, per_sample, seed, sv, dhyp, g, stream):
+        """d AtAy (a buffer of the plan, overwritten by the next call) from d hyp; the parameter
+        gradients are added into ``g``'s accumulators."""
+        if self.dAtAy is None:   # columns n .. ns stay zero: the kernels write the first n
+            self.dAtAy = torch.zeros((self.B, self.P, self.ns), device=self.dev)
+        _lib.check("dadmm_hyper_train_backward", self.L.dadmm_hyper_train_backward(
+            ctypes.byref(self.net), self.B, _ptr(AtAy), _ptr(Atb), _ptr(ahat), int(per_sample), seed,
+            ctypes.byref(sv), _ptr(dhyp), ctypes.byref(g), _ptr(self.dAtAy), _ptr(self.work), stream))
+        return self.dAtAy
 
 
 def _native_forward(ctx, L, AtAy, Atb, ahat, model, n, per_sample, seed, defer):
     B, P, ns = AtAy.shape
     dev = AtAy.device
-    net = _native_net(model, P, n, ns, dev)
-    rows = B * P
-    W = list(net.width)
-    DW = list(net.dec_width)
-    H = net.H
-    # one arena for the call's saved activations (16-byte aligned slices)
-    sizes = ([rows * w for w in W] + [rows * w for w in W] + [B * w for w in W] + [B * w for w in W]
-             + [rows * W[4]] + [B * d for d in DW] + [B * d for d in DW] + [B * 4 * H, B * 4 * H])
-    offs, o = [], 0
-    for sz in sizes:
-        offs.append(o)
-        o += (sz + 3) & ~3
-    arena = torch.empty(o, device=dev)
-    base = arena.data_ptr()
-    sv = _lib.HyperSaved()
-    it = iter(range(len(sizes)))
-    for field in ("y", "m", "mean", "var"):
-        arr = getattr(sv, field)
-        for i in range(5):
-            arr[i] = base + 4 * offs[next(it)]
-    sv.e = base + 4 * offs[next(it)]
-    for j in range(3):
-        sv.dec_y[j] = base + 4 * offs[next(it)]
-    for j in range(3):
-        sv.dec_xd[j] = base + 4 * offs[next(it)]
-    sv.z = base + 4 * offs[next(it)]
-    ih = next(it)
-    sv.hyp = base + 4 * offs[ih]
-    work = _native_work(model, L, net, B, dev)
+    plan = NativeHyperPlan.get(model, B, P, n, ns, dev)
+    arena = torch.empty(plan.per, device=dev)
+    sv = plan.saved(arena)
     with torch.cuda.device(dev):
-        _lib.check("dadmm_hyper_train_forward", L.dadmm_hyper_train_forward(
-            ctypes.byref(net), B, _ptr(AtAy), _ptr(Atb), _ptr(ahat), int(per_sample), seed,
-            ctypes.byref(sv), _ptr(work), _stream(dev)))
-    # the batch statistics of every GCN block, for the running-statistics updates
-    enc = model.encoder
-    stats = []
-    for i, bn in enumerate((enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)):
-        mean = arena[offs[10 + i]:offs[10 + i] + B * W[i]].view(B, W[i])
-        var = arena[offs[15 + i]:offs[15 + i] + B * W[i]].view(B, W[i])
-        stats.append((bn, mean, var))
+        plan.forward(AtAy, Atb, ahat, per_sample, seed, sv, _stream(dev))
+    queue_running_stats(model, plan.stats(arena, 1), P, defer)
+    ctx.model, ctx.n, ctx.per_sample, ctx.seed = model, n, per_sample, seed
+    ctx.arena, ctx.sv, ctx.plan = arena, sv, plan
+    ctx.AtAy, ctx.Atb, ctx.ahat = AtAy, Atb, ahat
+    return plan.hyp(arena)
+
+
+def _native_backward(ctx, L, dhyp):
+    AtAy = ctx.AtAy
+    dev = AtAy.device
+    acc = _GradAccumulator.current(ctx.model, dev)
+    with torch.cuda.device(dev):
+        d = ctx.plan.backward(AtAy, ctx.Atb, ctx.ahat, ctx.per_sample, ctx.seed, ctx.sv, dhyp.contiguous(),
+                              acc.grads_struct(), _stream(dev))
+    ctx.arena = ctx.sv = None
+    return (d.clone(), None, None, None, None, None, None, None) + (None,) * ctx.n_params
+
+
+def queue_running_stats(model, stats, P, defer):
+    """The BatchNorm running-statistics updates of training-mode calls: applied now, or queued on
+    ``model`` for flush_running_stats (stats: [(bn, mean [T, B, N] or [B, N], var)])."""
     if defer:
         if not hasattr(model, "_bn_pending"):
             model._bn_pending = []
@@ -479,29 +544,6 @@ def _native_forward(ctx, L, AtAy, Atb, ahat, model, n, per_sample, seed, defer):
         with torch.no_grad():
             for bn, mean, var in stats:
                 _update_running_stats(bn, mean, var, P)
-    ctx.model, ctx.n, ctx.per_sample, ctx.seed = model, n, per_sample, seed
-    ctx.arena, ctx.sv, ctx.net = arena, sv, net
-    ctx.AtAy, ctx.Atb, ctx.ahat = AtAy, Atb, ahat
-    return arena[offs[ih]:offs[ih] + B * 4 * H].view(B, 4, H)
-
-
-def _native_backward(ctx, L, dhyp):
-    model, n = ctx.model, ctx.n
-    AtAy, Atb = ctx.AtAy, ctx.Atb
-    B, P, ns = AtAy.shape
-    dev = AtAy.device
-    acc = _GradAccumulator.current(model, dev)
-    g = acc.grads_struct()
-    net = ctx.net
-    work = _native_work(model, L, net, B, dev)
-    dAtAy = torch.zeros_like(AtAy) if ns != n else torch.empty_like(AtAy)
-    with torch.cuda.device(dev):
-        _lib.check("dadmm_hyper_train_backward", L.dadmm_hyper_train_backward(
-            ctypes.byref(net), B, _ptr(AtAy), _ptr(Atb), _ptr(ctx.ahat), int(ctx.per_sample), ctx.seed,
-            ctypes.byref(ctx.sv), _ptr(dhyp.contiguous()), ctypes.byref(g), _ptr(dAtAy), _ptr(work),
-            _stream(dev)))
-    ctx.arena = ctx.sv = None
-    return (dAtAy, None, None, None, None, None, None, None) + (None,) * len(_hyper_params(model))
 
 
 class _GradAccumulator:
@@ -621,11 +663,22 @@ class _GradAccumulator:
             self.model._grad_acc = None
         with torch.no_grad():
             for p in self.params:
+                if not p.requires_grad:
+                    continue
                 g = self.view(p)
                 if p.grad is None:
                     p.grad = g
                 else:
                     p.grad.add_(g)
+
+
+def param_list(model):
+    """_hyper_params(model), cached on the model (the Parameter objects outlive .to() / optimiser
+    steps, which replace or update their storage in place)."""
+    params = model.__dict__.get("_hyper_param_list")
+    if params is None:
+        params = model.__dict__["_hyper_param_list"] = _hyper_params(model)
+    return params
 
 
 def draw_dropout_seed() -> int:
@@ -640,4 +693,4 @@ def hypernetwork_train(model, AtAy, Atb, n, ahat, per_sample, seed=None, defer=F
     (the model's forward flushes once after its K iterations)."""
     if seed is None:
         seed = draw_dropout_seed()
-    return HyperTrainFn.apply(AtAy, Atb, ahat, model, n, per_sample, seed, defer, *_hyper_params(model))
+    return HyperTrainFn.apply(AtAy, Atb, ahat, model, n, per_sample, seed, defer, *param_list(model))

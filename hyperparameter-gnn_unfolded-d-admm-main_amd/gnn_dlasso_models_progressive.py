@@ -37,7 +37,7 @@ import torch.nn.functional as F
 from dadmm_hip import _lib
 from dadmm_hip import hyper_ops
 from dadmm_hip.autograd import tag_status
-from dadmm_hip.gnn_ops import GnnRun, GramFn, StepFn
+from dadmm_hip.gnn_ops import GnnRun, GnnTrainFn, GramFn, StepFn
 from dadmm_hip.graph import ingest, n_graphs
 from dadmm_hip.ops import PreparedOperator, draw_inits
 
@@ -259,6 +259,8 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         if fused and self.use_hip_graph and self.on_hyp is None:
             # the plan owns its device state: no per-forward GnnRun (its Y, Atb, G) is built
             return self._forward_graphed(bb, graphs, a_hat.contiguous(), y0, U0, d0, K, H)
+        if train_hip and n % 16 == 0 and self.on_hyp is None:
+            return self._forward_train_native(bb, graphs, a_hat.contiguous(), y0, U0, d0, K, H, grad)
         run = GnnRun(self.operator(), bb, graphs, K, H, _lib.VARIANT_GNN, y0, U0, d0, grad)
         Atb = run.Atb[..., :n]
         y, U, D = run.ys[0], run.U0, run.d0
@@ -294,6 +296,19 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         Y = torch.stack(ys) if run.Y is None else run.Y
         Y = Y[..., :n].unsqueeze(-1)
         return tag_status(Y, self.last_status), (alpha_k, tau_k, rho_k, eta_k)
+
+    def _forward_train_native(self, bb, graphs, a_hat, y0, U0, d0, K, H, grad):
+        """The training forward as one GnnTrainFn node: K x (gram, hypernetwork, step), each
+        hypernetwork one library call (n a multiple of 16: cat(AtAy, Atb) read in place)."""
+        B, n = bb.shape[0], self.n
+        run = GnnRun(self.operator(), bb, graphs, K, H, _lib.VARIANT_GNN, y0, U0, d0, False)
+        plan = hyper_ops.NativeHyperPlan.get(self, B, self.P, n, run.op.n_store, bb.device)
+        marker = next((p for p in hyper_ops.param_list(self) if p.requires_grad), None) if grad else None
+        seeds = [hyper_ops.draw_dropout_seed() for _ in range(K)]
+        Y, hyp = GnnTrainFn.apply(marker, run, self, plan, a_hat, not graphs.shared, seeds)
+        self.last_status = run.status
+        Y = Y[..., :n].unsqueeze(-1)
+        return tag_status(Y, self.last_status), tuple(hyp[:, c].view(B, H, 1, 1) for c in range(4))
 
     def _forward_graphed(self, bb, graphs, a_hat, y0, U0, d0, K, H):
         """The inference forward as one replay of a captured HIP graph (_EvalGraphPlan); the

@@ -414,7 +414,8 @@ int dadmm_hyper_head_act(int32_t mode, int32_t B, int32_t H, const float* z, con
  * gnn_dlasso_models_progressive.py:9-72, :93-123), accumulated in place in a fixed order.
  * dadmm_hyper_wgrad: g [N][K] (+)= dZ^T X over R rows (f32 MFMA); X = cat of x1 (columns < K1,
  *   leading dimension ld1) and x2 (the other K - K1 columns, ld2); gbias [N] (+)= column sums of dZ
- *   (nullable); beta = 1 accumulates. scratch: dadmm_hyper_wgrad_scratch_bytes (0: none needed).
+ *   (nullable); beta = 1 accumulates. scratch: dadmm_hyper_wgrad_scratch_bytes (0: none needed;
+ *   16-byte aligned).
  * dadmm_hyper_colsum: out [G][C] (+)= sum_r part [G][R][C] (the per-block partials of
  *   dadmm_hyper_gcn_train_bwd / dadmm_hyper_rownorm_bwd), rows in order.
  * dadmm_hyper_transpose: out [cols][rows] = in [rows][cols] (the weights of the input-gradient
@@ -434,7 +435,8 @@ int dadmm_hyper_transpose(int32_t rows, int32_t cols, const float* in, float* ou
  * aligned); dadmm_hyper_train_backward runs its backward from d hyp, ACCUMULATES (+=) every
  * parameter gradient into `g` (contiguous groups as the partial sums come: [bn.weight | bn.bias |
  * conv.bias], [LayerNorm weight | bias]) and writes the first n columns of d AtAy (row stride
- * net->ld). `work`: dadmm_hyper_train_work_bytes (16-byte aligned), shared by both. The dropout
+ * net->ld). `work`: dadmm_hyper_train_work_bytes (16-byte aligned), shared by both and by one
+ * stream at a time. The dropout
  * masks of both come from `seed` (the same value for an iteration's forward and backward).
  * Requires P >= 2, n % 16 == 0 and widths that are multiples of 4 (else DADMM_EINVAL /
  * DADMM_EUNSUPPORTED: the caller runs the per-kernel entry points above). */

@@ -36,8 +36,16 @@ def step():
 
 step()
 torch.cuda.synchronize()
+if os.environ.get("CPROF"):   # host-side profile of the timed steps
+    import cProfile
+    import pstats
+    pr = cProfile.Profile()
+    pr.enable()
 t0 = time.perf_counter()
 for _ in range(steps):
     step()
 torch.cuda.synchronize()
+if os.environ.get("CPROF"):
+    pr.disable()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(35)
 print(f"B={B} K={K}: {1e3 * (time.perf_counter() - t0) / steps:.2f} ms per train step (graphs pre-ingested)")

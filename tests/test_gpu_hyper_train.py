@@ -229,13 +229,16 @@ def test_deferred_running_stats_match_per_call_updates(cuda):
         assert int(b1.num_batches_tracked) == int(b2.num_batches_tracked) == B * calls
 
 
-def test_model_train_step_uses_hip_hypernetwork(cuda):
+@pytest.mark.parametrize("path", ["whole-forward", "per-iteration"])
+def test_model_train_step_uses_hip_hypernetwork(cuda, path):
     """DLASSO_GNNHyp3_Progressive in train mode: forward + compute_loss + backward through the
-    HIP hypernetwork; with dropout off it equals the torch backend (loss and gradients)."""
+    HIP hypernetwork; with dropout off it equals the torch backend (loss and gradients). Default:
+    one GnnTrainFn node for the K iterations; with an on_hyp hook the per-iteration nodes
+    (GramFn, HyperTrainFn, StepFn) run instead."""
     import copy
 
     import gnn_dlasso_utils as U
-    from dadmm_hip import hyper_ops
+    from dadmm_hip import gnn_ops, hyper_ops
     P, n, hidden, B, K = 5, 64, 16, 16, 3
     model, A, b = _model(cuda, P, n, hidden, "diff", seed=7)
     for mod in [model.encoder.dropout] + [model.decoder[i] for i in (1, 5, 9)]:
@@ -248,15 +251,23 @@ def test_model_train_step_uses_hip_hypernetwork(cuda):
                   for _ in range(3))
     bt = torch.from_numpy(b[:B]).to(cuda)[..., None]
     label = torch.randn(B, n, 1, device=cuda)
+    if path == "per-iteration":
+        model.on_hyp = lambda *a: None
+    fn = gnn_ops.GnnTrainFn if path == "whole-forward" else hyper_ops.HyperTrainFn
     calls = []
-    orig = hyper_ops.HyperTrainFn.apply
-    hyper_ops.HyperTrainFn.apply = lambda *a: (calls.append(1), orig(*a))[1]
+    orig = fn.apply
+    fn.apply = lambda *a: (calls.append(1), orig(*a))[1]
     try:
         Y1, _ = model(bt, graphs, K, inits=inits)
     finally:
-        hyper_ops.HyperTrainFn.apply = orig
-    assert len(calls) == K
+        fn.apply = orig
+    assert len(calls) == (1 if path == "whole-forward" else K)
     Y2, _ = ref(bt, graphs, K, inits=inits)
+    for i in range(1, 6):   # the B K running-statistics updates of each BatchNorm, in call order
+        bn1, bn2 = getattr(model.encoder, f"bn{i}"), getattr(ref.encoder, f"bn{i}")
+        _close(bn1.running_mean, bn2.running_mean, rel=1e-4, name=f"bn{i}.running_mean")
+        _close(bn1.running_var, bn2.running_var, rel=1e-4, name=f"bn{i}.running_var")
+        assert int(bn1.num_batches_tracked) == int(bn2.num_batches_tracked)
     l1, f1 = U.compute_loss(Y1, label)
     l2, f2 = U.compute_loss(Y2, label)
     assert abs(float(l1) - float(l2)) <= 1e-4 * abs(float(l2))
