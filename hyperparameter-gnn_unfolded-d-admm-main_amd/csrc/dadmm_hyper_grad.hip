@@ -8,10 +8,10 @@
 //                   g_bias[N] += sum_r dZ[r][n] (the bias gradient) from the same dZ reads.
 //                   f32 MFMA v_mfma_f32_16x16x4_f32 with the R rows as the reduction (k) dimension:
 //                   lane (i, h) feeds dZ[r + h][n0 + i] and X[r + h][k0 + i]. One workgroup per
-//                   32 x 32 output tile (and R-split): its 4 waves take interleaved 4-row steps
-//                   (RING in flight each) and add their partial tiles through LDS in wave order.
-//                   Splits > 1 (short grids) write partial tiles that reduce_kernel adds into G in
-//                   split order.
+//                   32 x 32 output tile (and R-split): its WV waves (4, 8 or 16: more for fewer
+//                   tiles) take interleaved 4-row steps (RING in flight each) and add their
+//                   partial tiles through LDS in a fixed pairwise tree. Splits > 1 (only for very
+//                   long R) write partial tiles that reduce_kernel adds into G in split order.
 //   colsum_kernel : out[g][c] += sum_r part[g][r][c] — the per-block partial sums of the BatchNorm /
 //                   bias (dadmm_hyper_gcn_train_bwd) and LayerNorm (dadmm_hyper_rownorm_bwd) parameter
 //                   gradients: 16 columns x 16 row slices per workgroup, slices added in order.
@@ -28,8 +28,7 @@ namespace hgrad {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int THREADS = 256;
-constexpr int TN = 32, TK = 32;   // output tile (n x k) per workgroup; 4 waves split its rows
-constexpr int WAVES = THREADS / 64;
+constexpr int TN = 32, TK = 32;   // output tile (n x k) per workgroup; its waves split the rows
 constexpr int RING = 8;           // row steps (4 rows each) of operands in flight per wave
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
@@ -44,9 +43,9 @@ __device__ __forceinline__ int xcd_tile(int bid, int G) {
     return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
 }
 
-__global__ __launch_bounds__(THREADS) void wgrad_kernel(WgradArgs a) {
-    __shared__ float red[WAVES - 1][16][64];    // waves 1..3's partial tiles (16 floats per lane)
-    __shared__ float redb[WAVES - 1][2][16];    // and their bias column sums
+template <int WV>
+__global__ __launch_bounds__(64 * WV) void wgrad_kernel(WgradArgs a) {
+    __shared__ float red[WV / 2][17][64];   // the tree's upper-half partials (16 tile + 1 bias / lane)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = lane & 15, h = lane >> 4;
     const int gn = (a.N + TN - 1) / TN, gk = (a.K + TK - 1) / TK;
@@ -83,7 +82,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(WgradArgs a) {
     for (int x = 0; x < 2; ++x) acc[x][0] = acc[x][1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
     float bsum[2] = {0.0f, 0.0f};
 
-    // wave w: steps s_begin + w, + WAVES, ...
+    // wave w: steps s_begin + w, + WV, ...
     float ra[RING][2], rb[RING][2];
     auto load = [&](int u, int st) {
         const int r = 4 * st + h;
@@ -96,11 +95,11 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(WgradArgs a) {
     };
     const int first = s_begin + w;
 #pragma unroll
-    for (int u = 0; u < RING; ++u) load(u, first + WAVES * u);
-    for (int st = first; st < s_end; st += WAVES * RING) {
+    for (int u = 0; u < RING; ++u) load(u, first + WV * u);
+    for (int st = first; st < s_end; st += WV * RING) {
 #pragma unroll
         for (int u = 0; u < RING; ++u) {
-            if (st + WAVES * u < s_end) {
+            if (st + WV * u < s_end) {
 #pragma unroll
                 for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -110,7 +109,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(WgradArgs a) {
                     bsum[1] += ra[u][1];
                 }
             }
-            load(u, st + WAVES * (u + RING));
+            load(u, st + WV * (u + RING));
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -120,34 +119,37 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(WgradArgs a) {
         const float v1 = __shfl_down(bsum[b], 16), v2 = __shfl_down(bsum[b], 32), v3 = __shfl_down(bsum[b], 48);
         bsum[b] = ((bsum[b] + v1) + v2) + v3;
     }
-    // waves 1..3 hand their partials to wave 0, which adds them in wave order
-    if (w > 0) {
+    // fixed pairwise tree over the waves: at each level the upper half hands its partials to the
+    // lower half (wave w adds wave w + half's)
+    // (the wave's bias sums sit in lanes h = 0; lane (i, h) carries that of column block h & 1)
+    const float b0 = __shfl(bsum[0], i), b1 = __shfl(bsum[1], i);
+    float bcol = (h & 1) ? b1 : b0;
 #pragma unroll
-        for (int x = 0; x < 2; ++x)
+    for (int half = WV / 2; half >= 1; half /= 2) {
+        if (w >= half && w < 2 * half) {
 #pragma unroll
-            for (int y = 0; y < 2; ++y)
+            for (int x = 0; x < 2; ++x)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) red[w - 1][8 * x + 4 * y + q][lane] = acc[x][y][q];
-        if (do_bias && h == 0) {
-            redb[w - 1][0][i] = bsum[0];
-            redb[w - 1][1][i] = bsum[1];
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) red[w - half][8 * x + 4 * y + q][lane] = acc[x][y][q];
+            red[w - half][16][lane] = bcol;
         }
+        __syncthreads();
+        if (w < half) {
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[x][y][q] += red[w][8 * x + 4 * y + q][lane];
+            bcol += red[w][16][lane];
+        }
+        __syncthreads();
     }
-    __syncthreads();
     if (w > 0) return;
-#pragma unroll
-    for (int v = 0; v < WAVES - 1; ++v) {
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-            for (int y = 0; y < 2; ++y)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) acc[x][y][q] += red[v][8 * x + 4 * y + q][lane];
-        if (do_bias && h == 0) {
-            bsum[0] += redb[v][0][i];
-            bsum[1] += redb[v][1][i];
-        }
-    }
+    bsum[0] = __shfl(bcol, i);
+    bsum[1] = __shfl(bcol, i + 16);
     // acc[x][y]: lane (i, h) holds G rows n0 + 16 x + 4 h + q (q = 0..3), column k0 + 16 y + i
     float* out = a.splits > 1 ? a.scratch + (size_t)split * a.N * a.K : a.g;
     const bool accum = a.splits == 1 && a.beta != 0;
@@ -248,19 +250,29 @@ hipError_t launch_transpose(const float* in, int rows, int cols, float* out, hip
     return hipGetLastError();
 }
 
+namespace {
+int wgrad_waves(int tiles) { return tiles >= 256 ? 4 : tiles >= 128 ? 8 : 16; }
+}
+
 int wgrad_splits(int R, int N, int K) {
     const int tiles = ((N + hgrad::TN - 1) / hgrad::TN) * ((K + hgrad::TK - 1) / hgrad::TK);
     const int steps = (R + 3) / 4;
+    const int wv = wgrad_waves(tiles);
     int s = 1;
-    // split the rows while the grid is short of one workgroup per CU and every wave of a split
-    // keeps >= 8 row steps
-    while (tiles * s * 2 <= 256 && steps / (2 * s) >= 8 * hgrad::WAVES) s *= 2;
+    // split the rows only when every wave would walk more than 128 row steps and the grid is
+    // short of 4 workgroups per CU
+    while (tiles * s < 1024 && steps / (wv * s) > 128) s *= 2;
     return s;
 }
 
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st) {
     const int tiles = ((a.N + hgrad::TN - 1) / hgrad::TN) * ((a.K + hgrad::TK - 1) / hgrad::TK);
-    hipLaunchKernelGGL(hgrad::wgrad_kernel, dim3(tiles * a.splits), dim3(hgrad::THREADS), 0, st, a);
+    const dim3 grid(tiles * a.splits);
+    switch (wgrad_waves(tiles)) {
+        case 4: hipLaunchKernelGGL(hgrad::wgrad_kernel<4>, grid, dim3(256), 0, st, a); break;
+        case 8: hipLaunchKernelGGL(hgrad::wgrad_kernel<8>, grid, dim3(512), 0, st, a); break;
+        default: hipLaunchKernelGGL(hgrad::wgrad_kernel<16>, grid, dim3(1024), 0, st, a); break;
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || a.splits == 1) return e;
     const size_t cnt = (size_t)a.N * a.K;
