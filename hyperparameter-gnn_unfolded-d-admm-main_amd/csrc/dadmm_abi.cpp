@@ -356,7 +356,7 @@ int dadmm_gnn_begin(const dadmm_dims* d, const void* op, const float* b, const f
     int rc = gnn_common(d, &a);
     if (rc) return rc;
     if (!flags) return fail(DADMM_EINVAL, "flags is NULL");
-    if (d->B == 0) return hip_rc(hipMemsetAsync(flags, 0, dadmm_gnn_flag_bytes(d->K), (hipStream_t)stream), "memset");
+    if (d->B == 0) return hip_rc(dadmm::gnn_launch_zero(flags, GNN_FLAG_WORDS(d->K), (hipStream_t)stream), "zero launch");
     if (!op || !b || !y0 || !U0 || !Atb) return fail(DADMM_EINVAL, "a required pointer is NULL");
     if (!aligned16(op) || !aligned16(y0) || !aligned16(U0) || !aligned16(Atb))
         return fail(DADMM_EINVAL, "op, y0, U0 and Atb must be 16-byte aligned");
@@ -364,8 +364,8 @@ int dadmm_gnn_begin(const dadmm_dims* d, const void* op, const float* b, const f
     a.b = b;
     a.U = U0;
     a.flags = flags;
-    hipError_t e = hipMemsetAsync(flags, 0, dadmm_gnn_flag_bytes(d->K), (hipStream_t)stream);
-    if (e != hipSuccess) return hip_rc(e, "memset");
+    hipError_t e = dadmm::gnn_launch_zero(flags, GNN_FLAG_WORDS(d->K), (hipStream_t)stream);
+    if (e != hipSuccess) return hip_rc(e, "zero launch");
     e = dadmm::gnn_launch_check0(a, y0, (hipStream_t)stream);
     if (e != hipSuccess) return hip_rc(e, "check0 launch");
     return hip_rc(dadmm::gnn_launch_gram(a, 0, nullptr, Atb, 1, (hipStream_t)stream), "Atb launch");

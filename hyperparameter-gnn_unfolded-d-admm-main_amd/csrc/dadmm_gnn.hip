@@ -5,9 +5,14 @@
 // the K-step loop cannot be fused: each iteration is
 //   gram     AtAy_k = A^T (A y_k)            (:158-162; MFMA GEMM pair, f32 fma chains)
 //   [host]   hyp_k = GNN(cat(AtAy_k, Atb))   (torch / hipBLASLt; :165-196)
-//   grad     g_k = clamp(AtAy - Atb + sign(y) tau + U deg + delta rho, +-gclip)   (:205-213)
-//   update   y_{k+1} = clamp(y - alpha g); delta_{k+1} = clamp(2 L y_{k+1}); U_{k+1} = clamp(U +
+//   step     g_k = clamp(AtAy - Atb + sign(y) tau + U deg + delta rho, +-gclip)   (:205-213)
+//            y_{k+1} = clamp(y - alpha g); delta_{k+1} = clamp(2 L y_{k+1}); U_{k+1} = clamp(U +
 //            delta eta)                                                           (:221-232)
+//            as ONE pass over the state (update_kernel<true>: g is formed in registers, never
+//            stored); the reference zeroes the WHOLE batch's gradient when any g is NaN
+//            (:216-218), which no workgroup can know while it updates, so the pass is optimistic
+//            and a resolve launch (resolve_kernel) either commits its y_next / U guard flags
+//            (no NaN: the common case, one workgroup's work) or redoes the update with g = 0.
 // with the reference's batch-global NaN/Inf guards (:150-156, :216-218, :235-237) decided through
 // device flag words between launches (no host synchronisation), exactly as dadmm_stepwise.hip
 // does for the unfolded model. Y[k] stores y_{k+1}; a y_next guard that fired is resolved by
@@ -78,6 +83,13 @@ __device__ __forceinline__ const float* y_source(const GnnArgs& a, int k, bool& 
 // hyp_k of sample s, agent p, component c (alpha, tau, rho, eta): [B][4][H] (view(B, 4, P|1))
 __device__ __forceinline__ float hyp_at(const GnnArgs& a, int s, int c, int p) {
     return a.hyp[((size_t)s * 4 + c) * a.hyp_rows + (a.hyp_rows == 1 ? 0 : p)];
+}
+
+// ---- zero: the guard flag words (a kernel, not hipMemsetAsync: the inference forward is captured
+// into a HIP graph, whose memset nodes were measured to replay with a corrupted fill pattern from
+// the second launch on — every guard flag set, profiles/r03/gnn_graph_memset_r03.txt) ------------
+__global__ __launch_bounds__(THREADS) void zero_kernel(int32_t* p, int words) {
+    for (int i = blockIdx.x * THREADS + threadIdx.x; i < words; i += gridDim.x * THREADS) p[i] = 0;
 }
 
 // ---- check0: the k = 0 guards on y0 / U0 (:150-156) --------------------------------------------
@@ -216,54 +228,19 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
     }
 }
 
-// ---- grad: g = clamp(((AtAy - Atb) + sign(y) tau) + U deg + delta rho) (:205-213) --------------
-__global__ __launch_bounds__(THREADS) void grad_kernel(GnnArgs a, int k) {
-    const int P = a.P, n = a.n;
-    const size_t S4 = (size_t)a.B * P * n / 4;
-    bool yzero = false;
-    const float* ys = y_source(a, k, yzero);
-    const bool uzero = flag_ld(a.flags + GNN_F_UBAD(k)) != 0;
-    // the y_next guard of iteration k - 1 fired (:235-237): the reference keeps y_k = y_{k-1}
-    // and appends it, so Y[k-1] (= yptr[k], which holds the rejected y_next) is rewritten with it
-    float* const fix = (k > 0 && flag_ld(a.flags + GNN_F_YNB(k - 1)) != 0) ? a.yptr[k] : nullptr;
-    float gclip, vclip;
-    clips(a, k, gclip, vclip);
-    bool bad = false;
-    for (size_t i = (size_t)blockIdx.x * THREADS + threadIdx.x; i < S4; i += (size_t)gridDim.x * THREADS) {
-        const size_t e = 4 * i;
-        const int s = (int)(e / ((size_t)P * n)), p = (int)((e / n) % P);
-        const float ta = hyp_at(a, s, 1, p), rh = hyp_at(a, s, 2, p);
-        const float dg = a.deg[(a.graph_shared ? 0 : (size_t)s * P) + p];
-        const f32x4 aty = ((const f32x4*)a.AtAy)[i];
-        const f32x4 atb = ((const f32x4*)a.Atb)[i];
-        const f32x4 yv = yzero ? (f32x4){0, 0, 0, 0} : ((const f32x4*)ys)[i];
-        if (fix != nullptr) ((f32x4*)fix)[i] = yv;
-        const f32x4 uv = uzero ? (f32x4){0, 0, 0, 0} : ((const f32x4*)a.U)[i];
-        const f32x4 dv = ((const f32x4*)a.D)[i];
-        f32x4 gv;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float y = yv[r];
-            const float st = sign_times(y, ta);   // sign(y) * tau
-            float g = aty[r] - atb[r];
-            g = g + st;
-            g = g + uv[r] * dg;
-            g = g + dv[r] * rh;
-            g = clamp_t(g, -gclip, gclip);
-            bad |= g != g;                                     // after the clamp only NaN (:216)
-            gv[r] = g;
-        }
-        ((f32x4*)a.G)[i] = gv;
-    }
-    flag_or(a.flags + GNN_F_GBAD(k), bad);
-}
-
-// ---- update: primal update, consensus and dual update of (sample, 128 columns) (:221-232) ------
+// ---- step: gradient, primal update, consensus and dual update of (sample, 128 columns) ----------
 // One workgroup per (sample, UCB = 128 columns). A lane owns 4 columns of one agent row; a wave
 // instruction covers two agent rows (lanes 0-31 and 32-63), so every global access is a 16-byte
 // vector and a wave keeps UP_CH row pairs of loads in flight. y_{k+1} of all P agents is staged in
 // LDS ([P][UCB], 25.6 KB at P = 50) next to the sample's visit lists, and the consensus reads its
 // neighbours from there in the reference's visit order (one fp32 add chain per column from 0).
+// update_item<FUSED> on item (sample, column block). FUSED: the gradient g = clamp(((AtAy - Atb) + sign(y) tau) + U deg + delta rho) (:205-213) is
+//   formed from AtAy, Atb, y, U, delta in the same pass (its NaN sets GBAD(k)); the y_next / U
+//   guard flags go to the optimistic slots. Also rewrites Y[k-1] when the previous y_next guard
+//   fired (:235-237: the reference keeps y_k = y_{k-1} and appends it).
+// !FUSED (resolve, launched after the fused pass): no NaN gradient -> block 0 commits the
+//   optimistic flags, every block exits; else the update again with g = 0 (:216-218), writing the
+//   guard flags themselves.
 constexpr int UP_CH = 4;
 constexpr int UCB = 128;
 // LDS bytes for one sample's visit lists: at most 2 P entries per agent (each incident edge is
@@ -272,21 +249,26 @@ __host__ __device__ constexpr int update_visit_words(int P) { return (2 * P * P 
 __host__ __device__ constexpr size_t update_lds_bytes(int P) {
     return 4 * ((size_t)P * UCB + (size_t)(P + 1) + update_visit_words(P));
 }
-__global__ __launch_bounds__(THREADS) void update_kernel(GnnArgs a, int k, int items) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
+template <bool FUSED>
+__device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, float* lds) {
+    // row pairs in flight per wave: the fused pass streams 5 state tensors, so fewer pairs keep
+    // its registers at 4+ waves per SIMD
+    constexpr int UP_CH = FUSED ? 2 : gnn::UP_CH;
     const int P = a.P, n = a.n;
     const int ncb = (n + UCB - 1) / UCB;
-    const int s = blockIdx.x / ncb;
+    const int s = item / ncb;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int half = lane >> 5;
-    const int c = (blockIdx.x % ncb) * UCB + 4 * (lane & 31);
+    const int c = (item % ncb) * UCB + 4 * (lane & 31);
     const int cl = 4 * (lane & 31);                  // column within the block
     const bool cv = c < n;
     const size_t base = (size_t)s * P * n + (cv ? c : 0);
     bool yzero = false;
     const float* __restrict__ ys = y_source(a, k, yzero);
-    const bool gzero = flag_ld(a.flags + GNN_F_GBAD(k)) != 0;
     const bool uzero = flag_ld(a.flags + GNN_F_UBAD(k)) != 0;
+    // the y_next guard of iteration k - 1 fired: Y[k-1] (= yptr[k], which holds the rejected
+    // y_next) is rewritten with y_k
+    float* const fix = (FUSED && k > 0 && flag_ld(a.flags + GNN_F_YNB(k - 1)) != 0) ? a.yptr[k] : nullptr;
     float gclip, vclip;
     clips(a, k, gclip, vclip);
     float* yl = lds;                                  // [P][UCB] y_{k+1}
@@ -296,21 +278,54 @@ __global__ __launch_bounds__(THREADS) void update_kernel(GnnArgs a, int k, int i
     const int vb = a.vptr[g0], vlen = a.vptr[g0 + P] - vb;
     for (int i = threadIdx.x; i <= P; i += THREADS) vpl[i] = a.vptr[g0 + i] - vb;
     for (int i = threadIdx.x; i < vlen; i += THREADS) vl[i] = a.vq[vb + i];
-    const float* __restrict__ G = a.G;
     const float* __restrict__ U = a.U;
     float* __restrict__ Yk = a.yptr[k + 1];
     const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
     // row pairs: wave w handles pairs w, w + 4, ...; lane half selects the row of the pair
-    bool bad_y = false;
+    bool bad_y = false, bad_g = false;
     for (int q0 = w; 2 * q0 < P; q0 += WAVES * UP_CH) {
         f32x4 gv[UP_CH], yv[UP_CH];
+        if constexpr (FUSED) {
+            f32x4 tv[UP_CH], bv[UP_CH], uv[UP_CH], dv[UP_CH];
 #pragma unroll
-        for (int u = 0; u < UP_CH; ++u) {
-            const int p = 2 * (q0 + WAVES * u) + half;
-            gv[u] = yv[u] = z4;
-            if (p < P && cv) {
-                if (!gzero) gv[u] = *(const f32x4*)(G + base + (size_t)p * n);       // :216-218
-                if (!yzero) yv[u] = *(const f32x4*)(ys + base + (size_t)p * n);
+            for (int u = 0; u < UP_CH; ++u) {
+                const int p = 2 * (q0 + WAVES * u) + half;
+                tv[u] = bv[u] = uv[u] = dv[u] = yv[u] = z4;
+                if (p < P && cv) {
+                    const size_t off = base + (size_t)p * n;
+                    tv[u] = *(const f32x4*)(a.AtAy + off);
+                    bv[u] = *(const f32x4*)(a.Atb + off);
+                    if (!yzero) yv[u] = *(const f32x4*)(ys + off);
+                    if (!uzero) uv[u] = *(const f32x4*)(U + off);
+                    dv[u] = *(const f32x4*)(a.D + off);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UP_CH; ++u) {
+                const int p = 2 * (q0 + WAVES * u) + half;
+                gv[u] = z4;
+                if (p < P && cv) {
+                    const float ta = hyp_at(a, s, 1, p), rh = hyp_at(a, s, 2, p);
+                    const float dg = a.deg[(a.graph_shared ? 0 : (size_t)s * P) + p];
+                    if (fix != nullptr) *(f32x4*)(fix + base + (size_t)p * n) = yv[u];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float g = tv[u][r] - bv[u][r];
+                        g = g + sign_times(yv[u][r], ta);   // sign(y) * tau
+                        g = g + uv[u][r] * dg;
+                        g = g + dv[u][r] * rh;
+                        g = clamp_t(g, -gclip, gclip);
+                        bad_g |= g != g;                    // after the clamp only NaN (:216)
+                        gv[u][r] = g;
+                    }
+                }
+            }
+        } else {   // resolve: the batch's gradient is zero (:216-218)
+#pragma unroll
+            for (int u = 0; u < UP_CH; ++u) {
+                const int p = 2 * (q0 + WAVES * u) + half;
+                gv[u] = yv[u] = z4;
+                if (p < P && cv && !yzero) yv[u] = *(const f32x4*)(ys + base + (size_t)p * n);
             }
         }
 #pragma unroll
@@ -365,8 +380,37 @@ __global__ __launch_bounds__(THREADS) void update_kernel(GnnArgs a, int k, int i
             *(f32x4*)(a.D_next + off) = acc;
         }
     }
-    flag_or(a.flags + GNN_F_YNB(k), bad_y);
-    flag_or(a.flags + GNN_F_UBAD(k + 1), bad_u);
+    if (FUSED) {
+        flag_or(a.flags + GNN_F_GBAD(k), bad_g);
+        flag_or(a.flags + GNN_F_YNB_OPT(k), bad_y);
+        flag_or(a.flags + GNN_F_UNB_OPT(k), bad_u);
+    } else {
+        flag_or(a.flags + GNN_F_YNB(k), bad_y);
+        flag_or(a.flags + GNN_F_UBAD(k + 1), bad_u);
+    }
+}
+
+// the fused pass: one workgroup per item
+__global__ __launch_bounds__(THREADS) void step_kernel(GnnArgs a, int k) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    update_item<true>(a, k, blockIdx.x, lds);
+}
+
+// the resolve: a short grid (every workgroup reads one flag word); the g = 0 update, if needed,
+// strides over the items
+__global__ __launch_bounds__(THREADS) void resolve_kernel(GnnArgs a, int k, int items) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (!flag_ld(a.flags + GNN_F_GBAD(k))) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            a.flags[GNN_F_YNB(k)] = flag_ld(a.flags + GNN_F_YNB_OPT(k));
+            a.flags[GNN_F_UBAD(k + 1)] = flag_ld(a.flags + GNN_F_UNB_OPT(k));
+        }
+        return;
+    }
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+        update_item<false>(a, k, item, lds);
+        __syncthreads();   // the LDS tile is reused by the next item
+    }
 }
 
 // ---- finish: Y[K-1] = y_{K-1} when the last y_next failed its guard; status bits ----------------
@@ -523,6 +567,12 @@ static int grid_for(size_t work, int per_block, int cap) {
     return (int)(g < (size_t)cap ? g : cap);
 }
 
+hipError_t gnn_launch_zero(int32_t* p, int words, hipStream_t st) {
+    hipLaunchKernelGGL(gnn::zero_kernel, dim3(grid_for((size_t)words, gnn::THREADS, 64)), dim3(gnn::THREADS), 0, st,
+                       p, words);
+    return hipGetLastError();
+}
+
 hipError_t gnn_launch_check0(const GnnArgs& a, const float* y0, hipStream_t st) {
     const int g = grid_for((size_t)a.B * a.P * a.n / 4, gnn::THREADS, 2048);
     hipLaunchKernelGGL(gnn::check0_kernel, dim3(g), dim3(gnn::THREADS), 0, st, a, y0);
@@ -546,17 +596,19 @@ hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* o
 }
 
 hipError_t gnn_launch_step(const GnnArgs& a, int k, hipStream_t st) {
-    const int g = grid_for((size_t)a.B * a.P * a.n / 4, gnn::THREADS, 4096);
-    hipLaunchKernelGGL(gnn::grad_kernel, dim3(g), dim3(gnn::THREADS), 0, st, a, k);
     const int items = a.B * ((a.n + gnn::UCB - 1) / gnn::UCB);
     const size_t lds = gnn::update_lds_bytes(a.P);
-    auto kern = gnn::update_kernel;
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds);
-        if (e != hipSuccess) return e;
+        for (const void* f : {(const void*)gnn::step_kernel, (const void*)gnn::resolve_kernel}) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
     }
-    hipLaunchKernelGGL(kern, dim3(items), dim3(gnn::THREADS), lds, st, a, k, items);
+    hipLaunchKernelGGL(gnn::step_kernel, dim3(items), dim3(gnn::THREADS), lds, st, a, k);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int rg = items < 256 ? items : 256;
+    hipLaunchKernelGGL(gnn::resolve_kernel, dim3(rg), dim3(gnn::THREADS), lds, st, a, k, items);
     return hipGetLastError();
 }
 

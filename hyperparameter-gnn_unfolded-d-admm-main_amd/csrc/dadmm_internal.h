@@ -101,12 +101,15 @@ hipError_t launch_adjoint(const AdjArgs& a, float* dhyp, hipStream_t st);
 
 // ---- GNN-model per-iteration path (dadmm_gnn.hip) -----------------------------------------------
 // flag words (int32, zeroed by dadmm_gnn_begin): y0 guard, then U_k non-finite (k = 0..K),
-// gradient NaN and y_next non-finite (k = 0..K-1)
+// gradient NaN and y_next non-finite (k = 0..K-1), and the fused step's optimistic y_next /
+// U_{k+1} flags (committed by its resolve launch when no gradient was NaN)
 #define GNN_F_Y0 0
-#define GNN_F_UBAD(k) (1 + 3 * (k))
-#define GNN_F_GBAD(k) (2 + 3 * (k))
-#define GNN_F_YNB(k) (3 + 3 * (k))
-#define GNN_FLAG_WORDS(K) (3 * (K) + 4)
+#define GNN_F_UBAD(k) (1 + 5 * (k))
+#define GNN_F_GBAD(k) (2 + 5 * (k))
+#define GNN_F_YNB(k) (3 + 5 * (k))
+#define GNN_F_YNB_OPT(k) (4 + 5 * (k))
+#define GNN_F_UNB_OPT(k) (5 + 5 * (k))
+#define GNN_FLAG_WORDS(K) (5 * (K) + 4)
 
 struct GnnArgs {
     const float* A;         // prepared operator [P][m_pad][n_pad]
@@ -139,6 +142,7 @@ struct GnnGrads {
     float* gAtAy;           // dL/dAtAy_k
     float* ghyp;            // dL/dhyp_k [B][4][hyp_rows]
 };
+hipError_t gnn_launch_zero(int32_t* p, int words, hipStream_t st);
 hipError_t gnn_launch_check0(const GnnArgs& a, const float* y0, hipStream_t st);
 hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* out, int mode,
                            hipStream_t st);

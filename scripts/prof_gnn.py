@@ -32,12 +32,14 @@ def main():
     with torch.no_grad():
         g(bt, graphs)
         torch.cuda.synchronize()
+        first = int(g.last_status.item())
         t0 = time.perf_counter()
         for _ in range(reps):
             g(bt, graphs)
         torch.cuda.synchronize()
     print(f"B={B} P={P} n={n} m={m} K={K} backend={backend}: "
-          f"{1e3 * (time.perf_counter() - t0) / reps:.2f} ms per forward")
+          f"{1e3 * (time.perf_counter() - t0) / reps:.2f} ms per forward, "
+          f"guard status {first} / {int(g.last_status.item())}")
 
 
 if __name__ == "__main__":

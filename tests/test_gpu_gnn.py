@@ -191,6 +191,35 @@ def test_hip_graph_replay_matches_eager(cuda, P, m, n, B, K, mode, per_sample):
     assert not torch.equal(outs[True][0][0], outs[True][2][0])
 
 
+def test_hip_graph_back_to_back_replays(cuda):
+    """Replays enqueued back to back (no host sync between them), with allocations in between
+    (the forward's own RNG draws): every replay starts from zeroed guard flags (status 0) and
+    equals the launch-by-launch forward. Regression: a hipMemsetAsync captured into the graph
+    replayed with a corrupted fill pattern from the second launch on (all guards set)."""
+    from dadmm_hip.ops import draw_inits
+    P, m, n, B, K = 5, 32, 64, 24, 5
+    model, A, b, x, graphs, _ = _setup(cuda, P, m, n, B, K, "diff", True, seed=3)
+    model.eval()
+    sets = [tuple(torch.randn(B, P, n, device=cuda) * 1e-2 for _ in range(3)) for _ in range(6)]
+    bt = _t(b, cuda)[..., None]
+    with torch.no_grad():
+        model.use_hip_graph = False
+        want = [model(bt, graphs, inits=s)[0].clone() for s in sets]
+        model.use_hip_graph = True
+        got = []
+        for s in sets:
+            draw_inits((B, P, n), torch.device(cuda))     # allocation churn between replays
+            Y, _ = model(bt, graphs, inits=s)
+            got.append((Y, model.last_status))
+        model(bt, graphs)                                  # drawn inits
+        got_drawn = model.last_status
+    torch.cuda.synchronize()
+    assert [int(st.item()) for _, st in got] == [0] * len(sets)
+    assert int(got_drawn.item()) == 0
+    for (Y, _), Ye in zip(got, want):
+        assert torch.equal(Y, Ye)
+
+
 def test_features_are_the_reference_gram_and_atb(cuda):
     """AtAy_0 = AtA @ y0 and Atb = compute_Atx(b) (fp64 check, fp32 tolerance)."""
     P, m, n, B, K = 4, 24, 48, 10, 1
