@@ -120,7 +120,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int G) {
 // has no masks; a K tail that is not a multiple of 16 runs as one masked step.
 template <int WR, int EPI, bool SPLIT, bool DMA>
 __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
-    [[maybe_unused]] constexpr int D = 4;          // register ring depth (k-steps in flight)
+    [[maybe_unused]] constexpr int D = WR >= 5 ? 3 : 4;   // register ring depth (k-steps in flight; 2 waves/SIMD)
     constexpr int TM = 32 * WR;                    // rows per workgroup tile
     extern __shared__ __attribute__((aligned(16))) float zt[];   // GCN epilogue (dynamic)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -616,10 +616,16 @@ hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
 
 template <int EPI, bool SPLIT>
 hipError_t launch_wr(int wr, bool dma, int grid, const HyperArgs& a, hipStream_t st) {
+    constexpr bool GCN = EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN;
     switch (wr) {
         case 1: return launch_one<1, EPI, SPLIT, false>(grid, a, st);
         case 2: return dma ? launch_one<2, EPI, SPLIT, true>(grid, a, st) : launch_one<2, EPI, SPLIT, false>(grid, a, st);
         case 4: return dma ? launch_one<4, EPI, SPLIT, true>(grid, a, st) : launch_one<4, EPI, SPLIT, false>(grid, a, st);
+        case 5:   // 160-row tiles: whole samples with little padding (3 x 50 nodes, 32 x 5)
+            if constexpr (GCN)
+                return dma ? launch_one<5, EPI, SPLIT, true>(grid, a, st) : launch_one<5, EPI, SPLIT, false>(grid, a, st);
+            else
+                return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
 }
@@ -644,6 +650,29 @@ static int pick_tiles(HyperArgs& a, int epi) {
     const int unit = gcn ? a.P : 1;                             // rows per tiling unit
     const int units = gcn ? a.B : a.rows;
     a.gn = (a.N + hyper::TN - 1) / hyper::TN;
+    if (gcn) {
+        // whole samples per tile: the candidate that wastes the fewest padding rows among those
+        // whose grid still gives ~two workgroups per CU (P = 50: 160-row tiles hold 150 rows,
+        // 128-row tiles only 100)
+        int best = 0;
+        double best_fill = 0.0;
+        for (int cand : {5, 4, 2, 1}) {
+            const int su = 32 * cand / unit;
+            if (su < 1) continue;
+            const long gm = (units + su - 1) / su;
+            if (gm * a.gn < 480) continue;
+            const double fill = (double)(su * unit) / (32 * cand);
+            if (fill > best_fill + 1e-9) {
+                best_fill = fill;
+                best = cand;
+            }
+        }
+        if (best != 0) {
+            a.S_t = 32 * best / unit;
+            a.gm = (units + a.S_t - 1) / a.S_t;
+            return best;
+        }
+    }
     int wr = 0;
     for (int cand = 4; cand >= 1; cand >>= 1) {
         const int su = 32 * cand / unit;
