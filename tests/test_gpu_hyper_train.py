@@ -321,3 +321,80 @@ def test_wgrad_colsum_transpose_kernels(cuda, R, N, K, K1, beta):
     t = torch.empty(K, N, device=cuda)
     _lib.check("dadmm_hyper_transpose", L.dadmm_hyper_transpose(N, K, _ptr(G0), _ptr(t), _stream(cuda)))
     assert torch.equal(t, G0.t())
+
+
+def _train_pair(cuda, P, n, hidden, mode, shared, B=12, seed=11):
+    """(HIP model, torch-backend copy) with dropout off, graphs, inits, b and a label."""
+    import copy
+    model, A, b = _model(cuda, P, n, hidden, mode, seed=seed)
+    for mod in [model.encoder.dropout] + [model.decoder[i] for i in (1, 5, 9)]:
+        mod.p = 0.0
+    ref = copy.deepcopy(model)
+    ref.hyper_backend = "torch"
+    graphs = ([O.connected_er_graph(P, 0.5, seed=3)] * B if shared
+              else [O.connected_er_graph(P, 0.5, seed=40 + s) for s in range(B)])
+    rng = np.random.default_rng(seed)
+    inits = tuple(torch.from_numpy((1e-2 * rng.standard_normal((B, P, n))).astype(np.float32)).to(cuda)
+                  for _ in range(3))
+    bt = torch.from_numpy(b[:B]).to(cuda)[..., None]
+    label = torch.randn(B, n, 1, device=cuda, generator=torch.Generator(device=cuda).manual_seed(seed))
+    return model, ref, graphs, inits, bt, label
+
+
+@pytest.mark.parametrize("mode,shared", [("same", True), ("diff", True), ("same", False)])
+def test_whole_forward_node_modes(cuda, mode, shared):
+    """GnnTrainFn (one autograd node for the K iterations) in 'same' mode (H = 1) and with one
+    shared graph: loss and every parameter gradient equal the torch backend's; the returned
+    hyper-parameters of the last iteration carry their gradient too."""
+    import gnn_dlasso_utils as U
+    from dadmm_hip import gnn_ops
+    P, n, hidden, K = 5, 32, 8, 3
+    model, ref, graphs, inits, bt, label = _train_pair(cuda, P, n, hidden, mode, shared)
+    calls = []
+    orig = gnn_ops.GnnTrainFn.apply
+    gnn_ops.GnnTrainFn.apply = lambda *a: (calls.append(1), orig(*a))[1]
+    try:
+        Y1, h1 = model(bt, graphs, K, inits=inits)
+    finally:
+        gnn_ops.GnnTrainFn.apply = orig
+    assert calls == [1]
+    Y2, h2 = ref(bt, graphs, K, inits=inits)
+    _close(Y1, Y2, rel=1e-4, name="Y")
+    for a_, b_ in zip(h1, h2):
+        _close(a_, b_, rel=1e-4, name="hyp")
+    # loss through Y and through the last iteration's hyper-parameters
+    l1 = U.compute_loss(Y1, label)[1] + 0.1 * sum(h.sum() for h in h1)
+    l2 = U.compute_loss(Y2, label)[1] + 0.1 * sum(h.sum() for h in h2)
+    l1.backward()
+    l2.backward()
+    for (name, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
+        assert p1.grad is not None, name
+        _close(p1.grad, p2.grad, rel=5e-3, name=name)
+
+
+def test_whole_forward_node_accumulates_and_respects_frozen(cuda):
+    """Two backward passes add into .grad (as autograd does); a parameter with requires_grad
+    False keeps .grad None; zero_grad between steps resets."""
+    import gnn_dlasso_utils as U
+    P, n, hidden, K = 5, 32, 8, 2
+    model, ref, graphs, inits, bt, label = _train_pair(cuda, P, n, hidden, "diff", False)
+    for m_ in (model, ref):
+        m_.encoder.conv2.lin.weight.requires_grad_(False)
+    for _ in range(2):
+        for m_ in (model, ref):
+            Y, _ = m_(bt, graphs, K, inits=inits)
+            U.compute_loss(Y, label)[1].backward()
+    for (name, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
+        if not p2.requires_grad:
+            assert p1.grad is None and p2.grad is None, name
+            continue
+        _close(p1.grad, p2.grad, rel=5e-3, name=name)
+    model.zero_grad()
+    Y, _ = model(bt, graphs, K, inits=inits)
+    U.compute_loss(Y, label)[1].backward()
+    ref.zero_grad()
+    Y, _ = ref(bt, graphs, K, inits=inits)
+    U.compute_loss(Y, label)[1].backward()
+    for (name, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
+        if p2.requires_grad:
+            _close(p1.grad, p2.grad, rel=5e-3, name=name)
