@@ -50,6 +50,7 @@ __device__ __forceinline__ f32x4 bload4(rsrc_t r, uint32_t voff, uint32_t soff) 
 }
 __device__ __forceinline__ float tclamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 __device__ __forceinline__ bool inside(float x, float lo, float hi) { return x >= lo && x <= hi; }
+typedef const __attribute__((address_space(4))) float cfloat;
 // compiler-only barrier: bounds how far the scheduler hoists loads (register budget)
 __device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
 // a per-iteration opaque copy of a wave-uniform value: keeps the shared graph's neighbour tests
@@ -182,7 +183,9 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
         float al[P], ta[P], rh[P], et[P];
 #pragma unroll
         for (int p = 0; p < P; ++p) {
-            const float* hp = a.hyp + ((size_t)k * a.hyp_rows + (a.hyp_rows == 1 ? 0 : p)) * 4;
+            // through the scalar cache (constant address space: the table is read-only for the
+            // launch), so the per-iteration hyper-parameters sit in SGPRs, not VGPRs
+            const cfloat* hp = (const cfloat*)a.hyp + ((size_t)k * a.hyp_rows + (a.hyp_rows == 1 ? 0 : p)) * 4;
             al[p] = hp[0]; ta[p] = hp[1]; rh[p] = hp[2]; et[p] = hp[3];
         }
         float gclip, vclip;

@@ -43,8 +43,8 @@ class _UnfoldedFn(torch.autograd.Function):
         out = forward_raw(op, b, graphs, table.detach(), y0, U0, d0, variant=variant,
                           record=record)
         Y, _, status = out[:3]
-        if _WARN:
-            for msg in describe_status(check_status(status)):
+        if _WARN:   # the reference's warnings (bit 16 is internal: the exact recomputation ran)
+            for msg in describe_status(check_status(status) & ~_lib.STATUS_RECOMPUTE):
                 print(f"Warning: {msg}")
         ctx.mark_non_differentiable(status)
         if record:
@@ -53,7 +53,10 @@ class _UnfoldedFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gY, gstatus):
-        st = check_status(ctx.status)   # one host sync per backward
+        # one host sync per backward. Bit 16 (an asymmetric shared adjacency sent the batch
+        # through the exact recomputation, which records the trajectory itself) is no guard event:
+        # the adjoints follow any adjacency
+        st = check_status(ctx.status) & ~_lib.STATUS_RECOMPUTE
         if st:
             raise GuardAdjointError(
                 "backward through a forward in which the reference's NaN/Inf guards fired ("

@@ -106,6 +106,10 @@ def _check_guards(run: GnnRun):
     """Once per backward pass (one host sync): the adjoint assumes no guard fired."""
     if getattr(run, "_checked", False):
         return
+    if not getattr(run.graphs, "symmetric", True):
+        raise NotImplementedError(
+            "the GNN model's adjoint needs undirected graphs (it applies delta = 2 L y as its own "
+            "transpose); the forward follows any adjacency")
     st = int(run.status.item())
     run._checked = True
     if st:

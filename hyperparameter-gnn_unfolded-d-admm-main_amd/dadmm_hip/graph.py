@@ -96,9 +96,9 @@ def _visit_lists(adj, P: int):
 class GraphBatch:
     """Device-resident graph layouts for one forward call."""
 
-    __slots__ = ("nbr", "deg", "shared", "order", "vptr", "vq", "fused_ok")
+    __slots__ = ("nbr", "deg", "shared", "order", "vptr", "vq", "fused_ok", "symmetric")
 
-    def __init__(self, nbr, deg, shared, order, vptr, vq, fused_ok=True):
+    def __init__(self, nbr, deg, shared, order, vptr, vq, fused_ok=True, symmetric=True):
         self.nbr = nbr      # int64 (uint64 bit patterns) [P] if shared else [B, P]
         self.deg = deg      # float32 [P] if shared else [B, P]
         self.shared = shared
@@ -108,6 +108,18 @@ class GraphBatch:
         # False when the fused kernel cannot follow the adjacency order (non-ascending lists with
         # P > 8): such batches take the stepwise path, which follows any order
         self.fused_ok = fused_ok
+        # every graph undirected (p in N(q) <=> q in N(p)), as the reference's Erdos-Renyi graphs
+        # are. The adjoints use delta = 2 L y as its own transpose, which holds only then: they
+        # refuse a batch with a directed graph (the forward follows any adjacency)
+        self.symmetric = symmetric
+
+
+def _symmetric(masks) -> bool:
+    """Whether the uint64 neighbour masks [..., P] describe undirected graphs."""
+    m = np.asarray(masks, np.uint64)
+    P = m.shape[-1]
+    bits = (m[..., :, None] >> np.arange(P, dtype=np.uint64)) & np.uint64(1)   # [..., p, q]
+    return bool(np.array_equal(bits, np.swapaxes(bits, -1, -2)))
 
 
 def _to_device(arrays, device):
@@ -149,7 +161,7 @@ def _batch(infos, P: int, device) -> GraphBatch:
     vq = _vq_nonempty(np.concatenate(vqs) if vqs else np.zeros(0, np.uint8))
     arrays = [nbr.view(np.int64), deg, vptr, vq] + ([order.view(np.int32)] if ordered else [])
     t = _to_device(arrays, device)
-    return GraphBatch(t[0], t[1], False, t[4] if ordered else None, t[2], t[3], fused_ok)
+    return GraphBatch(t[0], t[1], False, t[4] if ordered else None, t[2], t[3], fused_ok, _symmetric(nbr))
 
 
 def _adjacency(g, P: int):
@@ -254,7 +266,7 @@ def _batch_native(graph_list, P: int, device):
     if mod is None:
         return None
     try:
-        nbr, deg, order, vptr, vq, ascending, _ = mod.batch(graph_list, P)
+        nbr, deg, order, vptr, vq, ascending, symmetric = mod.batch(graph_list, P)
     except TypeError:
         return None
     B = len(graph_list)
@@ -266,7 +278,8 @@ def _batch_native(graph_list, P: int, device):
     if ordered:
         arrays.append(np.frombuffer(order, np.int32).reshape(B, P))
     t_ = _to_device(arrays, device)
-    return GraphBatch(t_[0], t_[1], False, t_[4] if ordered else None, t_[2], t_[3], fused_ok)
+    return GraphBatch(t_[0], t_[1], False, t_[4] if ordered else None, t_[2], t_[3], fused_ok,
+                      bool(symmetric))
 
 
 def n_graphs(graph_list, batch_size: int) -> int:
@@ -324,7 +337,7 @@ def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
                 vptr = np.zeros(P + 1, np.int32)
                 np.cumsum(i.vcnt, out=vptr[1:])
                 t = _to_device([i.mask.view(np.int64), i.deg, vptr, _vq_nonempty(i.vq)], device)
-                hit = GraphBatch(t[0], t[1], True, None, t[2], t[3])
+                hit = GraphBatch(t[0], t[1], True, None, t[2], t[3], symmetric=_symmetric(i.mask))
                 if len(_SHARED_CACHE) > 256:
                     _SHARED_CACHE.clear()
                 _SHARED_CACHE[key] = hit

@@ -232,6 +232,10 @@ def backward_raw(op: PreparedOperator, graphs: GraphBatch, traj: Trajectory,
     _dev_check(gY)
     if path not in ("auto", "fused", "general"):
         raise ValueError(f"unknown path {path!r}")
+    if not getattr(graphs, "symmetric", True):
+        raise NotImplementedError(
+            "the adjoint needs undirected graphs (p in N(q) <=> q in N(p), as the reference's "
+            "Erdos-Renyi graphs are): it applies delta = 2 L y as its own transpose")
     K, B, P, ns = traj.Y.shape
     H = int(traj.hyp.shape[1])
     gY = _pad_n(gY.float(), ns).contiguous()

@@ -378,7 +378,7 @@ class _EvalGraphPlan:
         self.gb = GraphBatch(graphs.nbr.clone(), graphs.deg.clone(), graphs.shared,
                              graphs.order.clone() if graphs.order is not None else None,
                              graphs.vptr.clone(), torch.zeros(self.vq_cap, dtype=torch.uint8, device=dev),
-                             graphs.fused_ok)
+                             graphs.fused_ok, graphs.symmetric)
         self.ahat = a_hat.clone()
         self.run_ = GnnRun(op, self.b, self.gb, K, H, _lib.VARIANT_GNN, self.y0, self.U0, self.d0,
                            False, begin=False)

@@ -112,7 +112,7 @@ def _graphs(args, batch_seed, lo, hi, device):
     base = int(vptr[0])
     return GraphBatch(gb.nbr[lo:], gb.deg[lo:], False,
                       gb.order[lo:] if gb.order is not None else None,
-                      vptr - base, gb.vq[base:], gb.fused_ok)
+                      vptr - base, gb.vq[base:], gb.fused_ok, gb.symmetric)
 
 
 def _batches(N, bs, gen):

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """GNN model train steps (model.train(): dropout, per-sample BatchNorm statistics, autograd) as in
-bench.py's gnn_train_step extra, for rocprofv3 kernel traces: python scripts/prof_gnn_train.py [B K steps]"""
+bench.py's gnn_train_step extra, for rocprofv3 kernel traces:
+python scripts/prof_gnn_train.py [B K steps [P m n]]"""
 import argparse
 import os
 import sys
@@ -16,7 +17,7 @@ import oracle as O  # noqa: E402
 from dadmm_hip.graph import ingest  # noqa: E402
 
 B, K, steps = (int(v) for v in (sys.argv[1:4] if len(sys.argv) > 3 else (256, 25, 3)))
-P, m, n = 5, 64, 256
+P, m, n = (int(v) for v in (sys.argv[4:7] if len(sys.argv) > 6 else (5, 64, 256)))
 dev = torch.device("cuda:0")
 A, b, x = O.make_problem(P, m, n, B, seed=1234)
 args = argparse.Namespace(GHN_iter_num=K, GHyp_hidden=100, DADMM_mode="diff", alpha_max=0.1,
@@ -48,4 +49,5 @@ torch.cuda.synchronize()
 if os.environ.get("CPROF"):
     pr.disable()
     pstats.Stats(pr).sort_stats("tottime").print_stats(35)
-print(f"B={B} K={K}: {1e3 * (time.perf_counter() - t0) / steps:.2f} ms per train step (graphs pre-ingested)")
+print(f"B={B} K={K} P={P} m={m} n={n}: {1e3 * (time.perf_counter() - t0) / steps:.2f} ms per train step "
+      f"(graphs pre-ingested, backend {gnn.last_backend})")

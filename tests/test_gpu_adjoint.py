@@ -292,3 +292,36 @@ def test_training_steps_reduce_loss(cuda):
         losses.append(float(loss_final))
     assert np.isfinite(losses).all()
     assert min(losses[-3:]) < losses[0], losses
+
+
+def test_directed_graph_forward_exact_adjoint_refuses(cuda):
+    """A DIRECTED adjacency (successor lists, not symmetric; outside the reference's Erdos-Renyi
+    graphs): the recording forward follows it bit-exactly (a shared-graph launch flags it with
+    status bit 16 and the exact recomputation runs), and the adjoints, which apply delta = 2 L y
+    as its own transpose, refuse it instead of returning wrong gradients."""
+    import networkx as nx
+    from dadmm_hip import _lib
+    from dadmm_hip.autograd import dadmm_unfolded_apply
+    from dadmm_hip.ops import backward_raw
+    P, m, n, B, K = 5, 64, 256, 24, 8
+    A, b, _ = O.make_problem(P, m, n, B, seed=77)
+    g0 = nx.DiGraph()
+    g0.add_nodes_from(range(P))
+    g0.add_edges_from([(0, 1), (1, 0), (1, 2), (2, 3), (3, 2), (3, 4), (4, 0), (0, 3)])
+    y0, U0, d0 = _inits(B, P, n, seed=5)
+    rng = np.random.default_rng(3)
+    hyp = O.hyp_table((0.5 * rng.standard_normal((K, P, 4))).astype(np.float32), MAXP)
+    for graphs in ([g0] * B, [g0] + [O.er_graph(P, 0.5, seed=s) for s in range(B - 1)]):
+        op, g, Y, U, st, traj = _record(cuda, A, b, graphs, hyp, y0, U0, d0)
+        Yo, Uo, sto, Go, Uro = O.forward_f32_rec(A, b, graphs, hyp, y0, U0, d0)
+        assert sto == 0 and st in (0, _lib.STATUS_RECOMPUTE)
+        assert not g.symmetric
+        assert np.array_equal(Y.cpu().numpy(), Yo)
+        assert np.array_equal(traj.Grec[..., :n].cpu().numpy(), Go)
+        gY = _t(np.ones((K, B, P, n), np.float32), cuda)
+        with pytest.raises(NotImplementedError, match="undirected"):
+            backward_raw(op, g, traj, gY)
+        table = _t(hyp, cuda).requires_grad_(True)
+        Y2, _ = dadmm_unfolded_apply(op, _t(b, cuda), g, table, _t(y0, cuda), _t(U0, cuda), _t(d0, cuda))
+        with pytest.raises(NotImplementedError, match="undirected"):
+            Y2.sum().backward()

@@ -308,3 +308,22 @@ def test_vectorized_ingestion_rejects_asymmetric_graphs():
     assert Gm._batch_vectorized(graphs, P, "cpu") is None
     gb = Gm.ingest(graphs, P, 70, "cpu")                # falls back to the per-graph path
     assert gb.deg.numpy()[0].tolist() == [1, 1, 0, 0]
+
+
+def test_graph_batch_symmetric_flag():
+    """GraphBatch.symmetric: True for undirected graphs (the reference's), False as soon as one
+    graph of the batch is directed, on every ingestion path (shared, per-sample, many distinct)."""
+    import networkx as nx
+    from dadmm_hip.graph import _symmetric, ingest
+    P = 6
+    dg = nx.DiGraph()
+    dg.add_nodes_from(range(P))
+    dg.add_edges_from([(0, 1), (1, 2), (2, 1), (3, 4), (5, 0)])
+    ers = [O.connected_er_graph(P, 0.5, seed=s) for s in range(80)]
+    assert ingest([ers[0]] * 4, P, 4, "cpu").symmetric
+    assert ingest(ers[:4], P, 4, "cpu").symmetric
+    assert ingest(ers, P, 80, "cpu").symmetric                   # many distinct: native / numpy
+    assert not ingest([dg] * 4, P, 4, "cpu").symmetric
+    assert not ingest([dg] + ers[:3], P, 4, "cpu").symmetric
+    assert not ingest([dg] + ers[:79], P, 80, "cpu").symmetric
+    assert _symmetric(np.array([0b10, 0b01], np.uint64)) and not _symmetric(np.array([0b10, 0], np.uint64))
