@@ -362,10 +362,11 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
             const f32x4 yp = *(const f32x4*)(yl + p * UCB + cl);
             f32x4 acc = z4;
             const int v0 = vpl[p], v1 = vpl[p + 1];
+            // whole-vector ops: two v_pk_add_f32 / v_pk_add_f32(neg) per visit instead of eight
+            // scalar instructions, each lane of the pair rounded exactly as the scalar op
             for (int t = v0; t < v1; ++t) {
                 const f32x4 yq = *(const f32x4*)(yl + (int)vl[t] * UCB + cl);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[r] = acc[r] + (yp[r] - yq[r]);
+                acc = acc + (yp - yq);
             }
             const float et = hyp_at(a, s, 3, p);
             f32x4 un;
