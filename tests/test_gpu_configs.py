@@ -201,3 +201,73 @@ def test_headline_batch_4096_strided_slice_bit_exact(cuda):
     Y64, _, _ = O.forward_f64(A, b[sl], [graphs[0]] * len(sl), table, y0[sl], U0[sl], d0[sl])
     mse = float(((Ys[-1].astype(np.float64) - Y64[-1]) ** 2).mean())
     assert mse <= 1e-5, mse
+
+
+def test_configs2_full_batch_strided_slice_bit_exact(cuda):
+    """BASELINE configs[2] at its own size: B = 4096, P = 16, n = 512, m = 64, K = 25, per-sample
+    ER(0.3) graphs (the tiled path + the gated stepwise recomputation). One forward over the
+    whole batch; a strided slice of 16 samples bit-for-bit against oracle.forward_f32 (samples
+    are independent), status 0."""
+    import unfolded_DLASSO
+    P, m, n, B, K = 16, 64, 512, 4096, 25
+    A, b, x = O.make_problem(P, m, n, B, seed=2024)
+    graphs = [O.er_graph(P, 0.3, seed=50_000 + s) for s in range(B)]
+    rng = np.random.default_rng(5)
+    y0, U0, d0 = (1e-2 * rng.standard_normal((3, B, P, n))).astype(np.float32)
+    args = argparse.Namespace(GHN_iter_num=K, DADMM_mode="diff", alpha_max=0.1, tau_max=0.99,
+                              rho_max=0.99, eta_max=0.99, max_penalty_threshold=0.8,
+                              penalty_reduction_factor=0.95)
+    torch.manual_seed(6)
+    model = unfolded_DLASSO.DLASSO_unfolded(_t(A, cuda)[None], args).to(cuda).eval()
+    with torch.no_grad():
+        Y, _ = model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in (y0, U0, d0)))
+    assert int(model.last_status.item()) == 0
+    sl = np.arange(0, B, 256) + np.arange(16) % 5
+    Ys = Y[:, torch.from_numpy(sl).to(cuda), :, :, 0].cpu().numpy()
+    table = model.hyp_table(K).detach().cpu().numpy()
+    Yo, _, st = O.forward_f32(A, b[sl], [graphs[s] for s in sl], table, y0[sl], U0[sl], d0[sl])
+    assert st == 0
+    assert np.array_equal(Ys, Yo), f"max |diff| {np.abs(Ys - Yo).max():.3e}"
+
+
+def test_configs4_shard_full_batch_strided_slice(cuda):
+    """BASELINE configs[4]'s per-GPU shard at its own size: B = 1024, P = 50, n = 1024, m = 32,
+    K = 50, h = 100, per-sample connected ER(0.5) graphs. One eval forward over the whole shard
+    (every iteration's hyper-parameters recorded); for a strided slice of 4 samples the
+    hypernetwork's outputs at iterations 0, 24 and 49 against oracle/gnn_np.py (1e-4) and the
+    whole recurrence bit-for-bit against oracle.forward_f32_gram given the recorded table."""
+    import gnn_dlasso_models_progressive as G
+    P, m, n, B, K = 50, 32, 1024, 1024, 50
+    A, b, x = O.make_problem(P, m, n, B, seed=31)
+    torch.manual_seed(8)
+    model = G.DLASSO_GNNHyp3_Progressive(_t(A, cuda)[None], _gnn_args(K)).to(cuda)
+    _randomise_bn(model, 21)
+    model.eval()
+    graphs = [O.connected_er_graph(P, 0.5, seed=600 + s) for s in range(B)]
+    rng = np.random.default_rng(12)
+    inits = tuple((1e-2 * rng.standard_normal((3, B, P, n))).astype(np.float32))
+    sl = np.arange(0, B, 256) + np.arange(4) % 3
+    sl_t = torch.from_numpy(sl).to(cuda)
+    rec = []
+    model.on_hyp = lambda AtAy, Atb, out: rec.append(
+        (torch.cat([AtAy[sl_t, :, :n], Atb[sl_t, :, :n]], dim=2).cpu(),
+         torch.stack([o[sl_t, :, 0, 0] for o in out], dim=1).cpu()))
+    with torch.no_grad():
+        Y, _ = model(_t(b, cuda)[..., None], graphs, inits=tuple(_t(v, cuda) for v in inits))
+    assert int(model.last_status.item()) == 0
+    assert len(rec) == K
+    sd = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in model.state_dict().items()}
+    maxima = tuple(float(np.float32(v)) for v in MAXP)
+    gsl = [graphs[s] for s in sl]
+    for k in (0, 24, 49):
+        feats, got = rec[k]
+        want = gnn_np.hypernetwork(sd, feats.numpy().astype(np.float64), gsl, maxima, False)
+        for c in range(4):
+            w = want[c][..., 0, 0] if want[c].ndim == 4 else want[c]
+            np.testing.assert_allclose(got[:, c].numpy(), w.reshape(got[:, c].shape), rtol=1e-4,
+                                       atol=1e-4 * np.abs(w).max(), err_msg=f"iteration {k}, c {c}")
+    table = np.stack([r[1].numpy() for r in rec]).astype(np.float32)          # [K, 4 samples, 4, P]
+    Ys = Y[:, sl_t, :, :, 0].cpu().numpy()
+    Yo, _, st = O.forward_f32_gram(A, b[sl], gsl, table, *(v[sl] for v in inits), variant=1, hyp_mode=1)
+    assert st == 0
+    assert np.array_equal(Ys, Yo), f"max |diff| {np.abs(Ys - Yo).max():.3e}"
