@@ -173,6 +173,10 @@ struct TiledArgs {
 };
 size_t tiled_lds_bytes(int n_pad, int m_pad);
 hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream);
+// the whole forward in one launch, state streamed once per iteration (dadmm_stream.hip); U_k in
+// place in a.Ubuf[0]
+bool stream_applies(const TiledArgs& a);
+hipError_t launch_stream(const TiledArgs& a, hipStream_t stream);
 
 // ---- fused loss (dadmm_loss.hip) ----------------------------------------------------------------
 struct LossArgs {

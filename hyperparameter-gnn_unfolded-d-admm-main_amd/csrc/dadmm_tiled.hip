@@ -790,6 +790,10 @@ static hipError_t launch_colsplit(const TiledArgs& a, int CW, int vcap, hipStrea
 }
 
 hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream) {
+    // the single-launch streamed form (dadmm_stream.hip) wherever it applies; DADMM_TILED_STREAM=0
+    // selects the per-iteration launches below (A/B timing, tests of both forms)
+    const char* senv = getenv("DADMM_TILED_STREAM");
+    if ((senv == nullptr || atoi(senv) != 0) && stream_applies(a)) return launch_stream(a, stream);
     const size_t lds = tiled_lds_bytes(a.n_pad, a.m_pad);
     const char* env = getenv("DADMM_TILED_SPLIT");   // runtime override of the build default
     const bool split = env != nullptr ? atoi(env) != 0 : DADMM_TILED_SPLIT != 0;
