@@ -397,7 +397,8 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
                 mod(b3t, graphs3)
         ms_module = _event_ms(f3, 2, warm=1)
         out["c3_tiled"] = {"B": B3, "P": P3, "n": n3, "m": m3, "K": K3, "graph_prob": 0.3,
-                           "path": "tiled + gated stepwise", "ms_per_forward": ms,
+                           "path": "streamed single launch (dadmm_stream.hip) + gated stepwise",
+                           "ms_per_forward": ms,
                            "units_per_s": B3 * K3 / (ms * 1e-3),
                            "alg_bytes_per_unit": 4 * P3 * (4 * n3 + m3),
                            "alg_GBs": 4 * P3 * (4 * n3 + m3) * B3 * K3 / (ms * 1e-3) / 1e9,

@@ -50,9 +50,52 @@ constexpr int THREADS = 64 * NW;
 constexpr int CT = 2;            // 16-column MFMA tiles per step
 constexpr int CW = 16 * CT;      // columns per step
 constexpr int SLOTS = 3;         // y-block ring: the block of step bs + 2 is loaded during step bs
+// DADMM_ST_ABL (timing builds only, wrong results): 1 = no consensus walk, 2 = no operator loads,
+// 4 = no step-top wait / barrier, 8 = no Y / U stores, 16 = no y-block DMA
+#ifndef DADMM_ST_ABL
+#define DADMM_ST_ABL 0
+#endif
+// cache policy of the state streams (y-block copies, U, d0, Y and U stores); 2 = non-temporal (so
+// that they would not evict the operator from L2) measured no faster (6.04 vs 5.96 ms, configs[2])
+#ifndef DADMM_ST_AUX
+#define DADMM_ST_AUX 0
+#endif
+#define DADMM_STR_(x) #x
+#define DADMM_STR(x) DADMM_STR_(x)
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// A raw buffer descriptor as four SGPRs (for inline asm): base, stride 0, num_records = bytes,
+// the gfx950 default data format (the word __builtin_amdgcn_make_buffer_rsrc takes).
+__device__ __forceinline__ i32x4 rsrc_words(const void* base, uint32_t bytes) {
+    const uint64_t b = (uint64_t)base;
+    return (i32x4){(int)(uint32_t)b, (int)(uint32_t)(b >> 32) & 0xffff, (int)bytes, 0x00020000};
+}
+#if DADMM_ST_AUX == 2
+#define DADMM_ST_DMA_POL " nt"
+#else
+#define DADMM_ST_DMA_POL ""
+#endif
+// LDS-DMA of 16 bytes per lane into LDS at m0 + 16 lane, issued from inline asm: the compiler's
+// wait analysis then does not treat every later LDS read as a possible alias of the copy (it would
+// wait for the whole copy before the first such read, i.e. two steps too early); the kernel waits
+// for its copies itself (wait_prev_step). The compiler's own vmcnt waits stay correct: a copy it
+// does not count only makes them wait longer.
+__device__ __forceinline__ void dma16(uint32_t lds_addr, uint32_t voff, i32x4 rsrc) {
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" DADMM_ST_DMA_POL " lds"
+                 :
+                 : "s"(lds_addr), "v"(voff), "s"(rsrc)
+                 : "memory", "m0");
+}
+// a - b on both halves (v_pk_add_f32 with the second operand negated: a + (-b) == a - b exactly)
+__device__ __forceinline__ f32x2 pk_sub(f32x2 a, f32x2 b) {
+    f32x2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -126,9 +169,9 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
     const bool sok = s < B;
     const int sc = sok ? s : 0;
     const size_t S = (size_t)B * P * n;
+    const uint32_t s_bytes = (uint32_t)(S * 4);          // one iterate (< 2^31: the ABI checks)
     const int NB = NP / CW;
     const int kend = a.U_out != nullptr ? K : K - 1;     // phase K: the final dual update only
-    const int total = (kend + 2) * NB;                   // steps of phases -1 .. kend
     uint32_t status = 0;
 
     // ---- the tile's visit lists -> LDS rows (padded with the agent itself)
@@ -158,7 +201,6 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
         const int p = w + NW * ai;
         dg[ai] = (sok && p < P) ? a.deg[(a.graph_shared ? 0 : s * P) + p] : 0.0f;
     }
-    const uint32_t b_bytes = (uint32_t)((size_t)B * P * m * 4);
     auto col_ok = [&](int c0, int ct) { return sok && c0 + 16 * ct + 4 * bq < n; };
     auto elem = [&](int p, int c0, int ct) {   // [s][p][col] of this lane's 4 columns
         return ((size_t)sc * P + p) * n + c0 + 16 * ct + 4 * bq;
@@ -168,7 +210,7 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
     // offset past the range, which the hardware returns as zeros)
     auto dma = [&](int k, int blk, float* slot) {
         const float* src = k <= 0 ? a.y0 : a.Y + (size_t)(k - 1) * S;
-        const rsrc_t r = make_rsrc(src, k <= kend ? (uint32_t)(S * 4) : 0u);
+        const i32x4 r = rsrc_words(src, (k <= kend && !(DADMM_ST_ABL & 16)) ? s_bytes : 0u);
 #pragma unroll
         for (int ai = 0; ai < PW; ++ai) {
             const int q = w + NW * ai;
@@ -176,8 +218,7 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
             for (int ct = 0; ct < CT; ++ct) {
                 const uint32_t off = (q < P && col_ok(blk * CW, ct))
                                          ? (uint32_t)(elem(q, blk * CW, ct) * 4) : 0x80000000u;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(slot + 4 * ((q * CT + ct) * 64)),
-                                                         16, off, 0, 0, 0);
+                dma16((uint32_t)(uintptr_t)(lds_void*)(slot + 4 * ((q * CT + ct) * 64)), off, r);
             }
         }
     };
@@ -188,6 +229,11 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
     // (descriptors are built per use from a selected base and size: selecting between descriptor
     // values puts them on the stack)
     const uint32_t at_bytes = (uint32_t)((size_t)P * NP * 64 * 4);
+    // launch-constant descriptors; a phase or lane without the operand gets an out-of-range offset
+    // (zeros, no memory access) instead of a different descriptor
+    const rsrc_t dAt = make_rsrc(a.At, (DADMM_ST_ABL & 2) ? 0u : at_bytes);
+    const rsrc_t dA = make_rsrc(a.A, (DADMM_ST_ABL & 2) ? 0u : at_bytes);
+    const rsrc_t dd0 = make_rsrc(a.d0, s_bytes), db = make_rsrc(a.b, (uint32_t)((size_t)B * P * m * 4));
     const uint32_t vat = (uint32_t)((j * 64 + 4 * bq) * 4), vam = (uint32_t)((j * NP + 4 * bq) * 4);
     // the global operands of tile i = (agent i / CT, columns 16 (i % CT)) of step bs: fetch_a (A^T
     // rows, U_{k-1}, d0) is issued at the start of the previous tile, fetch_m (A rows, needed only at
@@ -196,29 +242,30 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
         const int ai = i / CT, ct = i % CT;
         const int p = w + NW * ai;
         const bool pin = p < P;
-        const rsrc_t ra = make_rsrc(a.At, (k >= 0 && k < K && pin) ? at_bytes : 0u);
         const int pc = pin ? p : 0;
+        const uint32_t vo = (k >= 0 && k < K && pin) ? vat : 0x80000000u;
+        const uint32_t sb = (uint32_t)((((size_t)pc * NP + c0 + 16 * ct) * 64) * 4);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-            r.at[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                ra, vat, (uint32_t)((((size_t)pc * NP + c0 + 16 * ct) * 64 + 16 * t) * 4), 0));
-        const uint32_t off = col_ok(c0, ct) ? (uint32_t)(elem(pc, c0, ct) * 4) : 0x80000000u;
-        const float* us = k <= 1 ? a.U0 : a.Ubuf[0];   // U_{k-1} (k = 0: U0 itself)
+            r.at[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dAt, vo + 64 * t, sb, 0));
+        const uint32_t off = (pin && col_ok(c0, ct)) ? (uint32_t)(elem(pc, c0, ct) * 4) : 0x80000000u;
+        // U_{k-1} (k = 0: U0 itself; k = 1: U_0 = U0)
         r.u = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-            make_rsrc(us, (k >= 0 && pin) ? (uint32_t)(S * 4) : 0u), off, 0, 0));
-        r.d = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-            make_rsrc(a.d0, (k == 0 && pin) ? (uint32_t)(S * 4) : 0u), off, 0, 0));
+            make_rsrc(k <= 1 ? a.U0 : a.Ubuf[0], s_bytes), k >= 0 ? off : 0x80000000u, 0, DADMM_ST_AUX));
+        r.d = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dd0, k == 0 ? off : 0x80000000u, 0,
+                                                                              DADMM_ST_AUX));
     };
     auto fetch_m = [&](int k, int c0, int i, Ring& r) {
         const int ai = i / CT, ct = i % CT;
         const int p = w + NW * ai;
         const bool pin = p < P;
-        const rsrc_t rm = make_rsrc(a.A, (k < K - 1 && pin) ? at_bytes : 0u);
         const int pc = pin ? p : 0;
+        const bool ok = k < K - 1 && pin;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
             r.am[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                rm, vam, (uint32_t)((((size_t)pc * 64 + 16 * t) * NP + c0 + 16 * ct) * 4), 0));
+                dA, ok ? vam + (uint32_t)(16 * t * NP * 4) : 0x80000000u,
+                (uint32_t)((((size_t)pc * 64) * NP + c0 + 16 * ct) * 4), 0));
     };
 
     f32x4 Rk[PW][4], Rn[PW][4];
@@ -244,17 +291,23 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
         const f32x4 yo = *(const f32x4*)(ys + 4 * ((p * CT + ct) * 64 + lane));
         // delta_k = compute_delta(y_k) (unfolded_DLASSO.py:127-140): acc + (y_p - y_q) over p's visit
         // row, four entries per LDS word (no walk in phases -1 and 0)
-        const int D = k >= 1 ? __builtin_amdgcn_readfirstlane(dmx[p]) : 0;   // 0 for p >= P
+        const int D = (k >= 1 && !(DADMM_ST_ABL & 1)) ? __builtin_amdgcn_readfirstlane(dmx[p]) : 0;   // 0 for p >= P
         const uint32_t* vrow = vt + (p * BT + j) * DP;
         const char* ybase = (const char*)(ys + 4 * (ct * 64 + lane));
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
         for (int t4 = 0; t4 < D; t4 += 4) {
             const uint4 qo = *(const uint4*)(vrow + t4);
             const uint32_t qa[4] = {qo.x, qo.y, qo.z, qo.w};
+            f32x4 yqs[4];   // the four neighbour reads in flight together
+#pragma unroll
+            for (int u = 0; u < 4; ++u) yqs[u] = *(const f32x4*)(ybase + qa[u]);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const f32x4 yq = *(const f32x4*)(ybase + qa[u]);
-                acc = acc + (yo + (-yq));   // == yo - yq exactly; folds into v_pk_add_f32's negation
+                const f32x4 yq = yqs[u];
+                const f32x2 d0 = pk_sub((f32x2){yo[0], yo[1]}, (f32x2){yq[0], yq[1]});
+                const f32x2 d1 = pk_sub((f32x2){yo[2], yo[3]}, (f32x2){yq[2], yq[3]});
+                acc = acc + (f32x4){d0[0], d0[1], d1[0], d1[1]};
             }
         }
         pre();   // the next tile's A^T rows, U, d0: after the walk (its LDS reads in flight need the VGPRs)
@@ -270,8 +323,6 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
             const float un = tclamp(r.u[r4] + dv[r4] * etp[ai], -vclip_prev, vclip_prev);
             uv[r4] = k >= 1 ? un : r.u[r4];
         }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, uv),
-                                               make_rsrc(k == K ? a.U_out : a.Ubuf[0], (uint32_t)(S * 4)), k >= 1 ? soff : 0x80000000u, 0, 0);
         bad_u0 |= k == 0 && okc && !finite4(uv);
         f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};   // GEMM2: A_p^T R_k, this tile's columns
 #pragma unroll
@@ -279,6 +330,11 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
 #pragma unroll
             for (int r4 = 0; r4 < 4; ++r4) gc = mfma4(r.at[t][r4], Rk[ai][t][r4], gc);
         mid();
+        // U_k after the next tile's A rows are issued: vector-memory operations complete in order,
+        // so a load issued after a store waits for it
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, uv),
+                                               make_rsrc(k == K ? a.U_out : a.Ubuf[0], (DADMM_ST_ABL & 8) ? 0u : s_bytes),
+                                               k >= 1 ? soff : 0x80000000u, 0, DADMM_ST_AUX);
         const bool upd = k >= 0 && k < K;
         f32x4 yn;
 #pragma unroll
@@ -294,8 +350,8 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
             yn[r4] = okc ? v : 0.0f;
         }
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, yn),
-                                               make_rsrc(a.Y + (size_t)(upd ? k : 0) * S, upd ? (uint32_t)(S * 4) : 0u),
-                                               soff, 0, 0);
+                                               make_rsrc(a.Y + (size_t)(upd ? k : 0) * S, (DADMM_ST_ABL & 8) ? 0u : s_bytes),
+                                               upd ? soff : 0x80000000u, 0, DADMM_ST_AUX);
         bad_y0 |= k == -1 && okc && !finite4(yo);   // the :55 guard on y_0
         // GEMM1: R_{k+1} += A_p[:, tile] y_{k+1}[tile] (phase -1: R_0 from y_0)
         const f32x4 gin = k == -1 ? yo : yn;
@@ -338,7 +394,7 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
                 for (int t = 0; t < 4; ++t) Rk[ai][t] = Rn[ai][t];
         }
         {   // (unconditional: Rn is dead in phases K - 1 and K)
-            const rsrc_t rbk = make_rsrc(a.b, k < K - 1 ? b_bytes : 0u);
+            const bool bk = k < K - 1;
 #pragma unroll
             for (int ai = 0; ai < PW; ++ai) {
                 const int p = w + NW * ai;
@@ -347,9 +403,9 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
 #pragma unroll
                     for (int r4 = 0; r4 < 4; ++r4) {
                         const int row = 16 * t + 4 * bq + r4;
-                        const uint32_t boff = (sok && p < P && row < m)
+                        const uint32_t boff = (bk && sok && p < P && row < m)
                                                   ? (uint32_t)((((size_t)s * P + p) * m + row) * 4) : 0x80000000u;
-                        Rn[ai][t][r4] = -__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbk, boff, 0, 0));
+                        Rn[ai][t][r4] = -__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(db, boff, 0, 0));
                     }
             }
         }
@@ -357,8 +413,10 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
             // step bs's block has landed (every wave's DMA), every wave is done with step bs - 1's
             // slot, and this wave's stores of step bs - 2 have completed (the ring reads Y[k - 1]'s
             // block NB - 2 >= 2 steps after it was written)
-            if (bs > 0) wait_prev_step(blk > 0 ? k : k - 1, K);
-            __syncthreads();
+            if (!(DADMM_ST_ABL & 4)) {
+                if (bs > 0) wait_prev_step(blk > 0 ? k : k - 1, K);
+                __syncthreads();
+            }
             // step bs + 2's block (past the last step: a zero-size descriptor, zeros into a slot no
             // step reads)
             dma(dk, dblk, lds + (slot == 0 ? 2 : slot - 1) * SF);
