@@ -223,6 +223,27 @@ __device__ __forceinline__ void lds_wait(uint32_t* c, uint32_t target) {
     asm volatile("" ::: "memory");
 }
 
+// DADMM_DMA_ASM=1: the A^T ring's LDS-DMA issued from inline asm. With the builtin the compiler
+// treats every later LDS read as a possible alias of an outstanding copy and adds its own
+// vmcnt waits before them (on top of the plan's exact waits); from inline asm the copies are
+// invisible to it and only the plan's waits (wait_vm(younger[q])) order them. Bit-identical, but
+// measured no faster here (0.599-0.613 vs 0.586-0.599 ms at H, profiles/r03/fused_dma_asm_r03.jsonl;
+// the streamed kernel needed it, dadmm_stream.hip), so off.
+#ifndef DADMM_DMA_ASM
+#define DADMM_DMA_ASM 0
+#endif
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4_t rsrc_words4(const void* base, uint32_t bytes) {
+    const uint64_t b = (uint64_t)base;
+    return (i32x4_t){(int)(uint32_t)b, (int)(uint32_t)(b >> 32) & 0xffff, (int)bytes, 0x00020000};
+}
+__device__ __forceinline__ void dma_lds16(uint32_t lds_addr, uint32_t voff, uint32_t soff, i32x4_t rsrc) {
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :
+                 : "s"(lds_addr), "v"(voff), "s"(rsrc), "s"(soff)
+                 : "memory", "m0");
+}
+
 // Compiler-only memory barrier: bounds how far the scheduler hoists operand loads.
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
 
@@ -282,6 +303,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     const uint32_t state_bytes = (uint32_t)((size_t)B * P * n * 4);
     const rsrc_t rA = make_rsrc(a.A, (uint32_t)(P * MP * NP * 4));
     const rsrc_t rAt = make_rsrc(a.At, (uint32_t)(P * MP * NP * 4));
+    const i32x4_t rAtw = rsrc_words4(a.At, (uint32_t)(P * MP * NP * 4));
 
     // ---- graph data --------------------------------------------------------------------------
     uint32_t msk[P], ord[P];
@@ -413,8 +435,13 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
         const int c = q >> 2, t = q & 3;
         const int p = c / T2, tt = c % T2;
 #endif
+#if DADMM_DMA_ASM
+        dma_lds16((uint32_t)(uintptr_t)(lds_void*)(Qlds + (w * QD + q % QD) * 256), vAt[tt] + 64 * t,
+                  (uint32_t)(p * NP * MP * 4), rAtw);
+#else
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rAt, (lds_void*)(Qlds + (w * QD + q % QD) * 256), 16,
                                                  vAt[tt] + 64 * t, (uint32_t)(p * NP * MP * 4), 0, 0);
+#endif
     };
 
 #if !DADMM_AT_DMA && DADMM_G2_PAIR

@@ -57,6 +57,9 @@ constexpr int SLOTS = 3;         // y-block ring: the block of step bs + 2 is lo
 #endif
 // cache policy of the state streams (y-block copies, U, d0, Y and U stores); 2 = non-temporal (so
 // that they would not evict the operator from L2) measured no faster (6.04 vs 5.96 ms, configs[2])
+#ifndef DADMM_ST_DESYNC
+#define DADMM_ST_DESYNC 0
+#endif
 #ifndef DADMM_ST_AUX
 #define DADMM_ST_AUX 0
 #endif
@@ -294,23 +297,48 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
         const int D = (k >= 1 && !(DADMM_ST_ABL & 1)) ? __builtin_amdgcn_readfirstlane(dmx[p]) : 0;   // 0 for p >= P
         const uint32_t* vrow = vt + (p * BT + j) * DP;
         const char* ybase = (const char*)(ys + 4 * (ct * 64 + lane));
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-        for (int t4 = 0; t4 < D; t4 += 4) {
-            const uint4 qo = *(const uint4*)(vrow + t4);
-            const uint32_t qa[4] = {qo.x, qo.y, qo.z, qo.w};
-            f32x4 yqs[4];   // the four neighbour reads in flight together
+        auto walk = [&]() {
+            f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (int t4 = 0; t4 < D; t4 += 4) {
+                const uint4 qo = *(const uint4*)(vrow + t4);
+                const uint32_t qa[4] = {qo.x, qo.y, qo.z, qo.w};
+                f32x4 yqs[4];   // the four neighbour reads in flight together
 #pragma unroll
-            for (int u = 0; u < 4; ++u) yqs[u] = *(const f32x4*)(ybase + qa[u]);
-            __builtin_amdgcn_sched_barrier(0);
+                for (int u = 0; u < 4; ++u) yqs[u] = *(const f32x4*)(ybase + qa[u]);
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const f32x4 yq = yqs[u];
-                const f32x2 d0 = pk_sub((f32x2){yo[0], yo[1]}, (f32x2){yq[0], yq[1]});
-                const f32x2 d1 = pk_sub((f32x2){yo[2], yo[3]}, (f32x2){yq[2], yq[3]});
-                acc = acc + (f32x4){d0[0], d0[1], d1[0], d1[1]};
+                for (int u = 0; u < 4; ++u) {
+                    const f32x4 yq = yqs[u];
+                    const f32x2 d0 = pk_sub((f32x2){yo[0], yo[1]}, (f32x2){yq[0], yq[1]});
+                    const f32x2 d1 = pk_sub((f32x2){yo[2], yo[3]}, (f32x2){yq[2], yq[3]});
+                    acc = acc + (f32x4){d0[0], d0[1], d1[0], d1[1]};
+                }
             }
+            return acc;
+        };
+        // GEMM2: A_p^T R_k, this tile's columns (16 dependent MFMAs, no input from the walk).
+        // DADMM_ST_DESYNC=1: the two waves of a SIMD (w and w + 4) take the walk and GEMM2 in opposite
+        // orders (one's VALU / LDS work beside the other's MFMA chain): measured 6.18-6.31 vs
+        // 6.13-6.19 ms at configs[2], so off.
+        auto gemm2 = [&]() {
+            f32x4 g = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4) g = mfma4(r.at[t][r4], Rk[ai][t][r4], g);
+            return g;
+        };
+        f32x4 acc, gc;
+        if (DADMM_ST_DESYNC && (w & 4)) {
+            gc = gemm2();
+            acc = walk();
+        } else {
+            acc = walk();
+            gc = gemm2();
         }
-        pre();   // the next tile's A^T rows, U, d0: after the walk (its LDS reads in flight need the VGPRs)
+        // the next tile's A^T rows, U, d0 and A rows: issued at one program point (outside the branch)
+        pre();
+        mid();
         f32x4 dv = k == 0 ? r.d : acc;
         if (k >= 1 && a.variant != 0) {
 #pragma unroll
@@ -324,12 +352,6 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
             uv[r4] = k >= 1 ? un : r.u[r4];
         }
         bad_u0 |= k == 0 && okc && !finite4(uv);
-        f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};   // GEMM2: A_p^T R_k, this tile's columns
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int r4 = 0; r4 < 4; ++r4) gc = mfma4(r.at[t][r4], Rk[ai][t][r4], gc);
-        mid();
         // U_k after the next tile's A rows are issued: vector-memory operations complete in order,
         // so a load issued after a store waits for it
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, uv),
