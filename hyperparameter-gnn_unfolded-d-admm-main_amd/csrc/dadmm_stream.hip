@@ -45,8 +45,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int NW = 8;            // waves per workgroup
-constexpr int THREADS = 64 * NW;
+constexpr int NW = 8;            // waves per workgroup (the default form; 16: one agent per wave)
 constexpr int CT = 2;            // 16-column MFMA tiles per step
 constexpr int CW = 16 * CT;      // columns per step
 constexpr int SLOTS = 3;         // y-block ring: the block of step bs + 2 is loaded during step bs
@@ -57,6 +56,9 @@ constexpr int SLOTS = 3;         // y-block ring: the block of step bs + 2 is lo
 #endif
 // cache policy of the state streams (y-block copies, U, d0, Y and U stores); 2 = non-temporal (so
 // that they would not evict the operator from L2) measured no faster (6.04 vs 5.96 ms, configs[2])
+#ifndef DADMM_ST_QPF
+#define DADMM_ST_QPF 0
+#endif
 #ifndef DADMM_ST_DESYNC
 #define DADMM_ST_DESYNC 0
 #endif
@@ -127,10 +129,10 @@ __device__ __forceinline__ void clips(int variant, int k, float& gclip, float& v
 __host__ __device__ constexpr int vt_stride(int P) {
     return 4 * (((2 * P + 3) / 4) | 1);
 }
-constexpr int slot_floats(int PW) { return NW * PW * CT * 64 * 4; }
-size_t lds_bytes(int PW, int P) {
-    const int PA = NW * PW;
-    return 4 * (size_t)SLOTS * slot_floats(PW) + 4 * (size_t)PA * BT * vt_stride(P) + 4 * (size_t)PA;
+constexpr int slot_floats(int NWT, int PW) { return NWT * PW * CT * 64 * 4; }
+size_t lds_bytes(int NWT, int PW, int P) {
+    const int PA = NWT * PW;
+    return 4 * (size_t)SLOTS * slot_floats(NWT, PW) + 4 * (size_t)PA * BT * vt_stride(P) + 4 * (size_t)PA;
 }
 
 // Step bs's block in the ring: chunk (q, ct, bq, j) = 16 bytes of agent q, sample j, columns
@@ -156,11 +158,13 @@ __device__ __forceinline__ void wait_prev_step(int kprev, int K) {
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
 }
 
-template <int PW>
-__global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
+template <int NWT, int PW>
+__global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
+    constexpr int NW = NWT;
+    constexpr bool RING = NWT == 8;   // the operand ring one tile ahead (two waves per SIMD)
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int PA = NW * PW;
-    constexpr int SF = slot_floats(PW);
+    constexpr int SF = slot_floats(NWT, PW);
     const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad, K = a.K, H = a.hyp_rows;
     const int DP = vt_stride(P);
     uint32_t* vt = (uint32_t*)(lds + SLOTS * SF);        // [PA][BT][DP] visit rows (byte offsets)
@@ -299,8 +303,18 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
         const char* ybase = (const char*)(ys + 4 * (ct * 64 + lane));
         auto walk = [&]() {
             f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#if DADMM_ST_QPF
+            // the next four entries are read while this group's rows are in flight (one LDS round
+            // trip per group instead of two; the read past a row's end stays inside the table / dmx)
+            uint4 qn = *(const uint4*)vrow;
+#endif
             for (int t4 = 0; t4 < D; t4 += 4) {
+#if DADMM_ST_QPF
+                const uint4 qo = qn;
+                qn = *(const uint4*)(vrow + t4 + 4);
+#else
                 const uint4 qo = *(const uint4*)(vrow + t4);
+#endif
                 const uint32_t qa[4] = {qo.x, qo.y, qo.z, qo.w};
                 f32x4 yqs[4];   // the four neighbour reads in flight together
 #pragma unroll
@@ -388,8 +402,10 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
     Ring r0, r1;
     dma(-1, 0, lds);          // (NB >= 4: stream_applies)
     dma(-1, 1, lds + SF);
-    fetch_a(-1, 0, 0, r0);
-    fetch_m(-1, 0, 0, r0);
+    if constexpr (RING) {
+        fetch_a(-1, 0, 0, r0);
+        fetch_m(-1, 0, 0, r0);
+    }
     int bs = 0;
     int slot = 0;                                        // bs % SLOTS
     int dk = -1, dblk = 2;                               // phase / block of step bs + 2
@@ -452,6 +468,11 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
             // the PW x CT tiles of the step, each a compile-time index (static ring slots)
             auto tile = [&](auto ic) {
                 constexpr int i = decltype(ic)::value;
+                if constexpr (!RING) {   // four waves per SIMD: A^T / U / d0 loaded at the tile's start,
+                    fetch_a(k, c0, i, r0);   // A after GEMM2 (into the A^T registers' room)
+                    compute(k, c0, ys, i, r0, [] {}, [&] { fetch_m(k, c0, i, r0); });
+                    return;
+                }
                 Ring& cur = (i & 1) ? r1 : r0;
                 Ring& nxt = (i & 1) ? r0 : r1;
                 constexpr bool last = i + 1 == PW * CT;
@@ -483,22 +504,34 @@ __global__ __launch_bounds__(THREADS) void stream_kernel(TiledArgs a) {
 
 // The streamed single-launch form applies to m <= 64 rows per agent, P <= 16 agents, and at least
 // four 32-column blocks (the ring reads Y[k - 1]'s block >= 2 steps after it was written).
+// waves per workgroup: DADMM_STREAM_WAVES=16 runs one agent per wave (P <= 16, 128 VGPRs, four
+// waves per SIMD) instead of the default 8 waves with two agents each
+static int stream_waves(int P) {
+    const char* e = getenv("DADMM_STREAM_WAVES");
+    return (e != nullptr && atoi(e) == 16 && P <= 16) ? 16 : stream::NW;
+}
+
 bool stream_applies(const TiledArgs& a) {
+    const int nw = stream_waves(a.P);
     return a.m_pad == 64 && a.P >= 1 && a.P <= 2 * stream::NW && a.n_pad % stream::CW == 0 &&
-           a.n_pad / stream::CW >= 4 && stream::lds_bytes(a.P <= stream::NW ? 1 : 2, a.P) <= 160 * 1024;
+           a.n_pad / stream::CW >= 4 && stream::lds_bytes(nw, (a.P + nw - 1) / nw, a.P) <= 160 * 1024;
 }
 
 hipError_t launch_stream(const TiledArgs& a, hipStream_t st) {
-    const int PW = a.P <= stream::NW ? 1 : 2;
-    const void* kern = PW == 1 ? (const void*)stream::stream_kernel<1> : (const void*)stream::stream_kernel<2>;
-    const size_t lds = stream::lds_bytes(PW, a.P);
+    const int nw = stream_waves(a.P);
+    const int PW = (a.P + nw - 1) / nw;
+    const void* kern = nw == 16 ? (const void*)stream::stream_kernel<16, 1>
+                                : (PW == 1 ? (const void*)stream::stream_kernel<8, 1> : (const void*)stream::stream_kernel<8, 2>);
+    const size_t lds = stream::lds_bytes(nw, PW, a.P);
     hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const int grid = (a.B + BT - 1) / BT;
-    if (PW == 1)
-        hipLaunchKernelGGL(stream::stream_kernel<1>, dim3(grid), dim3(stream::THREADS), lds, st, a);
+    if (nw == 16)
+        hipLaunchKernelGGL((stream::stream_kernel<16, 1>), dim3(grid), dim3(64 * 16), lds, st, a);
+    else if (PW == 1)
+        hipLaunchKernelGGL((stream::stream_kernel<8, 1>), dim3(grid), dim3(64 * 8), lds, st, a);
     else
-        hipLaunchKernelGGL(stream::stream_kernel<2>, dim3(grid), dim3(stream::THREADS), lds, st, a);
+        hipLaunchKernelGGL((stream::stream_kernel<8, 2>), dim3(grid), dim3(64 * 8), lds, st, a);
     return hipGetLastError();
 }
 
