@@ -391,6 +391,9 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
         ingest_ms = 1e3 * (time.perf_counter() - t0)
         op3, tab3, b3d = mod.operator(), mod.hyp_table(K3).detach(), b3t[..., 0].contiguous()
         ms = _event_ms(lambda: _fr(op3, b3d, g3, tab3), 5, warm=1)
+        # the training forward (trajectory recording for the adjoint): streamed vs stepwise
+        ms_rec = _event_ms(lambda: _fr(op3, b3d, g3, tab3, record=True), 3, warm=1)
+        ms_rec_sw = _event_ms(lambda: _fr(op3, b3d, g3, tab3, record=True, path="stepwise"), 3, warm=1)
 
         def f3():
             with torch.no_grad():
@@ -403,7 +406,8 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
                            "alg_bytes_per_unit": 4 * P3 * (4 * n3 + m3),
                            "alg_GBs": 4 * P3 * (4 * n3 + m3) * B3 * K3 / (ms * 1e-3) / 1e9,
                            "graph_ingest_ms": ingest_ms,
-                           "module_forward_ms_incl_ingest": ms_module}
+                           "module_forward_ms_incl_ingest": ms_module,
+                           "record_forward_ms": ms_rec, "record_forward_stepwise_ms": ms_rec_sw}
     except Exception as e:
         out["c3_error"] = repr(e)[:300]
     return out

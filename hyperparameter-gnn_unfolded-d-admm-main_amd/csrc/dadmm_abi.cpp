@@ -543,10 +543,11 @@ size_t dadmm_tiled_scratch_bytes(const dadmm_dims* d) {
            align256(sizeof(float) * (size_t)d->B * d->P * m_pad_of(d));
 }
 
-int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
-                        const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
-                        const float* hyp, const float* y0, const float* U0, const float* d0,
-                        float* Y, float* U_out, int32_t* status, void* scratch, void* stream) {
+static int forward_tiled_impl(const dadmm_dims* d, const void* op, const float* b,
+                              const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
+                              const float* hyp, const float* y0, const float* U0, const float* d0,
+                              float* Y, float* Grec, float* Urec, float* U_out, int32_t* status,
+                              void* scratch, void* stream) {
     int rc = check_dims(d);
     if (rc) return rc;
     if (d->B == 0 || d->K == 0) return ok();
@@ -594,9 +595,41 @@ int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
     a.hyp_rows = d->hyp_rows;
     a.variant = d->variant;
     a.graph_shared = d->graph_shared;
+    if (Grec != nullptr || Urec != nullptr) {   // recording: the streamed single-launch form only
+        if (Grec == nullptr || Urec == nullptr || !aligned16(Grec) || !aligned16(Urec))
+            return fail(DADMM_EINVAL, "Grec and Urec: both, 16-byte aligned");
+        if ((size_t)d->K * d->B * d->P * d->n * 4 >= ((size_t)1 << 40))
+            return fail(DADMM_EINVAL, "recording too large");
+        a.Grec = Grec;
+        a.Urec = Urec;
+        if (!dadmm::stream_applies(a))
+            return fail(DADMM_EUNSUPPORTED, "recording on the tiled path needs the streamed form (P <= 16, "
+                                            "m <= 64, n_pad >= 128): use dadmm_forward_stepwise");
+        hipError_t e = dadmm::launch_stream(a, (hipStream_t)stream);
+        if (e != hipSuccess) return fail(DADMM_EHIP, "streamed recording launch: %s", hipGetErrorString(e));
+        return ok();
+    }
     hipError_t e = dadmm::launch_tiled(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(DADMM_EHIP, "tiled launch: %s", hipGetErrorString(e));
     return ok();
+}
+
+int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
+                        const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
+                        const float* hyp, const float* y0, const float* U0, const float* d0,
+                        float* Y, float* U_out, int32_t* status, void* scratch, void* stream) {
+    return forward_tiled_impl(d, op, b, visit_ptr, visit_q, deg, hyp, y0, U0, d0, Y, nullptr, nullptr,
+                              U_out, status, scratch, stream);
+}
+
+int dadmm_forward_tiled_record(const dadmm_dims* d, const void* op, const float* b,
+                               const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
+                               const float* hyp, const float* y0, const float* U0, const float* d0,
+                               float* Y, float* Grec, float* Urec, float* U_out, int32_t* status,
+                               void* scratch, void* stream) {
+    if (Grec == nullptr || Urec == nullptr) return fail(DADMM_EINVAL, "Grec and Urec are required");
+    return forward_tiled_impl(d, op, b, visit_ptr, visit_q, deg, hyp, y0, U0, d0, Y, Grec, Urec, U_out,
+                              status, scratch, stream);
 }
 
 size_t dadmm_loss_scratch_bytes(int32_t K, int64_t rows, int32_t n) {

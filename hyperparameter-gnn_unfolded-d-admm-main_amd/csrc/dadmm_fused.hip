@@ -303,7 +303,9 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     const uint32_t state_bytes = (uint32_t)((size_t)B * P * n * 4);
     const rsrc_t rA = make_rsrc(a.A, (uint32_t)(P * MP * NP * 4));
     const rsrc_t rAt = make_rsrc(a.At, (uint32_t)(P * MP * NP * 4));
+#if DADMM_DMA_ASM
     const i32x4_t rAtw = rsrc_words4(a.At, (uint32_t)(P * MP * NP * 4));
+#endif
 
     // ---- graph data --------------------------------------------------------------------------
     uint32_t msk[P], ord[P];

@@ -170,6 +170,8 @@ struct TiledArgs {
     float* U_out;           // [B][P][n] or nullptr
     int32_t* status;        // or nullptr (OR-ed DADMM_STATUS_* bits)
     int B, P, m, m_pad, n, n_pad, K, hyp_rows, variant, graph_shared;
+    float* Grec;            // streamed form only, nullable: [K][B][P][n] pre-clamp gradients
+    float* Urec;            //   and U_k entering iteration k (the adjoint's trajectory)
 };
 size_t tiled_lds_bytes(int n_pad, int m_pad);
 hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream);

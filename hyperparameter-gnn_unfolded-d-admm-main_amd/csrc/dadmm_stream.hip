@@ -158,7 +158,7 @@ __device__ __forceinline__ void wait_prev_step(int kprev, int K) {
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
 }
 
-template <int NWT, int PW>
+template <int NWT, int PW, bool REC = false>
 __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
     constexpr int NW = NWT;
     constexpr bool RING = NWT == 8;   // the operand ring one tile ahead (two waves per SIMD)
@@ -372,13 +372,14 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
                                                make_rsrc(k == K ? a.U_out : a.Ubuf[0], (DADMM_ST_ABL & 8) ? 0u : s_bytes),
                                                k >= 1 ? soff : 0x80000000u, 0, DADMM_ST_AUX);
         const bool upd = k >= 0 && k < K;
-        f32x4 yn;
+        f32x4 yn, grc;
 #pragma unroll
         for (int r4 = 0; r4 < 4; ++r4) {   // :69-93, left to right
             const float y = yo[r4];
             float gr = gc[r4] + sign_times(y, ta[ai]);
             gr = gr + uv[r4] * dg[ai];
             gr = gr + dv[r4] * rh[ai];
+            grc[r4] = gr;
             bad_g |= upd && okc && gr != gr;
             gr = tclamp(gr, -gclip, gclip);
             const float v = tclamp(y - al[ai] * gr, -vclip, vclip);
@@ -388,6 +389,13 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, yn),
                                                make_rsrc(a.Y + (size_t)(upd ? k : 0) * S, (DADMM_ST_ABL & 8) ? 0u : s_bytes),
                                                upd ? soff : 0x80000000u, 0, DADMM_ST_AUX);
+        if constexpr (REC) {   // the adjoint's trajectory: Grec[k] (pre-clamp gradient), Urec[k] = U_k
+            const size_t kS = (size_t)(upd ? k : 0) * S;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, grc),
+                                                   make_rsrc(a.Grec + kS, s_bytes), upd ? soff : 0x80000000u, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, uv),
+                                                   make_rsrc(a.Urec + kS, s_bytes), upd ? soff : 0x80000000u, 0, 0);
+        }
         bad_y0 |= k == -1 && okc && !finite4(yo);   // the :55 guard on y_0
         // GEMM1: R_{k+1} += A_p[:, tile] y_{k+1}[tile] (phase -1: R_0 from y_0)
         const f32x4 gin = k == -1 ? yo : yn;
@@ -526,6 +534,16 @@ hipError_t launch_stream(const TiledArgs& a, hipStream_t st) {
     hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const int grid = (a.B + BT - 1) / BT;
+    if (a.Grec != nullptr) {   // recording (8 waves)
+        const void* rk = PW == 1 ? (const void*)stream::stream_kernel<8, 1, true> : (const void*)stream::stream_kernel<8, 2, true>;
+        const size_t rl = stream::lds_bytes(8, (a.P + 7) / 8, a.P);
+        if ((e = hipFuncSetAttribute(rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rl)) != hipSuccess) return e;
+        if (a.P <= 8)
+            hipLaunchKernelGGL((stream::stream_kernel<8, 1, true>), dim3(grid), dim3(64 * 8), rl, st, a);
+        else
+            hipLaunchKernelGGL((stream::stream_kernel<8, 2, true>), dim3(grid), dim3(64 * 8), rl, st, a);
+        return hipGetLastError();
+    }
     if (nw == 16)
         hipLaunchKernelGGL((stream::stream_kernel<16, 1>), dim3(grid), dim3(64 * 16), lds, st, a);
     else if (PW == 1)

@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "dadmm_prologue",
     "dadmm_tiled_scratch_bytes",
     "dadmm_forward_tiled",
+    "dadmm_forward_tiled_record",
     "dadmm_graph_generate",
     "dadmm_loss_scratch_bytes",
     "dadmm_loss",
@@ -171,6 +172,8 @@ def load() -> ctypes.CDLL:
     L.dadmm_tiled_scratch_bytes.argtypes = [D]
     L.dadmm_forward_tiled.restype = ctypes.c_int
     L.dadmm_forward_tiled.argtypes = [D] + [vp] * 14
+    L.dadmm_forward_tiled_record.restype = ctypes.c_int
+    L.dadmm_forward_tiled_record.argtypes = [D] + [vp] * 16
     L.dadmm_graph_generate.restype = ctypes.c_int
     L.dadmm_graph_generate.argtypes = [i32, i32, f32, u64, i32] + [vp] * 7
     L.dadmm_loss_scratch_bytes.restype = ctypes.c_size_t

@@ -113,7 +113,7 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     path "auto": the fused kernel when the shape is compiled, otherwise the tiled kernel (one
     launch per iteration); either is followed by the device-gated stepwise recomputation (runs only
     if a guard event was flagged). Training (record) outside the fused shapes: the stepwise
-    kernels. "fused" / "tiled" / "stepwise" force one path ("fused" / "tiled" alone do NOT apply
+    kernels, or the streamed single launch where it applies (P <= 16, m <= 64). "fused" / "tiled" / "stepwise" force one path ("fused" / "tiled" alone do NOT apply
     the guards: their status only flags them).
 
     record: also store the trajectory the adjoint consumes (training; dadmm_forward_record).
@@ -182,7 +182,21 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
             else:
                 _lib.check("dadmm_forward_record" if record else "dadmm_forward", rc)
         tiled = path == "tiled" or (path == "auto" and not fused and not record)
-        if tiled:
+        if record and not fused and path in ("auto", "tiled"):
+            # the streamed single launch records the trajectory (P <= 16, m <= 64); otherwise the
+            # stepwise kernels below record it
+            tb = L.dadmm_tiled_scratch_bytes(ctypes.byref(d))
+            tscratch = torch.empty(max(tb, 256), dtype=torch.uint8, device=b.device)
+            rc = L.dadmm_forward_tiled_record(
+                ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.vptr), _ptr(graphs.vq),
+                _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(Grec),
+                _ptr(Urec), _ptr(U), _ptr(status), _ptr(tscratch), stream)
+            if rc == _lib.DADMM_EUNSUPPORTED and path == "auto":
+                tiled = False
+            else:
+                _lib.check("dadmm_forward_tiled_record", rc)
+                tiled = True
+        elif tiled:
             tb = L.dadmm_tiled_scratch_bytes(ctypes.byref(d))
             tscratch = torch.empty(max(tb, 256), dtype=torch.uint8, device=b.device)
             rc = L.dadmm_forward_tiled(

@@ -164,8 +164,11 @@ int dadmm_prologue(uint64_t seed, uint64_t offset, int64_t numel, int32_t n, int
 /* Bytes of device scratch dadmm_forward_tiled needs for `d` (256-byte aligned pointer). */
 size_t dadmm_tiled_scratch_bytes(const dadmm_dims* d);
 
-/* The K-step forward, two launches per iteration with the state in HBM — the path for shapes the
- * fused kernel cannot hold on chip (P > 6 or n > 256; e.g. P = 16, n = 512). A consensus launch forms
+/* The K-step forward for shapes the fused kernel cannot hold on chip (P > 6 or n > 256; e.g. P = 16,
+ * n = 512), state in HBM. For P <= 16, m <= 64, n_pad >= 128 it is ONE launch (the streamed form,
+ * dadmm_stream.hip: 16 samples x all agents per workgroup, y_k staged per 32-column block, R_k in
+ * registers, the next iteration's GEMM1 fused into the update; environment DADMM_TILED_STREAM=0
+ * selects the per-iteration launches below instead). Otherwise two launches per iteration: a consensus launch forms
  * delta_k for every agent of a sample from y_k (visit lists, the reference's order; scratch), then
  * each (32-sample tile, agent) workgroup applies the deferred dual update, the factored gradient
  * GEMM pair and the primal update; Y is bit-identical to dadmm_forward_stepwise's on guard-free
@@ -181,6 +184,20 @@ int dadmm_forward_tiled(const dadmm_dims* d, const void* op, const float* b,
                         const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
                         const float* hyp, const float* y0, const float* U0, const float* d0,
                         float* Y, float* U_out, int32_t* status, void* scratch, void* stream);
+
+/* dadmm_forward_tiled that also records the adjoint's trajectory, as dadmm_forward_record does for
+ * the fused shapes: Grec [K][B][P][n] = the pre-clamp gradient of iteration k (unfolded_DLASSO.py:
+ * 73-77) and Urec [K][B][P][n] = U_k entering iteration k; bit-identical to the stepwise recording
+ * (dadmm_forward_stepwise with Grec / Urec) on guard-free inputs. Only the streamed single-launch
+ * form records: P <= 16, m <= 64, n_pad >= 128 (DADMM_EUNSUPPORTED otherwise: record with
+ * dadmm_forward_stepwise). Guards are flagged in `status` as by dadmm_forward_tiled; the gated
+ * dadmm_forward_stepwise behind it (with the same Grec / Urec) re-records a flagged batch exactly.
+ * Replaces: the forward half of loss.backward() through DLASSO_unfolded (unfolded_train_new.py:74-80). */
+int dadmm_forward_tiled_record(const dadmm_dims* d, const void* op, const float* b,
+                               const int32_t* visit_ptr, const uint8_t* visit_q, const float* deg,
+                               const float* hyp, const float* y0, const float* U0, const float* d0,
+                               float* Y, float* Grec, float* Urec, float* U_out, int32_t* status,
+                               void* scratch, void* stream);
 
 /* Bytes of device scratch dadmm_forward_stepwise needs for `d` (256-byte aligned pointer). */
 size_t dadmm_stepwise_scratch_bytes(const dadmm_dims* d);

@@ -18,3 +18,4 @@ done
 DADMM_STREAM_WAVES=16 timeout -k 10 300 python -u -m pytest tests/test_gpu_stream.py -x -q --timeout 120 --timeout-method thread > $OUT/tests16.log 2>&1; echo "tests16 rc=$?"; tail -1 $OUT/tests16.log
 DADMM_LIB_VARIANT=$PWD/build/var/libdadmm_qpf.so timeout -k 10 300 python -u -m pytest tests/test_gpu_stream.py -x -q --timeout 120 --timeout-method thread > $OUT/testsqpf.log 2>&1; echo "testsqpf rc=$?"; tail -1 $OUT/testsqpf.log
 timeout -k 10 300 python -u -m pytest tests/test_gpu_stream.py -x -q --timeout 120 --timeout-method thread > $OUT/tests8.log 2>&1; echo "tests8 rc=$?"; tail -1 $OUT/tests8.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_adjoint.py tests/test_gpu_train.py -x -q --timeout 200 --timeout-method thread > $OUT/tests_adj.log 2>&1; echo "tests_adj rc=$?"; tail -1 $OUT/tests_adj.log

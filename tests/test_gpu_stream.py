@@ -100,3 +100,41 @@ def test_stream_flags_nonfinite_inputs(cuda, monkeypatch):
     h2 = hyp.copy(); h2[1, 9, 0] = np.nan
     assert run(b, [G] * B, h2, y0, U0, d0) & 8
     assert run(b, [G] * B, hyp, y0, U0, d0) == 0
+
+
+@pytest.mark.parametrize("P,m,n,B,K,prob,per_sample,variant,H", [
+    (16, 64, 512, 37, 6, 0.3, True, 0, 16),
+    (9, 40, 320, 18, 5, 0.4, True, 1, 1),
+    (8, 64, 128, 16, 3, 0.6, False, 0, 8),
+])
+def test_stream_recording_bit_exact(cuda, P, m, n, B, K, prob, per_sample, variant, H):
+    """Training forward (record=True) on the streamed launch (dadmm_forward_tiled_record): Y, U_K
+    and the adjoint's trajectory Grec / Urec bit-exact against oracle.forward_f32_rec, and the
+    general adjoint on it agrees with the one on the stepwise recording."""
+    from dadmm_hip import PreparedOperator, forward_raw, ingest
+    from dadmm_hip.ops import backward_raw
+    A, b, _ = O.make_problem(P, m, n, B, seed=7 * P + n)
+    graphs = ([O.connected_er_graph(P, prob, seed=900 + s) for s in range(B)] if per_sample
+              else [O.er_graph(P, prob, seed=9)] * B)
+    y0, U0, d0 = _inits(B, P, n, seed=K)
+    rng = np.random.default_rng(P * K)
+    hyp = O.hyp_table((0.5 * rng.standard_normal((K, H, 4))).astype(np.float32), MAXP)
+    op = PreparedOperator(_t(A, cuda))
+    g = ingest(graphs, P, B, cuda)
+    outs = {}
+    for path in ("auto", "stepwise"):
+        Y, U, st, traj = forward_raw(op, _t(b, cuda), g, _t(hyp, cuda), _t(y0, cuda), _t(U0, cuda),
+                                     _t(d0, cuda), variant=variant, want_U=True, path=path,
+                                     record=True)
+        torch.cuda.synchronize()
+        outs[path] = (Y, U, int(st.item()), traj)
+    Yo, Uo, sto, Go, Uro = O.forward_f32_rec(A, b, graphs, hyp, y0, U0, d0, variant=variant)
+    for path, (Y, U, st, traj) in outs.items():
+        assert st == sto == 0, path
+        assert np.array_equal(Y.cpu().numpy(), Yo), path
+        assert np.array_equal(U.cpu().numpy(), Uo), path
+        assert np.array_equal(traj.Grec[..., :n].cpu().numpy(), Go), path
+        assert np.array_equal(traj.Urec[..., :n].cpu().numpy(), Uro), path
+    gY = np.random.default_rng(3).standard_normal((K, B, P, n)).astype(np.float32)
+    dh = [backward_raw(op, g, outs[p][3], _t(gY, cuda)).cpu().numpy() for p in ("auto", "stepwise")]
+    assert np.array_equal(dh[0], dh[1])
