@@ -89,7 +89,8 @@ __device__ __forceinline__ i32x4 rsrc_words(const void* base, uint32_t bytes) {
 // wait analysis then does not treat every later LDS read as a possible alias of the copy (it would
 // wait for the whole copy before the first such read, i.e. two steps too early); the kernel waits
 // for its copies itself (wait_prev_step). The compiler's own vmcnt waits stay correct: a copy it
-// does not count only makes them wait longer.
+// does not count only makes them wait longer. (m0 is a reserved register, so the compiler warns
+// about the clobber; no other instruction of this kernel reads m0 — checked in its ISA.)
 __device__ __forceinline__ void dma16(uint32_t lds_addr, uint32_t voff, i32x4 rsrc) {
     asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" DADMM_ST_DMA_POL " lds"
                  :
