@@ -56,6 +56,11 @@ constexpr int SLOTS = 3;         // y-block ring: the block of step bs + 2 is lo
 #endif
 // cache policy of the state streams (y-block copies, U, d0, Y and U stores); 2 = non-temporal (so
 // that they would not evict the operator from L2) measured no faster (6.04 vs 5.96 ms, configs[2])
+// DADMM_ST_PRIO=1: raise the wave's priority while it issues an MFMA chain (the arbiter then
+// prefers it, so the matrix pipe is fed while the other wave of the SIMD runs its VALU work)
+#ifndef DADMM_ST_PRIO
+#define DADMM_ST_PRIO 0
+#endif
 #ifndef DADMM_ST_QPF
 #define DADMM_ST_QPF 0
 #endif
@@ -336,11 +341,13 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
         // orders (one's VALU / LDS work beside the other's MFMA chain): measured 6.18-6.31 vs
         // 6.13-6.19 ms at configs[2], so off.
         auto gemm2 = [&]() {
+            if (DADMM_ST_PRIO) __builtin_amdgcn_s_setprio(1);
             f32x4 g = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int r4 = 0; r4 < 4; ++r4) g = mfma4(r.at[t][r4], Rk[ai][t][r4], g);
+            if (DADMM_ST_PRIO) __builtin_amdgcn_s_setprio(0);
             return g;
         };
         f32x4 acc, gc;
@@ -401,10 +408,12 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
         // GEMM1: R_{k+1} += A_p[:, tile] y_{k+1}[tile] (phase -1: R_0 from y_0)
         const f32x4 gin = k == -1 ? yo : yn;
         if (k < K - 1) {
+            if (DADMM_ST_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int r4 = 0; r4 < 4; ++r4) Rn[ai][t] = mfma4(r.am[t][r4], gin[r4], Rn[ai][t]);
+            if (DADMM_ST_PRIO) __builtin_amdgcn_s_setprio(0);
         }
     };
 
