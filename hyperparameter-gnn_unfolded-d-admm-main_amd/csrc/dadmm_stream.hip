@@ -57,9 +57,11 @@ constexpr int SLOTS = 3;         // y-block ring: the block of step bs + 2 is lo
 // cache policy of the state streams (y-block copies, U, d0, Y and U stores); 2 = non-temporal (so
 // that they would not evict the operator from L2) measured no faster (6.04 vs 5.96 ms, configs[2])
 // DADMM_ST_PRIO=1: raise the wave's priority while it issues an MFMA chain (the arbiter then
-// prefers it, so the matrix pipe is fed while the other wave of the SIMD runs its VALU work)
+// prefers it, so the matrix pipe is fed while the other wave of the SIMD runs its VALU work):
+// 6.03-6.07 vs 6.09-6.14 ms at configs[2], four interleaved rounds, bit-identical
+// (profiles/r03/stream_prio_r03.jsonl)
 #ifndef DADMM_ST_PRIO
-#define DADMM_ST_PRIO 0
+#define DADMM_ST_PRIO 1
 #endif
 #ifndef DADMM_ST_QPF
 #define DADMM_ST_QPF 0
