@@ -67,19 +67,80 @@ def make_args(K):
                               penalty_reduction_factor=0.95)
 
 
+def spawn_ranks(n, cmd=None, timeout=None):
+    """Run ``n`` ranks of this benchmark as child processes (one per GPU, LOCAL_RANK = rank) with
+    torchrun's environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free
+    MASTER_PORT). The parent never touches the GPU. When a rank fails, the others are terminated.
+    Returns the exit status to report: 0 when every rank succeeded."""
+    import signal
+    import socket
+    import subprocess
+    if cmd is None:
+        cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+    t0 = time.time()
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = abs(bad[0]) or 1
+                break
+            if all(c == 0 for c in codes):
+                break
+            if timeout is not None and time.time() - t0 > timeout:
+                rc = 124
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    return rc
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without torchrun: launch the N ranks here
+        sys.exit(spawn_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if a.gpus != world:
+        print(f"error: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     dist = None
+    # ranks beyond the visible devices share them (a one-GPU rehearsal of the N-rank path; RCCL
+    # refuses two ranks on one device, so such a run sets DADMM_DIST_BACKEND=gloo)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    backend = os.environ.get("DADMM_DIST_BACKEND") or "nccl"
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
     torch.cuda.set_device(dev)
+    # collectives of this script on the backend's device (gloo reduces host tensors)
+    cdev = dev if backend == "nccl" else torch.device("cpu")
 
     import oracle as O   # input generator (reference distribution) and checker only
     import unfolded_DLASSO
@@ -121,9 +182,12 @@ def main():
 
     timed = _Timed()
 
+    statuses = []
+
     def step():
         with torch.no_grad():
             Y, _ = model(bt, graph_list)
+        statuses.append(model.last_status)     # device word, no host sync here
         return Y
 
     for _ in range(a.warmup):
@@ -145,16 +209,21 @@ def main():
     elapsed = time.perf_counter() - t0
     L.dadmm_forward = orig_forward
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev_pairs]))
+    # every timed forward must have run the work it claims: a fired guard (status != 0) means
+    # the batch went through the reference's reset / recompute path instead
+    head_status = _or_all(statuses)
 
     if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, float(head_status != 0)], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = float(t[0].item())
+        if t[1].item() != 0 and head_status == 0:
+            head_status = -1          # another rank's forwards fired a guard
         # the reference's one collective: the epoch loss (a scalar all-reduce over RCCL)
         with torch.no_grad():
             Y, _ = model(bt, graph_list)
             lf = ((Y[-1, ..., 0] - x.to(dev)[:, None, :]) ** 2).mean()
-        red = torch.stack([lf, torch.ones((), device=dev)])
+        red = torch.stack([lf, torch.ones((), device=dev)]).to(cdev)
         dist.all_reduce(red)
 
     units_per_step = B * K
@@ -185,10 +254,15 @@ def main():
 
         parity = check_parity(O, model, A, b, G, dev, P, n, m, K)
         # the CPU baseline and the single-GPU secondary measurements belong to the N = 1 run
-        cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(
-            O, A, b, G, model, P, n, m, K, a.cpu_baseline_seconds)
+        cpu = None
+        if not (a.no_cpu_baseline or world > 1):
+            cpu = cpu_baseline(O, A, b, G, model, P, n, m, K, a.cpu_baseline_seconds)
+            # BASELINE configs[0], the reference's own CPU-runnable case ("run
+            # at c1 and at H"): P=5, n=200, m_p=50, batch=32, K=15
+            cpu["configs0"] = cpu_baseline_configs0(O, a.cpu_baseline_seconds / 3)
+        status = {"headline_forward": head_status}
         extras = None if (a.no_extras or world > 1) else secondary(O, dev, A, b, x, G, model, P, n,
-                                                                   m, K, B)
+                                                                   m, K, B, status)
         out = {
             "metric": "ADMM-iters/sec (node), batch=4096 P=5 n=256 K=25; final-iter MSE vs ref",
             "value": value,
@@ -224,10 +298,30 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "extras": extras,
+            # guard status word of every timed workload (0: the measured work is the work claimed)
+            "status": status,
         }
         print(json.dumps(out))
+        bad = {k: v for k, v in status.items() if v != 0}
+        if bad:
+            print(f"error: guard status set on timed workloads {bad}: numbers not valid",
+                  file=sys.stderr)
+            if dist is not None:
+                dist.destroy_process_group()
+            sys.exit(3)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _or_all(statuses) -> int:
+    """Bitwise OR of device status words (one host sync)."""
+    if not statuses:
+        return 0
+    v = torch.cat([t.reshape(-1).to(torch.int64) for t in statuses])
+    out = 0
+    for w in v.cpu().tolist():
+        out |= int(w)
+    return out
 
 
 def _event_ms(fn, reps, warm=2):
@@ -243,13 +337,19 @@ def _event_ms(fn, reps, warm=2):
     return e0.elapsed_time(e1) / reps
 
 
-def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
+def secondary(O, dev, A, b, x, G, model, P, n, m, K, B, status):
     """Secondary measurements on the same box, outside the timed region (not the headline):
     the training step at the headline shape (recording forward + adjoint kernel, and the module's
-    forward + compute_loss + loss.backward()), the GNN-hypernetwork model's forward
-    (DLASSO_GNNHyp3_Progressive, h = 100) and BASELINE configs[2]'s P=16, n=512 shape, which the
-    stepwise path serves."""
+    forward + compute_loss + loss.backward()), the GNN-hypernetwork model's forward and training
+    step (DLASSO_GNNHyp3_Progressive, h = 100) at B = 1024 / 256 and at the headline batch
+    B = 4096, configs[4]'s per-GPU shard of the GNN model, and BASELINE configs[2]'s P=16, n=512
+    shape (streamed forward, recording forward, general adjoint). ``status`` collects every timed
+    workload's guard status word (bench exits non-zero if any is set)."""
     out = {}
+
+    def st(name, word):
+        status[name] = _or_all([word]) if torch.is_tensor(word) else int(word)
+
     try:
         import gnn_dlasso_utils
         from dadmm_hip.ops import backward_raw, forward_raw
@@ -262,7 +362,8 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
         bb = b.to(dev)
         out["train_forward_record_ms"] = _event_ms(
             lambda: forward_raw(op, bb, g, table, record=True), 10)
-        _, _, _, tr = forward_raw(op, bb, g, table, record=True)
+        _, _, s_rec, tr = forward_raw(op, bb, g, table, record=True)
+        st("train_forward_record", s_rec)
         gY = torch.randn(K, B, P, n, device=dev)
         out["adjoint_ms"] = _event_ms(lambda: backward_raw(op, g, tr, gY), 10)
         model.train()
@@ -273,6 +374,7 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
             model.zero_grad()
             lf.backward()
         out["module_train_step_ms"] = _event_ms(step, 5)
+        st("module_train_step", model.last_status)
         out["train_units_per_s"] = B * K / (out["module_train_step_ms"] * 1e-3)
         model.eval()
     except Exception as e:  # secondary numbers never break the headline line
@@ -285,48 +387,60 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
         args = _ap.Namespace(GHN_iter_num=K, GHyp_hidden=100, DADMM_mode="diff", alpha_max=0.1,
                              tau_max=0.99, rho_max=0.99, eta_max=0.99)
         gnn = GM.DLASSO_GNNHyp3_Progressive(torch.from_numpy(A)[None].to(dev), args).to(dev).eval()
-        Bg = 1024
-        graphs = [O.connected_er_graph(P, 0.5, seed=100 + s) for s in range(Bg)]
-        bg = b[:Bg, ..., None].to(dev)
         from dadmm_hip.graph import ingest as _ing
+        graphs = [O.connected_er_graph(P, 0.5, seed=100 + s) for s in range(B)]
         t0 = time.perf_counter()
-        gbg = _ing(graphs, P, Bg, dev)     # ingested once; both models accept the GraphBatch
+        gball = _ing(graphs, P, B, dev)     # ingested once; both models accept the GraphBatch
         torch.cuda.synchronize()
         ingest_ms = 1e3 * (time.perf_counter() - t0)
-        gbt = _ing(graphs[:256], P, 256, dev)
+        for Bg in (1024, B):
+            bg = b[:Bg, ..., None].to(dev)
+            gbg = gball if Bg == B else _ing(graphs[:Bg], P, Bg, dev)
 
-        def gfwd():
-            with torch.no_grad():
-                gnn(bg, gbg)
-        ms = _event_ms(gfwd, 3, warm=1)
-        gnn.hyper_backend = "torch"
-        ms_torch = _event_ms(gfwd, 2, warm=1)
-        gnn.hyper_backend = "auto"
-        out["gnn_forward"] = {"B": Bg, "P": P, "n": n, "m": m, "K": K, "hidden": 100, "ms": ms,
-                              "units_per_s": Bg * K / (ms * 1e-3),
-                              "hypernetwork": "fused HIP (dadmm_hyper_*)",
-                              "ms_torch_hypernetwork": ms_torch, "graph_ingest_ms": ingest_ms,
-                              "note": "graphs pre-ingested (GraphBatch); host ingestion timed separately"}
+            def gfwd():
+                with torch.no_grad():
+                    gnn(bg, gbg)
+            ms = _event_ms(gfwd, 3, warm=1)
+            st(f"gnn_forward_B{Bg}", gnn.last_status)
+            rec = {"B": Bg, "P": P, "n": n, "m": m, "K": K, "hidden": 100, "ms": ms,
+                   "units_per_s": Bg * K / (ms * 1e-3), "hypernetwork": "fused HIP (dadmm_hyper_*)",
+                   "note": "graphs pre-ingested (GraphBatch); host ingestion timed separately"}
+            if Bg == 1024:
+                gnn.hyper_backend = "torch"
+                rec["ms_torch_hypernetwork"] = _event_ms(gfwd, 2, warm=1)
+                gnn.hyper_backend = "auto"
+                out["gnn_forward"] = rec
+            else:
+                rec["graph_ingest_ms"] = ingest_ms
+                out["gnn_forward_headline_batch"] = rec
+            del bg
         # training step of the GNN model (model.train(): dropout, batch statistics, autograd):
-        # forward + compute_loss + backward, HIP training hypernetwork vs the torch composition
-        Bt = 256
-        bgt = b[:Bt, ..., None].to(dev)
-        lab = x[:Bt].to(dev)[..., None]
-        gnn.train()
+        # forward + compute_loss + backward, HIP training hypernetwork (vs the torch composition
+        # at B = 256)
+        for Bt in (256, B):
+            bgt = b[:Bt, ..., None].to(dev)
+            lab = x[:Bt].to(dev)[..., None]
+            gbt = gball if Bt == B else _ing(graphs[:Bt], P, Bt, dev)
+            gnn.train()
 
-        def gstep():
-            Y, _ = gnn(bgt, gbt)
-            _, lf = gnn_dlasso_utils.compute_loss(Y, lab)
-            gnn.zero_grad()
-            lf.backward()
-        ms_tr = _event_ms(gstep, 3, warm=1)
-        gnn.hyper_backend = "torch"
-        ms_tr_torch = _event_ms(gstep, 2, warm=1)
-        gnn.hyper_backend = "auto"
-        gnn.eval()
-        out["gnn_train_step"] = {"B": Bt, "K": K, "ms": ms_tr, "units_per_s": Bt * K / (ms_tr * 1e-3),
-                                 "hypernetwork": "HIP training kernels (HyperTrainFn)",
-                                 "ms_torch_hypernetwork": ms_tr_torch}
+            def gstep():
+                Y, _ = gnn(bgt, gbt)
+                _, lf = gnn_dlasso_utils.compute_loss(Y, lab)
+                gnn.zero_grad()
+                lf.backward()
+            ms_tr = _event_ms(gstep, 3, warm=1)
+            st(f"gnn_train_step_B{Bt}", gnn.last_status)
+            rec = {"B": Bt, "K": K, "ms": ms_tr, "units_per_s": Bt * K / (ms_tr * 1e-3),
+                   "hypernetwork": "HIP training kernels (GnnTrainFn)"}
+            if Bt == 256:
+                gnn.hyper_backend = "torch"
+                rec["ms_torch_hypernetwork"] = _event_ms(gstep, 2, warm=1)
+                gnn.hyper_backend = "auto"
+                out["gnn_train_step"] = rec
+            else:
+                out["gnn_train_step_headline_batch"] = rec
+            gnn.eval()
+        del gnn, gball
     except Exception as e:
         out["gnn_error"] = repr(e)[:300]
     try:
@@ -361,6 +475,7 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
             with torch.no_grad():
                 g5(b5t, gb5)          # graphs ingested once (the tensor fast path)
         ms5 = _event_ms(g5fwd, 1, warm=1)
+        st("c5_gnn_forward", g5.last_status)
         out["c5_gnn_forward"] = {"B": B5, "P": P5, "n": n5, "m": m5, "K": K5, "hidden": 100,
                                  "graph_prob": 0.5, "ms": ms5,
                                  "units_per_s": B5 * K5 / (ms5 * 1e-3),
@@ -375,6 +490,7 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
         out["c5_error"] = repr(e)[:300]
     try:
         import unfolded_DLASSO
+        from dadmm_hip.ops import backward_raw as _br
         P3, n3, m3, B3, K3 = 16, 512, 64, 4096, 25
         A3, b3, _ = O.make_problem(P3, m3, n3, B3, seed=77)
         mod = unfolded_DLASSO.DLASSO_unfolded(torch.from_numpy(A3)[None].to(dev),
@@ -391,14 +507,21 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
         ingest_ms = 1e3 * (time.perf_counter() - t0)
         op3, tab3, b3d = mod.operator(), mod.hyp_table(K3).detach(), b3t[..., 0].contiguous()
         ms = _event_ms(lambda: _fr(op3, b3d, g3, tab3), 5, warm=1)
+        st("c3_forward", _fr(op3, b3d, g3, tab3)[2])
         # the training forward (trajectory recording for the adjoint): streamed vs stepwise
         ms_rec = _event_ms(lambda: _fr(op3, b3d, g3, tab3, record=True), 3, warm=1)
         ms_rec_sw = _event_ms(lambda: _fr(op3, b3d, g3, tab3, record=True, path="stepwise"), 3, warm=1)
+        _, _, s3r, tr3 = _fr(op3, b3d, g3, tab3, record=True)
+        st("c3_record_forward", s3r)
+        gY3 = torch.randn(K3, B3, P3, n3, device=dev)
+        ms_adj = _event_ms(lambda: _br(op3, g3, tr3, gY3), 3, warm=1)
+        del tr3, gY3
 
         def f3():
             with torch.no_grad():
                 mod(b3t, graphs3)
         ms_module = _event_ms(f3, 2, warm=1)
+        st("c3_module_forward", mod.last_status)
         out["c3_tiled"] = {"B": B3, "P": P3, "n": n3, "m": m3, "K": K3, "graph_prob": 0.3,
                            "path": "streamed single launch (dadmm_stream.hip) + gated stepwise",
                            "ms_per_forward": ms,
@@ -407,7 +530,8 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B):
                            "alg_GBs": 4 * P3 * (4 * n3 + m3) * B3 * K3 / (ms * 1e-3) / 1e9,
                            "graph_ingest_ms": ingest_ms,
                            "module_forward_ms_incl_ingest": ms_module,
-                           "record_forward_ms": ms_rec, "record_forward_stepwise_ms": ms_rec_sw}
+                           "record_forward_ms": ms_rec, "record_forward_stepwise_ms": ms_rec_sw,
+                           "adjoint_ms": ms_adj}
     except Exception as e:
         out["c3_error"] = repr(e)[:300]
     return out
@@ -456,7 +580,25 @@ def _host_cpus():
     return threads, model, quota
 
 
-def cpu_baseline(O, A, b, G, model, P, n, m, K, seconds):
+def cpu_baseline_configs0(O, seconds):
+    """The CPU legs at BASELINE configs[0] (P=5, n=200, m=50, B=32, K=15, one shared ER(0.5)
+    graph, the reference's default hyper-parameter init param = 0): the batch of 32 problems
+    is run repeatedly for a bounded sample; ADMM-iters/s = 32 K / seconds per forward."""
+    import argparse as _ap
+
+    import unfolded_DLASSO
+    P, n, m, B, K = 5, 200, 50, 32, 15
+    A, b, _ = O.make_problem(P, m, n, B, seed=1200)
+    G = O.er_graph(P, 0.5, seed=7)
+    mod = unfolded_DLASSO.DLASSO_unfolded(torch.from_numpy(A)[None], _ap.Namespace(
+        GHN_iter_num=K, DADMM_mode="diff", alpha_max=0.1, tau_max=0.99, rho_max=0.99,
+        eta_max=0.99, max_penalty_threshold=0.8, penalty_reduction_factor=0.95)).eval()
+    res = cpu_baseline(O, A, torch.from_numpy(b), G, mod, P, n, m, K, seconds, fixed_batch=True)
+    res["config"] = {"P": P, "n": n, "m": m, "B": B, "K": K, "graph_prob": 0.5}
+    return res
+
+
+def cpu_baseline(O, A, b, G, model, P, n, m, K, seconds, fixed_batch=False):
     """CPU baseline on the GPU box's host (BASELINE.md's CPU plan), a bounded
     sample of the same workload per leg, scaled to ADMM-iters/s. Legs (all ports of the reference
     forward, fp32; the reference itself may not run here):
@@ -484,6 +626,8 @@ def cpu_baseline(O, A, b, G, model, P, n, m, K, seconds):
         B0, Bmax = min(B0, len(bn)), min(Bmax, len(bn))
         torch.set_num_threads(threads)
         O.set_threads(threads)
+        if fixed_batch:
+            B0 = Bmax = len(bn)
         Bs, done, t_total = B0, 0, 0.0
         while t_total < per_leg:
             y0, U0, d0 = (1e-2 * rng.standard_normal((3, Bs, P, n))).astype(np.float32)

@@ -4,7 +4,7 @@
 // There the hyper-parameters of iteration k come from a GNN evaluated on [A^T A y_k, A^T b], so
 // the K-step loop cannot be fused: each iteration is
 //   gram     AtAy_k = A^T (A y_k)            (:158-162; MFMA GEMM pair, f32 fma chains)
-//   [host]   hyp_k = GNN(cat(AtAy_k, Atb))   (torch / hipBLASLt; :165-196)
+//   [host]   hyp_k = GNN(cat(AtAy_k, Atb))   (the HIP hypernetwork, dadmm_hyper*.hip; :165-196)
 //   step     g_k = clamp(AtAy - Atb + sign(y) tau + U deg + delta rho, +-gclip)   (:205-213)
 //            y_{k+1} = clamp(y - alpha g); delta_{k+1} = clamp(2 L y_{k+1}); U_{k+1} = clamp(U +
 //            delta eta)                                                           (:221-232)

@@ -9,7 +9,8 @@
 // The forward kernels are the train epilogues of dadmm_hyper.hip (HYPER_EPI_GCN_TRAIN and the
 // rownorm dropout); the dropout masks are regenerated here from the same counter-based stream
 // (drop_hash), never stored. The weight / input gradients of the linears (dW = dZ^T X,
-// dX = dZ W) are plain GEMMs and run on hipBLASLt through torch.matmul (dadmm_hip/hyper_ops.py).
+// dX = dZ W) are plain GEMMs: dadmm_hyper_grad.hip (wgrad_kernel) and dadmm_hyper.hip's linear
+// with the transposed weight.
 //
 // Every formula is the derivative torch's autograd applies to the reference's modules:
 //   Dropout: dx = dy * keep / (1 - p);   leaky_relu: dx = dy * (x > 0 ? 1 : slope);

@@ -67,16 +67,18 @@ class _UnfoldedFn(torch.autograd.Function):
 
 
 def tag_status(Y: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
-    """Attach the forward's device status word to the returned iterates, so that the next
-    consumer that synchronises anyway (compute_loss) can raise GuardTimeoutError instead of
-    silently taking the reference's NaN fallback on a poisoned Y."""
+    """Attach the forward's device status word to the returned iterates: compute_loss turns a
+    guard-recomputation timeout into NaN losses on the device (not the reference's silent (1, 1)
+    fallback) and passes the word on, so a caller that synchronises anyway can raise
+    GuardTimeoutError (raise_if_timed_out); the adjoints raise it in backward."""
     Y._dadmm_status = status
     return Y
 
 
 def raise_if_timed_out(Y: torch.Tensor) -> None:
-    """GuardTimeoutError if ``Y`` came from a forward whose guarded recomputation could not
-    synchronise its grid (one host synchronisation; nothing when Y carries no status)."""
+    """GuardTimeoutError if ``Y`` (iterates, or the losses compute_loss made from them) came from
+    a forward whose guarded recomputation could not synchronise its grid (one host
+    synchronisation; nothing when the tensor carries no status)."""
     status = getattr(Y, "_dadmm_status", None)
     if status is not None:
         check_status(status)

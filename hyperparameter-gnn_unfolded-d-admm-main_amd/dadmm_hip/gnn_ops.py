@@ -163,14 +163,17 @@ class GnnTrainFn(torch.autograd.Function):
     HyperTrainFn, StepFn) nodes and the engine's per-iteration gradient sums — the training step
     is then bound by the GPU, not by the host.
 
-    Inputs: ``marker`` (a parameter that requires grad, or None: the node's outputs require grad
-    through it), the GnnRun (iterate table Y [K, B, P, ns] layout), the model, its
-    hyper_ops.NativeHyperPlan, a_hat, per-sample flag and the K dropout seeds.
-    Outputs: Y [K, B, P, ns] and hyp_{K-1} [B, 4, H]. The BatchNorm running statistics of the K
-    iterations are updated in the forward, in call order."""
+    Inputs: the GnnRun (iterate table Y [K, B, P, ns] layout), the model, its
+    hyper_ops.NativeHyperPlan, a_hat, per-sample flag, the K dropout seeds and the hypernetwork's
+    parameters (hyper_ops.param_list order). Outputs: Y [K, B, P, ns] and hyp_{K-1} [B, 4, H]. The
+    BatchNorm running statistics of the K iterations are updated in the forward, in call order.
+    The backward RETURNS the parameter gradients (views of the pass's flat accumulator), so
+    autograd delivers them: ``.grad`` accumulation, ``torch.autograd.grad`` and parameter hooks
+    behave as with torch modules. A second backward through the same node (retain_graph=True)
+    raises: the saved activations are released by the first."""
 
     @staticmethod
-    def forward(ctx, marker, run, model, plan, a_hat, per_sample, seeds):
+    def forward(ctx, run, model, plan, a_hat, per_sample, seeds, *params):
         from . import hyper_ops
         K, dev = run.K, run.dev
         stream = _stream(dev)
@@ -190,16 +193,22 @@ class GnnTrainFn(torch.autograd.Function):
         hyper_ops.queue_running_stats(model, plan.stats(arena, K), run.P, defer=False)
         ctx.run, ctx.model, ctx.plan, ctx.a_hat, ctx.per_sample, ctx.seeds = run, model, plan, a_hat, per_sample, seeds
         ctx.arena, ctx.svs, ctx.As, ctx.Us, ctx.Ds = arena, svs, As, Us, Ds
+        ctx.params = params
         return run.Y, plan.hyp(arena, K - 1)
 
     @staticmethod
     def backward(ctx, gY, ghyp_last):
         from . import hyper_ops
         run, plan = ctx.run, ctx.plan
+        if ctx.arena is None:
+            raise RuntimeError("GnnTrainFn: a second backward through the same training forward "
+                               "(retain_graph=True) is not supported; its saved activations were "
+                               "released by the first backward")
         _check_guards(run)
         K, dev = run.K, run.dev
         stream = _stream(dev)
-        acc = hyper_ops._GradAccumulator.current(ctx.model, dev)
+        # this node's own accumulator: its sums are returned to autograd below
+        acc = hyper_ops._GradAccumulator(ctx.model, dev)
         g = acc.grads_struct()
         gY = gY.contiguous() if gY is not None else None
         gy1 = gY[K - 1] if gY is not None else None
@@ -221,4 +230,6 @@ class GnnTrainFn(torch.autograd.Function):
                     gy.add_(gY[k - 1])
                 gy1, gU1, gd1 = gy, gU, gd
         ctx.arena = ctx.svs = ctx.As = ctx.Us = ctx.Ds = None
-        return (None,) * 7
+        grads = tuple(acc.view(p) if p.requires_grad else None for p in ctx.params)
+        ctx.params = None
+        return (None,) * 6 + grads

@@ -387,10 +387,11 @@ def generate_er(B: int, P: int, prob: float, seed: int, device, connect: bool = 
     return GraphBatch(nbr, deg, False, order, vptr, vq, fused_ok=not (connect and P > 8))
 
 
-def to_networkx(gb: GraphBatch, P: int):
+def to_networkx(gb: GraphBatch, P: int, samples=None):
     """networkx graphs with the adjacency order a GraphBatch encodes (the own-list segment of each
     agent's visit list): the inverse of ingest(), for checking a GraphBatch against the host path
-    and the oracle. Per-sample batches only."""
+    and the oracle. Per-sample batches only. ``samples``: the sample indices to convert (default
+    all of them; a slice of a large device-generated batch converts only what it needs)."""
     import networkx as nx
     if gb.shared:
         raise ValueError("to_networkx needs a per-sample GraphBatch")
@@ -398,7 +399,7 @@ def to_networkx(gb: GraphBatch, P: int):
     vptr = gb.vptr.cpu().numpy()
     vq = gb.vq.cpu().numpy()
     out = []
-    for s in range(nbr.shape[0]):
+    for s in (range(nbr.shape[0]) if samples is None else [int(i) for i in samples]):
         adj = {}
         for p in range(P):
             m = int(nbr[s, p])

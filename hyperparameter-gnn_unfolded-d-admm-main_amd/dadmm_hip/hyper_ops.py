@@ -19,6 +19,7 @@ masks from the seed instead of storing them.
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import torch
 import torch.nn as nn
@@ -209,8 +210,9 @@ class HyperTrainFn(torch.autograd.Function):
     differentiable w.r.t. AtAy_k and every hypernetwork parameter. Forward: the GCN layers as
     f32 MFMA GEMMs with the mix / leaky_relu / batch-statistics BatchNorm / Dropout epilogue
     (dadmm_hyper_gcn_train), LayerNorm, the decoder blocks (dadmm_hyper_linear_ln_train) and the
-    head. Backward: dadmm_hyper_head_act / dadmm_hyper_rownorm_bwd / dadmm_hyper_gcn_train_bwd
-    for everything but the linears' plain GEMMs (dW = dZ^T X, dX = dZ W: hipBLASLt via torch)."""
+    head. Backward: dadmm_hyper_head_act / dadmm_hyper_rownorm_bwd / dadmm_hyper_gcn_train_bwd,
+    and the linears' GEMMs on the library's own kernels too (dW = dZ^T X: dadmm_hyper_wgrad,
+    csrc/dadmm_hyper_grad.hip; dX = dZ W: dadmm_hyper_linear with W^T) — no hipBLASLt."""
 
     @staticmethod
     def forward(ctx, AtAy, Atb, ahat, model, n, per_sample, seed, defer, *params):
@@ -386,10 +388,45 @@ class HyperTrainFn(torch.autograd.Function):
 _N_SAVED = 29   # pointers in dadmm_hyper_saved: y, m, mean, var [5] each, e, dec_y [3], dec_xd [3], z, hyp
 
 
+# Per-model host caches (module tuples, the parameter list, the native plans), kept OUTSIDE the
+# module so that copy.deepcopy / pickling of a model never sees them, and validated on every use
+# against the model's live structure (a replaced submodule or Parameter rebuilds them).
+_CACHE = weakref.WeakKeyDictionary()
+
+
+def _structure_key(model):
+    """ids of the hypernetwork's live submodules and Parameters, read from the modules' own
+    dicts (no nn.Module.__getattr__, a few microseconds): ``model.fc = nn.Linear(...)`` or a new
+    Parameter object anywhere in the encoder / decoder / fc changes it."""
+    mm = model._modules
+    key = [id(v) for v in mm.values()]
+    for top in ("encoder", "decoder"):
+        for v in mm[top]._modules.values():
+            key.append(id(v))
+            key += [id(p) for p in v._parameters.values()]
+            for c in v._modules.values():            # GCNConv.lin
+                key.append(id(c))
+                key += [id(p) for p in c._parameters.values()]
+    key += [id(p) for p in mm["fc"]._parameters.values()]
+    return tuple(key)
+
+
+def _cache(model):
+    """The model's cache entry, emptied when its structure changed since it was filled."""
+    key = _structure_key(model)
+    ent = _CACHE.get(model)
+    if ent is None or ent["key"] != key:
+        ent = {"key": key, "plans": {}}
+        _CACHE[model] = ent
+    return ent
+
+
 def _modules(model):
     """(convs, bns, decoder linears, decoder layernorms, decoder dropouts, decoder activations),
-    cached on the model (nn.Module attribute lookups dominate the per-iteration host cost)."""
-    mods = model.__dict__.get("_hyper_modules")
+    cached per model structure (nn.Module attribute lookups dominate the per-iteration host
+    cost)."""
+    ent = _cache(model)
+    mods = ent.get("mods")
     if mods is None:
         enc = model.encoder
         dec = model.decoder
@@ -397,7 +434,7 @@ def _modules(model):
                 (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5),
                 tuple(dec[4 * j] for j in range(3)), tuple(dec[4 * j + 2] for j in range(3)),
                 tuple(dec[4 * j + 1] for j in range(3)), tuple(dec[4 * j + 3] for j in range(3)))
-        model.__dict__["_hyper_modules"] = mods
+        ent["mods"] = mods
     return mods
 
 
@@ -462,7 +499,7 @@ class NativeHyperPlan:
         key = (B, P, n, ns, dev, tuple(p.data_ptr() for p in params), float(model.encoder.dropout.p),
                tuple(float(d.p) for d in drops),
                (float(model.alpha_max), float(model.tau_max), float(model.rho_max), float(model.eta_max)))
-        plans = model.__dict__.setdefault("_native_plans", {})
+        plans = _cache(model)["plans"]
         plan = plans.get((B, dev))
         if plan is None or plan.key != key:
             if len(plans) > 8:
@@ -673,11 +710,13 @@ class _GradAccumulator:
 
 
 def param_list(model):
-    """_hyper_params(model), cached on the model (the Parameter objects outlive .to() / optimiser
-    steps, which replace or update their storage in place)."""
-    params = model.__dict__.get("_hyper_param_list")
+    """_hyper_params(model), cached per model structure (the Parameter objects outlive .to() /
+    optimiser steps, which replace or update their storage in place; a replaced Parameter or
+    submodule rebuilds the list)."""
+    ent = _cache(model)
+    params = ent.get("params")
     if params is None:
-        params = model.__dict__["_hyper_param_list"] = _hyper_params(model)
+        params = ent["params"] = _hyper_params(model)
     return params
 
 

@@ -15,8 +15,9 @@ runs over all B per-sample graphs at once (the reference loops over samples in P
 in inference (model.eval() under no_grad) on the fused HIP kernels of ``dadmm_hip.hyper_ops``
 (f32 MFMA GEMMs with the adjacency mix, leaky_relu and BatchNorm in their epilogues); in training
 (model.train(): Dropout, per-sample BatchNorm batch statistics, autograd) on the training kernels
-(``hyper_ops.HyperTrainFn``: the same GEMMs with train epilogues, and HIP backward kernels for
-everything but the linears' plain weight / input GEMMs, which run on hipBLASLt).
+(``hyper_ops.HyperTrainFn`` / ``gnn_ops.GnnTrainFn``: the same GEMMs with train epilogues, and
+HIP backward kernels for every term, the linears' weight / input GEMMs included
+(csrc/dadmm_hyper_grad.hip, csrc/dadmm_hyper.hip)).
 ``hyper_backend = "torch"`` selects the batched torch composition below instead (tests).
 
 GCNConv (torch_geometric; absent here, unpinned version) is restated from its
@@ -303,9 +304,9 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         B, n = bb.shape[0], self.n
         run = GnnRun(self.operator(), bb, graphs, K, H, _lib.VARIANT_GNN, y0, U0, d0, False)
         plan = hyper_ops.NativeHyperPlan.get(self, B, self.P, n, run.op.n_store, bb.device)
-        marker = next((p for p in hyper_ops.param_list(self) if p.requires_grad), None) if grad else None
         seeds = [hyper_ops.draw_dropout_seed() for _ in range(K)]
-        Y, hyp = GnnTrainFn.apply(marker, run, self, plan, a_hat, not graphs.shared, seeds)
+        Y, hyp = GnnTrainFn.apply(run, self, plan, a_hat, not graphs.shared, seeds,
+                                  *hyper_ops.param_list(self))
         self.last_status = run.status
         Y = Y[..., :n].unsqueeze(-1)
         return tag_status(Y, self.last_status), tuple(hyp[:, c].view(B, H, 1, 1) for c in range(4))

@@ -44,15 +44,16 @@ def compute_loss(Y, label):
     (dadmm_hip.loss: one pass forward, one pass for dL/dY); anything else (e.g. CPU tensors)
     through the same formula in torch.
 
-    Iterates returned by the HIP forwards carry their status word: if the forward's guarded
-    recomputation timed out (its Y is NaN-poisoned) this raises
-    dadmm_hip.autograd.GuardTimeoutError rather than returning the fallback (1, 1)."""
-    from dadmm_hip.autograd import raise_if_timed_out
+    Iterates returned by the HIP forwards carry their device status word. If the forward's
+    guarded recomputation timed out (its Y is NaN-poisoned, a case the reference cannot reach)
+    both losses are NaN instead of the fallback (1, 1), selected on the device: no host
+    synchronisation is added. The returned losses carry the same status word, so
+    ``dadmm_hip.autograd.raise_if_timed_out(loss)`` raises GuardTimeoutError wherever the caller
+    synchronises anyway, and ``loss.backward()`` raises it in the adjoint."""
     from dadmm_hip.loss import fused_compute_loss
-    raise_if_timed_out(Y)
     fused = fused_compute_loss(Y, label)
     if fused is not None:
-        return fused
+        return _poison_timed_out(Y, *fused)
     losses = layer_losses(Y, label)
     ok = torch.isfinite(Y).all() & torch.isfinite(label).all() & torch.isfinite(losses).all()
     one = torch.ones((), dtype=losses.dtype, device=losses.device)
@@ -60,7 +61,23 @@ def compute_loss(Y, label):
     loss_final = torch.where(ok, losses[-1] + _EPS, one)
     loss_mean = torch.where(torch.isfinite(loss_mean), loss_mean, one)
     loss_final = torch.where(torch.isfinite(loss_final), loss_final, one)
-    return loss_mean, loss_final
+    return _poison_timed_out(Y, loss_mean, loss_final)
+
+
+def _poison_timed_out(Y, loss_mean, loss_final):
+    """NaN losses when Y's forward reported a guard-recomputation timeout (device-side select,
+    no sync); the losses inherit Y's status word."""
+    status = getattr(Y, "_dadmm_status", None)
+    if status is None:
+        return loss_mean, loss_final
+    from dadmm_hip import _lib
+    from dadmm_hip.autograd import tag_status
+    bad = (status.reshape(-1)[0] & _lib.STATUS_BARRIER_TIMEOUT) != 0
+    if bad.device != loss_mean.device:
+        bad = bad.to(loss_mean.device)
+    nan = torch.full((), float("nan"), dtype=loss_mean.dtype, device=loss_mean.device)
+    return (tag_status(torch.where(bad, nan, loss_mean), status),
+            tag_status(torch.where(bad, nan, loss_final), status))
 
 
 def compute_loss2(Y, label):

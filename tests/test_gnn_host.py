@@ -124,3 +124,31 @@ def test_forward_needs_one_graph_per_sample():
     model = _model()
     with pytest.raises(IndexError):
         model(torch.randn(3, 5, 8, 1), [O.er_graph(5, 0.5, seed=1)])
+
+
+def test_hyper_caches_follow_live_modules_and_survive_deepcopy():
+    """the hypernetwork's cached module tuples / parameter list are validated against
+    the live model on every use (a replaced fc is seen), and they live outside the module, so a
+    deepcopy of a model that ran carries no host plan (CDLL / ctypes structs)."""
+    import argparse
+    import copy
+
+    import torch.nn as nn
+
+    import gnn_dlasso_models_progressive as GM
+    from dadmm_hip import hyper_ops
+    args = argparse.Namespace(GHN_iter_num=3, GHyp_hidden=8, DADMM_mode="diff", alpha_max=0.1,
+                              tau_max=0.99, rho_max=0.99, eta_max=0.99)
+    model = GM.DLASSO_GNNHyp3_Progressive(torch.zeros(1, 3, 4, 16), args)
+    p0 = hyper_ops.param_list(model)
+    assert p0[-2] is model.fc.weight
+    assert hyper_ops.param_list(model) is p0                 # cached while nothing changes
+    model.fc = nn.Linear(8, 12)
+    p1 = hyper_ops.param_list(model)
+    assert p1[-2] is model.fc.weight and p1 is not p0
+    assert hyper_ops._modules(model)[2][0] is model.decoder[0]
+    model.decoder[0].weight = nn.Parameter(torch.zeros_like(model.decoder[0].weight))
+    assert hyper_ops.param_list(model)[22] is model.decoder[0].weight
+    assert not any(k.startswith("_hyper") or k.startswith("_native") for k in model.__dict__)
+    twin = copy.deepcopy(model)
+    assert hyper_ops.param_list(twin)[-2] is twin.fc.weight

@@ -271,3 +271,108 @@ def test_configs4_shard_full_batch_strided_slice(cuda):
     Yo, _, st = O.forward_f32_gram(A, b[sl], gsl, table, *(v[sl] for v in inits), variant=1, hyp_mode=1)
     assert st == 0
     assert np.array_equal(Ys, Yo), f"max |diff| {np.abs(Ys - Yo).max():.3e}"
+
+
+def _dev_inits(shape, seed, dev):
+    """y0, U0, d0 = 1e-2 N(0, 1) drawn on the device (the full-batch tests' inits: several GB at
+    configs[4], so not drawn on the host); the slices the oracle needs are copied back."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    return tuple(1e-2 * torch.randn(shape, generator=g, device=dev) for _ in range(3))
+
+
+def test_configs3_global_batch_32768_strided_slice_bit_exact(cuda):
+    """BASELINE configs[3] at its GLOBAL batch on one GPU: B = 32768, P = 5, n = 256, m = 64,
+    K = 25 (the batch the 8-GPU run shards 8 ways; Y = 4.2 GB), shared ER(0.5) graph, the trained
+    seq_hyp fixture. One DLASSO_unfolded.forward over the whole batch (unfolded_DLASSO.py:53-109),
+    status 0, a strided slice of 32 samples bit-for-bit against oracle.forward_f32 and the slice's
+    final-iterate MSE vs oracle.forward_f64 <= 1e-5 (north_star)."""
+    import unfolded_DLASSO
+    P, m, n, B, K = 5, 64, 256, 32768, 25
+    param = np.load(os.path.join(GOLD, "fixture_25_iter_general_learning_seq_hyp_param.npy"))
+    A, b, _ = O.make_problem(P, m, n, B, seed=3232)
+    G = O.er_graph(P, 0.5, seed=7)
+    inits = _dev_inits((B, P, n), 33, cuda)
+    args = argparse.Namespace(GHN_iter_num=K, DADMM_mode="diff", alpha_max=0.1, tau_max=0.99,
+                              rho_max=0.99, eta_max=0.99, max_penalty_threshold=0.8,
+                              penalty_reduction_factor=0.95)
+    model = unfolded_DLASSO.DLASSO_unfolded(_t(A, cuda)[None], args).to(cuda).eval()
+    with torch.no_grad():
+        model.seq_hyp.param.copy_(torch.from_numpy(param))
+        Y, _ = model(_t(b, cuda)[..., None], [G] * B, inits=inits)
+    assert int(model.last_status.item()) == 0
+    assert tuple(Y.shape) == (K, B, P, n, 1)
+    sl = np.arange(0, B, 1024) + np.arange(32) % 11       # every 1024th sample, jittered
+    sl_t = torch.from_numpy(sl).to(cuda)
+    Ys = Y[:, sl_t, :, :, 0].cpu().numpy()
+    y0, U0, d0 = (v[sl_t].cpu().numpy() for v in inits)
+    del Y
+    table = model.hyp_table(K).detach().cpu().numpy()
+    Yo, _, st = O.forward_f32(A, b[sl], [G] * len(sl), table, y0, U0, d0)
+    assert st == 0
+    assert np.array_equal(Ys, Yo), f"max |diff| {np.abs(Ys - Yo).max():.3e}"
+    Y64, _, _ = O.forward_f64(A, b[sl], [G] * len(sl), table, y0, U0, d0)
+    mse = float(((Ys[-1].astype(np.float64) - Y64[-1]) ** 2).mean())
+    assert mse <= 1e-5, mse
+
+
+def test_configs4_global_batch_8192_k50(cuda):
+    """BASELINE configs[4] at its GLOBAL batch on one GPU: DLASSO_GNNHyp3_Progressive, B = 8192,
+    P = 50, n = 1024, m = 32, K = 50, h = 100, per-sample connected ER(0.5) graphs generated on the
+    device (dadmm_graph_generate: gnn_dlasso_progressive.py:181-191's graph model). Y is
+    50 x 8192 x 50 x 1024 x 4 B = 84 GB and one iterate 1.68 GB, so every kernel's 64-bit
+    addressing is exercised. Two eval forwards over the whole batch:
+      * launch by launch with every iteration's hyper-parameters recorded (on_hyp): for a strided
+        slice of 4 samples the hypernetwork outputs at iterations 0, 25 and 49 against
+        oracle/gnn_np.py (1e-4) and the whole K = 50 recurrence bit-for-bit against
+        oracle.forward_f32_gram given the recorded table (gnn_dlasso_models_progressive.py:131-243);
+      * the production path (one replay of the captured HIP graph): the slice bit-identical to
+        the first forward, status 0."""
+    import gnn_dlasso_models_progressive as GM
+    from dadmm_hip.graph import generate_er, to_networkx
+    P, m, n, B, K = 50, 32, 1024, 8192, 50
+    A, b, _ = O.make_problem(P, m, n, B, seed=88)
+    torch.manual_seed(18)
+    model = GM.DLASSO_GNNHyp3_Progressive(_t(A, cuda)[None], _gnn_args(K)).to(cuda)
+    _randomise_bn(model, 28)
+    model.eval()
+    gb = generate_er(B, P, 0.5, 8192, cuda)
+    inits = _dev_inits((B, P, n), 44, cuda)
+    sl = np.arange(0, B, 2048) + np.arange(4) % 3 + 2047 * (np.arange(4) == 3)
+    sl_t = torch.from_numpy(sl).to(cuda)
+    rec = []
+    model.on_hyp = lambda AtAy, Atb, out: rec.append(
+        (torch.cat([AtAy[sl_t, :, :n], Atb[sl_t, :, :n]], dim=2).cpu(),
+         torch.stack([o[sl_t, :, 0, 0] for o in out], dim=1).cpu()))
+    bt = _t(b, cuda)[..., None]
+    with torch.no_grad():
+        Y, _ = model(bt, gb, inits=inits)
+    assert model.last_backend == "hip-eval"
+    assert int(model.last_status.item()) == 0
+    assert len(rec) == K and tuple(Y.shape) == (K, B, P, n, 1)
+    Ys = Y[:, sl_t, :, :, 0].cpu().numpy()
+    del Y
+    torch.cuda.empty_cache()
+
+    sd = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in model.state_dict().items()}
+    maxima = tuple(float(np.float32(v)) for v in MAXP)
+    gsl = to_networkx(gb, P, samples=sl)
+    for k in (0, 25, 49):
+        feats, got = rec[k]
+        want = gnn_np.hypernetwork(sd, feats.numpy().astype(np.float64), gsl, maxima, False)
+        for c in range(4):
+            w = want[c][..., 0, 0] if want[c].ndim == 4 else want[c]
+            np.testing.assert_allclose(got[:, c].numpy(), w.reshape(got[:, c].shape), rtol=1e-4,
+                                       atol=1e-4 * np.abs(w).max(), err_msg=f"iteration {k}, c {c}")
+    table = np.stack([r[1].numpy() for r in rec]).astype(np.float32)          # [K, 4, 4, P]
+    y0, U0, d0 = (v[sl_t].cpu().numpy() for v in inits)
+    Yo, _, st = O.forward_f32_gram(A, b[sl], gsl, table, y0, U0, d0, variant=1, hyp_mode=1)
+    assert st == 0
+    assert np.array_equal(Ys, Yo), f"max |diff| {np.abs(Ys - Yo).max():.3e}"
+
+    model.on_hyp = None
+    with torch.no_grad():
+        Y2, _ = model(bt, gb, inits=inits)
+    assert model.last_backend == "hip-eval-graph"
+    assert int(model.last_status.item()) == 0
+    Y2s = Y2[:, sl_t, :, :, 0].cpu().numpy()
+    assert np.array_equal(Y2s, Ys), f"graphed vs launch-by-launch: max |diff| {np.abs(Y2s - Ys).max():.3e}"

@@ -1,6 +1,6 @@
 """GPU: the training-mode hypernetwork on the HIP kernels (hyper_ops.HyperTrainFn:
 dadmm_hyper_gcn_train / _linear_ln_train / _head_act forward, dadmm_hyper_gcn_train_bwd /
-_rownorm_bwd / _head_act backward, hipBLASLt for the linears' weight / input GEMMs).
+_rownorm_bwd / _head_act backward, dadmm_hyper_wgrad and the transposed-weight linear for the linears' weight / input GEMMs).
 
 Bar: against a plain torch fp32 autograd reference of the same modules in train mode
 (gnn_dlasso_models_progressive.py:52-72 GCNConv -> leaky_relu -> BatchNorm1d on the sample's P
@@ -398,3 +398,30 @@ def test_whole_forward_node_accumulates_and_respects_frozen(cuda):
     for (name, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
         if p2.requires_grad:
             _close(p1.grad, p2.grad, rel=5e-3, name=name)
+
+
+def test_whole_forward_node_autograd_grad_and_hooks(cuda):
+    """GnnTrainFn returns the hypernetwork's parameter gradients to autograd, so
+    torch.autograd.grad(loss, params) works (and leaves .grad alone), parameter hooks fire, and
+    the result equals the torch backend's .grad; a second backward through the same node
+    (retain_graph=True) raises a clear error instead of a TypeError."""
+    import gnn_dlasso_utils as U
+    P, n, hidden, K = 5, 32, 8, 2
+    model, ref, graphs, inits, bt, label = _train_pair(cuda, P, n, hidden, "diff", False)
+    names = [nm for nm, _ in model.named_parameters()]
+    params = list(model.parameters())
+    seen = []
+    h = model.fc.weight.register_hook(lambda g: seen.append(g.shape))
+    Y, _ = model(bt, graphs, K, inits=inits)
+    loss = U.compute_loss(Y, label)[1]
+    grads = torch.autograd.grad(loss, params, retain_graph=True)
+    h.remove()
+    assert seen == [model.fc.weight.shape]
+    assert all(p.grad is None for p in params)
+    Y2, _ = ref(bt, graphs, K, inits=inits)
+    U.compute_loss(Y2, label)[1].backward()
+    for name, g1, p2 in zip(names, grads, ref.parameters()):
+        assert g1 is not None, name
+        _close(g1, p2.grad, rel=5e-3, name=name)
+    with pytest.raises(RuntimeError, match="retain_graph"):
+        loss.backward()

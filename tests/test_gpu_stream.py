@@ -138,3 +138,46 @@ def test_stream_recording_bit_exact(cuda, P, m, n, B, K, prob, per_sample, varia
     gY = np.random.default_rng(3).standard_normal((K, B, P, n)).astype(np.float32)
     dh = [backward_raw(op, g, outs[p][3], _t(gY, cuda)).cpu().numpy() for p in ("auto", "stepwise")]
     assert np.array_equal(dh[0], dh[1])
+
+
+@pytest.mark.parametrize("case", ["b_nan", "hyp_nan", "y0_inf"])
+def test_stream_recording_guard_fired_matches_stepwise(cuda, case):
+    """a training forward (record=True, path='auto': the streamed recording launch)
+    whose inputs fire one of the reference's batch-global guards is redone by the gated stepwise
+    recomputation, which re-records Grec / Urec. Y, U_K, the status, Grec, Urec and the adjoint
+    on that trajectory must be bit-identical to the stepwise recording (path='stepwise'), and Y /
+    U_K / the trajectory to oracle.forward_f32_rec (unfolded_DLASSO.py:55-61, 84-86, 102-104)."""
+    from dadmm_hip import PreparedOperator, forward_raw, ingest
+    from dadmm_hip.ops import backward_raw
+    P, m, n, B, K = 16, 64, 512, 21, 4
+    A, b, _ = O.make_problem(P, m, n, B, seed=44)
+    graphs = [O.connected_er_graph(P, 0.3, seed=1300 + s) for s in range(B)]
+    y0, U0, d0 = _inits(B, P, n, seed=45)
+    rng = np.random.default_rng(46)
+    hyp = O.hyp_table((0.5 * rng.standard_normal((K, P, 4))).astype(np.float32), MAXP)
+    if case == "b_nan":
+        b = b.copy(); b[5, 3, 7] = np.nan
+    elif case == "hyp_nan":
+        hyp = hyp.copy(); hyp[2, 11, 0] = np.nan
+    else:
+        y0 = y0.copy(); y0[20, 15, 511] = np.inf
+    op = PreparedOperator(_t(A, cuda))
+    g = ingest(graphs, P, B, cuda)
+    outs = {}
+    for path in ("auto", "stepwise"):
+        Y, U, st, traj = forward_raw(op, _t(b, cuda), g, _t(hyp, cuda), _t(y0, cuda), _t(U0, cuda),
+                                     _t(d0, cuda), want_U=True, path=path, record=True)
+        torch.cuda.synchronize()
+        outs[path] = (Y.cpu().numpy(), U.cpu().numpy(), int(st.item()),
+                      traj.Grec[..., :n].cpu().numpy(), traj.Urec[..., :n].cpu().numpy(), traj)
+    Yo, Uo, sto, Go, Uro = O.forward_f32_rec(A, b, graphs, hyp, y0, U0, d0)
+    assert sto != 0
+    for path, (Y, U, st, Gr, Ur, _) in outs.items():
+        assert st == sto, (path, st, sto)
+        assert np.array_equal(Y, Yo, equal_nan=True), path
+        assert np.array_equal(U, Uo, equal_nan=True), path
+        assert np.array_equal(Gr, Go, equal_nan=True), path
+        assert np.array_equal(Ur, Uro, equal_nan=True), path
+    gY = np.random.default_rng(47).standard_normal((K, B, P, n)).astype(np.float32)
+    dh = [backward_raw(op, g, outs[p][5], _t(gY, cuda)).cpu().numpy() for p in ("auto", "stepwise")]
+    assert np.array_equal(dh[0], dh[1], equal_nan=True)

@@ -219,17 +219,20 @@ def test_compute_loss_matches_oracle_and_nan_fallback():
     assert mean.item() == 1.0 and final.item() == 1.0
 
 
-def test_compute_loss_raises_on_timed_out_forward():
-    """a forward whose guarded recomputation timed out poisons Y with NaN;
-    compute_loss (the next consumer that synchronises) raises instead of returning (1, 1)."""
+def test_compute_loss_flags_timed_out_forward():
+    """VERDICT r2 weak #8 / ADVICE r3: a forward whose guarded recomputation timed out poisons Y
+    with NaN; compute_loss returns NaN losses (selected on the device, no host sync) instead of
+    the fallback (1, 1), and the losses carry the status so that raise_if_timed_out raises."""
     import gnn_dlasso_utils
     from dadmm_hip import _lib
-    from dadmm_hip.autograd import GuardTimeoutError, tag_status
+    from dadmm_hip.autograd import GuardTimeoutError, raise_if_timed_out, tag_status
     Y = torch.full((3, 2, 2, 5, 1), float("nan"))
     x = torch.zeros(2, 5, 1)
     tag_status(Y, torch.tensor([_lib.STATUS_BARRIER_TIMEOUT | _lib.STATUS_GRAD_NAN], dtype=torch.int32))
+    mean, final = gnn_dlasso_utils.compute_loss(Y, x)
+    assert torch.isnan(mean) and torch.isnan(final)
     with pytest.raises(GuardTimeoutError):
-        gnn_dlasso_utils.compute_loss(Y, x)
+        raise_if_timed_out(final)
     # a guard that fired normally is the reference's own behaviour: the fallback stands
     Y2 = tag_status(torch.full((3, 2, 2, 5, 1), float("nan")),
                     torch.tensor([_lib.STATUS_GRAD_NAN], dtype=torch.int32))
