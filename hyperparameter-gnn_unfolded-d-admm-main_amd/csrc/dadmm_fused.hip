@@ -64,6 +64,24 @@
 #ifndef DADMM_AGENT_SYNC
 #define DADMM_AGENT_SYNC 0
 #endif
+// LDS row padding (floats) of the y tile Ylds and the R tile Rlds. The tiles are read with
+// ds_read_b128 (GEMM1's B operand, GEMM2's R operand, the primal update): a 16-lane b128 group
+// {j = 0-3, 12-15 at h} + {j = 4-11 at h + 1} hits distinct 16-B bank slots iff the row stride is
+// 8 mod 64 floats (slot = (2 j + h) mod 16); +4 (slot = j + h) puts two lanes of every group on
+// one slot (2-way: 8 LDS cycles per read instead of 4)
+#ifndef DADMM_YS_PAD
+#define DADMM_YS_PAD 4
+#endif
+#ifndef DADMM_RS_PAD
+#define DADMM_RS_PAD 4
+#endif
+// DADMM_DUAL_B128=1: the deferred dual update reads the lane's 4 rows of a chunk of every agent as
+// one ds_read_b128 each (conflict-free with DADMM_YS_PAD 8) and updates the 4 rows back to back,
+// instead of 4 ds_read_b32 per agent (a b32 read of the same row position r by 32 lanes of
+// 16-B aligned rows touches at most 8 of the 32 banks: 4-way conflicts for any row stride)
+#ifndef DADMM_DUAL_B128
+#define DADMM_DUAL_B128 0
+#endif
 
 namespace dadmm {
 
@@ -267,8 +285,8 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     constexpr int E = T2 * 4;                        // state elements per lane per agent
     constexpr int TH = (P - HALF + AS - 1) / AS;     // GEMM1 tiles of this wave: agents HALF + AS*i
     constexpr int THA = TH > 0 ? TH : 1;             // array extent (P = 1 leaves half 1 idle)
-    constexpr int YS = NP + 4;                       // LDS row strides (floats): +16 B per row
-    constexpr int RS = MP + 4;                       //   breaks the power-of-two bank period
+    constexpr int YS = NP + DADMM_YS_PAD;            // LDS row strides (floats): the padding
+    constexpr int RS = MP + DADMM_RS_PAD;            //   breaks the power-of-two bank period
     // GEMM1 A-operand ring depth: one step in flight under the MFMAs of the current step. A
     // deeper ring for the small-state instantiations perturbs the register allocation of the
     // large ones compiled in the same module (MI355X_MICROARCH §5.4 rule 19): measured 65 VGPR
@@ -489,10 +507,10 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     for (int p = 0; p < P; ++p) et_prev[p] = 0.0f;
     // GNN variant: delta clamped to +-20 (:229); the unfolded variant: +-inf (a no-op on finite d)
     const float dlim = a.variant != 0 ? 20.0f : __builtin_inff();
-    auto dual_update_row = [&](int e, const uint32_t (&mk)[P], bool live) {
+    auto dual_update_row = [&](int e, const uint32_t (&mk)[P], bool live, const float* yrow = nullptr) {
         float yy[P][1], dd[P][1];
 #pragma unroll
-        for (int p = 0; p < P; ++p) yy[p][0] = *ylds_at(p, e);   // y_{k+1}, this lane's row e
+        for (int p = 0; p < P; ++p) yy[p][0] = yrow != nullptr ? yrow[p] : *ylds_at(p, e);   // y_{k+1}, row e
         if constexpr (GRAPH == GRAPH_SHARED)
             consensus_fma<P>(yy, dd, mf);
         else if constexpr (GRAPH == GRAPH_LANE)
@@ -586,10 +604,29 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                     for (int st = 0; st + 1 < DADMM_AT_RS && st < 4 * P; ++st) load_at_step(tring2[st], vAt, st);
                 }
 #endif
+#if DADMM_DUAL_B128
+                // chunks tt with tt * NB / T2 == t: the 4 rows of every agent in one b128 read each
+#pragma unroll
+                for (int tt = 0; tt < T2; ++tt) {
+                    if ((tt * NB) / T2 == t && has_tiles) {
+                        f32x4 yc[P];
+#pragma unroll
+                        for (int p = 0; p < P; ++p) yc[p] = *(const f32x4*)ylds_at(p, 4 * tt);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float yr[P];
+#pragma unroll
+                            for (int p = 0; p < P; ++p) yr[p] = yc[p][r];
+                            dual_update_row(4 * tt + r, mk, deferred, yr);
+                        }
+                    }
+                }
+#else
                 // rows e with e * NB / E == t
 #pragma unroll
                 for (int e = 0; e < E; ++e)
                     if ((e * NB) / E == t && has_tiles) dual_update_row(e, mk, deferred);
+#endif
             }
 #pragma unroll
             for (int i = 0; i < TH; ++i)
@@ -874,8 +911,8 @@ template <int P, int NT, int GRAPH, int WV, bool REC>
 __global__ __launch_bounds__(WV * 64) void fused_forward_kernel(FusedArgs a) {
     constexpr int NP = NT * 64;
     __shared__ __attribute__((aligned(16))) float lds[(DADMM_AT_DMA
-        ? P * BT * ((NP + 4) + (M_PAD + 4)) + WV * DADMM_AT_QD * 256
-        : P * BT * ((NP + 4) + 2 * (M_PAD + 4))) + 4];   // + the agent-sync counters
+        ? P * BT * ((NP + DADMM_YS_PAD) + (M_PAD + DADMM_RS_PAD)) + WV * DADMM_AT_QD * 256
+        : P * BT * ((NP + DADMM_YS_PAD) + 2 * (M_PAD + DADMM_RS_PAD))) + 4];   // + the agent-sync counters
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave id, in an SGPR
     if constexpr (WV == 4) {
         fused_body<P, NT, GRAPH, 4, 0, REC>(a, lds, w);
