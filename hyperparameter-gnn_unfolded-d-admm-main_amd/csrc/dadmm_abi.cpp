@@ -36,7 +36,9 @@ int check_dims(const dadmm_dims* d) {
     if (d->B < 0 || d->P < 1 || d->m < 1 || d->n < 1 || d->K < 0)
         return fail(DADMM_EINVAL, "bad dims B=%d P=%d m=%d n=%d K=%d", d->B, d->P, d->m, d->n,
                     d->K);
-    if (d->P > 64) return fail(DADMM_EINVAL, "P=%d > 64 does not fit the uint64 neighbour mask", d->P);
+    // visit lists carry uint8 agent ids; the uint64 neighbour masks (fused kernels, P <= 6) are
+    // only read for the shapes the fused kernels serve
+    if (d->P > 255) return fail(DADMM_EINVAL, "P=%d > 255 agents does not fit the uint8 visit-list ids", d->P);
     if (d->variant != DADMM_VARIANT_UNFOLDED && d->variant != DADMM_VARIANT_GNN)
         return fail(DADMM_EINVAL, "unknown variant %d", d->variant);
     if (d->hyp_rows != 1 && d->hyp_rows != d->P)
@@ -245,7 +247,7 @@ int dadmm_backward(const dadmm_dims* d, const void* op, const uint64_t* nbr,
 size_t dadmm_adjoint_scratch_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;
     const size_t state = align256(sizeof(float) * (size_t)d->B * d->P * d->n);
-    const size_t part = sizeof(float) * (size_t)dadmm::adjoint_workgroups(d->B, d->n) * d->K * d->P * 4;
+    const size_t part = sizeof(float) * (size_t)dadmm::adjoint_workgroups(d->B, d->n, d->P) * d->K * d->P * 4;
     return 3 * state + align256(part > 0 ? part : 16);
 }
 
@@ -736,7 +738,8 @@ int dadmm_hyper_gcn(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1,
                     const float* ahat, int32_t ahat_per_sample, const float* bn_mean,
                     const float* bn_var, const float* bn_weight, const float* bn_bias, float bn_eps,
                     float slope, float* y, int32_t ldy, void* stream) {
-    if (B < 0 || P < 1 || P > 64) return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d", B, P);
+    // the GCN epilogue's row tile holds whole samples: at most 160 rows
+    if (B < 0 || P < 1 || P > 160) return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d (P <= 160)", B, P);
     dadmm::HyperArgs a;
     int rc = hyper_input(B * P, K, N, x1, ld1, K1, x2, ld2, W, y, ldy, &a);
     if (rc) return rc;
@@ -832,8 +835,8 @@ int dadmm_hyper_gcn_train(int32_t B, int32_t P, int32_t K, int32_t N, const floa
                           const float* bn_bias, float bn_eps, float slope, float drop_p, uint64_t seed,
                           int32_t site, float* y, int32_t ldy, float* m_out, float* mean_out,
                           float* var_out, void* stream) {
-    if (B < 0 || P < 2 || P > 64)
-        return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d (training BatchNorm needs P >= 2)", B, P);
+    if (B < 0 || P < 2 || P > 160)
+        return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d (training BatchNorm needs P >= 2; P <= 160)", B, P);
     if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(DADMM_EINVAL, "dropout p=%g not in [0, 1)", drop_p);
     dadmm::HyperArgs a;
     int rc = hyper_input(B * P, K, N, x1, ld1, K1, x2, ld2, W, y, ldy, &a);

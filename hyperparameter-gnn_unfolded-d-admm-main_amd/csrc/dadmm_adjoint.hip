@@ -28,6 +28,11 @@ namespace adj {
 
 constexpr int THREADS = 256;   // 4 waves, one (sample, 64-column) item each
 constexpr int WAVES = 4;
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+// DADMM_ADJ_V4=1: the 16-byte-lane form of the register-resident update (adj_update_v4)
+#ifndef DADMM_ADJ_V4
+#define DADMM_ADJ_V4 1
+#endif
 
 __device__ __forceinline__ float tclamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 __device__ __forceinline__ bool inside(float x, float lo, float hi) { return x >= lo && x <= hi; }
@@ -61,7 +66,11 @@ __device__ __forceinline__ void wave_accum(float* red, int p, int c, float v, in
     if (lane == 0) red[p * 4 + c] += v;
 }
 
-__global__ __launch_bounds__(THREADS) void adj_update_kernel(AdjArgs a, int k, int items) {
+// W waves per workgroup (4; 2 or 1 for the agent counts whose per-wave LDS rows and visit lists
+// would not fit four times, P > 64)
+template <int W>
+__global__ __launch_bounds__(64 * W) void adj_update_kernel(AdjArgs a, int k, int items) {
+    constexpr int WAVES = W, THREADS = 64 * W;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int P = a.P, n = a.n, K = a.K, H = a.hyp_rows;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -368,15 +377,194 @@ __global__ __launch_bounds__(THREADS) void adj_update_reg(AdjArgs a, int k, int 
     }
 }
 
+// The register-resident iteration with 16-byte lanes (P <= PM, DADMM_ADJ_V4): lane l owns agent
+// p0 + l / 16 of the current group of four and columns 4 (l % 16) .. + 3 of the item's 64, so one
+// wave instruction moves four agents' 256-byte rows (1 KB) instead of one agent's 256 bytes, and
+// the LDS rows are read as b128 (a 16-lane group spans 16 distinct 16-byte bank slots). Every
+// element's value and operation order is adj_update_reg's; only the dhyp partial sums are
+// associated differently (each lane's 4 columns, then a 16-lane shuffle tree per agent).
+__device__ __forceinline__ f32x4v visit_sum4(const float* __restrict__ x, const int32_t* __restrict__ vp,
+                                             const uint8_t* __restrict__ vq, int p, int cq) {
+    const f32x4v xp = *(const f32x4v*)(x + p * 64 + 4 * cq);
+    f32x4v acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const int t1 = vp[p + 1];
+    for (int t = vp[p]; t < t1; ++t) {
+        const f32x4v xq = *(const f32x4v*)(x + (int)vq[t] * 64 + 4 * cq);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = acc[r] + (xp[r] - xq[r]);
+    }
+    return acc;
+}
+
+// sum of v over this lane's 4 columns and its 16-lane group -> red[p][c] (lane 16 a adds)
+__device__ __forceinline__ void group_accum(float* red, int p, int c, f32x4v v, bool live, int lane) {
+    float s = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    if ((lane & 15) == 0 && live) red[p * 4 + c] += s;
+}
+
+template <int PM>
+__global__ __launch_bounds__(THREADS) void adj_update_v4(AdjArgs a, int k, int items) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int P = a.P, n = a.n, K = a.K, H = a.hyp_rows;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ag = lane >> 4, cq = lane & 15;          // agent within the group, column quad
+    float* xs = lds + w * (2 * P * 64);
+    float* ds = xs + P * 64;
+    float* red = lds + WAVES * 2 * P * 64;
+    float* rw = red + w * P * 4;
+    int32_t* vpl = (int32_t*)(red + WAVES * P * 4) + w * (P + 1 + (2 * P * P + 3) / 4);
+    uint8_t* vql = (uint8_t*)(vpl + P + 1);
+    for (int i = lane; i < P * 4; i += 64) rw[i] = 0.0f;
+    const int item = blockIdx.x * WAVES + w;
+    const size_t S = (size_t)a.B * P * n;
+    constexpr int NG = (PM + 3) / 4;                   // agent groups
+    if (item < items) {
+        const int nch = (n + 63) / 64;
+        const int s = item / nch, c = (item % nch) * 64 + 4 * cq;
+        const bool cv = c < n;                          // n % 4 == 0: all 4 columns or none
+        const int g0 = a.graph_shared ? 0 : s * P;
+        {
+            const int v0 = a.vptr[g0], ve = a.vptr[g0 + P];
+            for (int i = lane; i <= P; i += 64) vpl[i] = a.vptr[g0 + i] - v0;
+            for (int i = lane; i < ve - v0; i += 64) vql[i] = a.vq[v0 + i];
+        }
+        float gclip, vclip;
+        clips(a.variant, k, gclip, vclip);
+        auto hyp = [&](int kk, int p, int comp) {
+            return a.hyp[((size_t)kk * H + (H == 1 ? 0 : p)) * 4 + comp];
+        };
+        auto off_of = [&](int p) { return (size_t)s * P * n + (size_t)p * n + (cv ? c : 0); };
+        const f32x4v z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+        auto ld = [&](const float* __restrict__ base, int p) {
+            return (cv && p < P) ? *(const f32x4v*)(base + off_of(p)) : z4;
+        };
+        auto st = [&](float* __restrict__ base, int p, f32x4v v) {
+            if (cv && p < P) *(f32x4v*)(base + off_of(p)) = v;
+        };
+        const float* __restrict__ y1 = a.Y + (size_t)k * S;
+        const float* __restrict__ yk = k > 0 ? a.Y + (size_t)(k - 1) * S : a.y0;
+        const float* __restrict__ gYk = a.gY + (size_t)k * S;
+        const float* __restrict__ Urk = a.Urec + (size_t)k * S;
+        const float* __restrict__ Grk = a.Grec + (size_t)k * S;
+        float* __restrict__ ybs = a.yb;
+        float* __restrict__ Ubs = a.Ub;
+        float* __restrict__ Gbs = a.Gb;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int p = 4 * g + ag;
+            if (4 * g < P && p < P) *(f32x4v*)(xs + p * 64 + 4 * cq) = ld(y1, p);
+        }
+        __builtin_amdgcn_wave_barrier();
+        f32x4v ybr[NG], ubr[NG];
+        // dual-update adjoint of iteration k (:95-99): the group's loads in flight together, then
+        // the visit sums (LDS) under them
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            ybr[g] = ubr[g] = z4;
+            if (4 * g >= P) continue;
+            const int p = 4 * g + ag;
+            const f32x4v gy = ld(gYk, p), ur = ld(Urk, p), gb = ld(Gbs, p);
+            ubr[g] = ld(Ubs, p);
+            ybr[g] = ld(ybs, p);
+            const bool pv = p < P;
+            const f32x4v d1 = pv ? visit_sum4(xs, vpl, vql, p, cq) : z4;
+            const float et = hyp(k, pv ? p : 0, 3);
+            const float rh1 = k + 1 < K ? hyp(k + 1, pv ? p : 0, 2) : 0.0f;
+            f32x4v pe = z4, db = z4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool md = a.variant == 0 || inside(d1[r], -20.0f, 20.0f);   // GNN clamp :229
+                const float dcl = a.variant == 0 ? d1[r] : tclamp(d1[r], -20.0f, 20.0f);
+                ybr[g][r] = ybr[g][r] + gy[r];                                   // + gY[k]
+                const float wv = ur[r] + dcl * et;
+                const float wb = inside(wv, -vclip, vclip) ? ubr[g][r] : 0.0f;
+                pe[r] = wb * dcl;
+                db[r] = md ? gb[r] * rh1 + wb * et : 0.0f;
+                ubr[g][r] = wb;
+            }
+            if (!cv) pe = db = z4;
+            if (pv) *(f32x4v*)(ds + p * 64 + 4 * cq) = db;
+            group_accum(rw, pv ? p : 0, 3, pe, pv, lane);
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int p = 4 * g + ag;
+            if (4 * g < P && p < P) *(f32x4v*)(xs + p * 64 + 4 * cq) = ld(yk, p);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // y_bar += 2 L d_bar; primal-update and gradient-clamp adjoint (:73-93)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            if (4 * g >= P) continue;
+            const int p = 4 * g + ag;
+            const bool pv = p < P;
+            const int pc = pv ? p : 0;
+            const f32x4v gr = ld(Grk, p);
+            f32x4v dk = k == 0 ? ld(a.d0, p) : z4;
+            const f32x4v tv = pv ? visit_sum4(ds, vpl, vql, p, cq) : z4;
+            if (k > 0 && pv) {
+                dk = visit_sum4(xs, vpl, vql, p, cq);
+                if (a.variant != 0) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dk[r] = tclamp(dk[r], -20.0f, 20.0f);
+                }
+            }
+            const float al = hyp(k, pc, 0);
+            const float dg = a.deg[g0 + pc];
+            const f32x4v y = *(const f32x4v*)(xs + pc * 64 + 4 * cq);
+            f32x4v pa = z4, pt = z4, pr = z4, ubn, zbv, grbv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float gv = tclamp(gr[r], -gclip, gclip);
+                const float z = y[r] - al * gv;
+                const float ybv = ybr[g][r] + tv[r];
+                const float zb = inside(z, -vclip, vclip) ? ybv : 0.0f;
+                pa[r] = -zb * gv;
+                const float grb = inside(gr[r], -gclip, gclip) ? -al * zb : 0.0f;
+                pt[r] = grb * sign_times(y[r], 1.0f);
+                pr[r] = grb * dk[r];
+                ubn[r] = ubr[g][r] + grb * dg;
+                zbv[r] = zb;
+                grbv[r] = grb;
+            }
+            st(Ubs, p, ubn);
+            st(ybs, p, zbv);
+            st(Gbs, p, grbv);
+            if (!cv) pa = pt = pr = z4;
+            group_accum(rw, pc, 0, pa, pv, lane);
+            group_accum(rw, pc, 1, pt, pv, lane);
+            group_accum(rw, pc, 2, pr, pv, lane);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < P * 4; i += THREADS) {
+        float v = 0.0f;
+#pragma unroll
+        for (int ww = 0; ww < WAVES; ++ww) v += red[ww * P * 4 + i];
+        a.partial[((size_t)blockIdx.x * K + k) * P * 4 + i] = v;
+    }
+}
+
 }  // namespace adj
 
-size_t adjoint_lds_bytes(int P) {
-    return 4 * ((size_t)adj::WAVES * 2 * P * 64 + (size_t)adj::WAVES * P * 4 +
-                (size_t)adj::WAVES * (P + 1 + (2 * P * P + 3) / 4));
+static size_t lds_for(int P, int W) {
+    return 4 * ((size_t)W * 2 * P * 64 + (size_t)W * P * 4 + (size_t)W * (P + 1 + (2 * P * P + 3) / 4));
 }
-int adjoint_workgroups(int B, int n) {
+// waves per workgroup of the update kernel: 4, or fewer where four waves' LDS would not fit
+int adjoint_waves(int P) {
+    if (P <= 16) return adj::WAVES;
+    for (int W = adj::WAVES; W > 1; W /= 2)
+        if (lds_for(P, W) <= 160 * 1024) return W;
+    return 1;
+}
+size_t adjoint_lds_bytes(int P) { return lds_for(P, adjoint_waves(P)); }
+int adjoint_workgroups(int B, int n, int P) {
     const long items = (long)B * ((n + 63) / 64);
-    return (int)((items + adj::WAVES - 1) / adj::WAVES);
+    const int W = adjoint_waves(P);
+    return (int)((items + W - 1) / W);
 }
 
 hipError_t launch_adjoint(const AdjArgs& a, float* dhyp, hipStream_t st) {
@@ -389,13 +577,16 @@ hipError_t launch_adjoint(const AdjArgs& a, float* dhyp, hipStream_t st) {
     const size_t lds = adjoint_lds_bytes(a.P);
     if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
     // y_bar / U_bar register-resident between the phases for P <= 16, the generic kernel above
-    auto kern = a.P <= 8 ? adj::adj_update_reg<8> : a.P <= 16 ? adj::adj_update_reg<16> : adj::adj_update_kernel;
+    const int W = adjoint_waves(a.P);
+    auto kern = a.P <= 8 ? (DADMM_ADJ_V4 ? adj::adj_update_v4<8> : adj::adj_update_reg<8>)
+              : a.P <= 16 ? (DADMM_ADJ_V4 ? adj::adj_update_v4<16> : adj::adj_update_reg<16>)
+              : W == 4 ? adj::adj_update_kernel<4> : W == 2 ? adj::adj_update_kernel<2> : adj::adj_update_kernel<1>;
     if (lds > 64 * 1024 &&
         (e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) !=
             hipSuccess)
         return e;
     const int items = a.B * ((a.n + 63) / 64);
-    const int nwg = adjoint_workgroups(a.B, a.n);
+    const int nwg = adjoint_workgroups(a.B, a.n, a.P);
     GnnArgs g{};
     g.A = a.A;
     g.At = a.At;
@@ -407,7 +598,7 @@ hipError_t launch_adjoint(const AdjArgs& a, float* dhyp, hipStream_t st) {
     g.n_pad = a.n_pad;
     g.K = a.K;
     for (int k = a.K - 1; k >= 0; --k) {
-        hipLaunchKernelGGL(kern, dim3(nwg), dim3(adj::THREADS), lds, st, a, k, items);
+        hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * W), lds, st, a, k, items);
         if ((e = gnn_launch_gram(g, k, a.Gb, a.yb, 2, st)) != hipSuccess) return e;
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;

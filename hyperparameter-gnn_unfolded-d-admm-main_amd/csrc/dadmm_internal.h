@@ -92,11 +92,12 @@ struct AdjArgs {
     float* yb;              // scratch [B][P][n]: dL/dy
     float* Ub;              // scratch [B][P][n]: dL/dU
     float* Gb;              // scratch [B][P][n]: dL/d(pre-clamp gradient) of the later iteration
-    float* partial;         // scratch [adjoint_workgroups(B, n)][K][P][4]
+    float* partial;         // scratch [adjoint_workgroups(B, n, P)][K][P][4]
     int B, P, m, m_pad, n, n_pad, K, hyp_rows, variant, graph_shared;
 };
 size_t adjoint_lds_bytes(int P);
-int adjoint_workgroups(int B, int n);
+int adjoint_workgroups(int B, int n, int P);
+int adjoint_waves(int P);
 hipError_t launch_adjoint(const AdjArgs& a, float* dhyp, hipStream_t st);
 
 // ---- GNN-model per-iteration path (dadmm_gnn.hip) -----------------------------------------------

@@ -7,8 +7,13 @@ walk of ``compute_delta`` (:127-140) with (include/dadmm.h):
     P <= 8);
   * stepwise kernel: visit lists ``vptr``/``vq`` — for each agent p the neighbour ids in the
     order compute_delta accumulates delta[p] (its own ``neighbors(p)`` loop between the visits
-    of lower and higher agents), any P <= 64;
+    of lower and higher agents), any P <= MAX_P;
   * both: ``deg[s][p] = len(neighbors(p))``.
+
+More than 64 agents (up to MAX_P = 255, the visit lists' uint8 ids) have no neighbour masks: the
+batch is described by its degrees and visit lists (a CSR form of the adjacency in the reference's
+accumulation order) plus a dense 0/1 adjacency ``adj`` [G, P, P] for the GNN model's GCN
+normalisation, and takes the non-fused kernels (the fused ones serve P <= 6).
 
 compute_delta sums each agent's own neighbour terms in ``graph.neighbors(p)`` order. For the
 graphs the reference builds with ``erdos_renyi_graph`` that order is ascending (edges are added in
@@ -32,6 +37,8 @@ import torch
 
 _SHARED_CACHE: dict = {}
 _INFO_CACHE: dict = {}
+MASK_P = 64    # agents the uint64 neighbour masks describe (the fused kernels' layout)
+MAX_P = 255    # agents the uint8 visit-list ids describe (every other kernel)
 
 
 def _info(g, P: int) -> "_GraphInfo":
@@ -51,10 +58,12 @@ def _info(g, P: int) -> "_GraphInfo":
 class _GraphInfo:
     """Host arrays of one graph on agents 0..P-1."""
 
-    __slots__ = ("mask", "deg", "order", "ascending", "vcnt", "vq")
+    __slots__ = ("mask", "deg", "order", "ascending", "vcnt", "vq", "adj")
 
     def __init__(self, adj, P: int):
-        self.mask = np.zeros(P, np.uint64)
+        wide = P > MASK_P
+        self.adj = adj
+        self.mask = np.zeros(P, np.uint64)     # (all zero for P > MASK_P: no mask layout)
         self.deg = np.zeros(P, np.float32)
         self.order = np.zeros(P, np.uint32)
         self.ascending = True
@@ -63,7 +72,8 @@ class _GraphInfo:
             for t, q in enumerate(nb):
                 if not (0 <= q < P):
                     raise ValueError(f"neighbour id {q} of agent {p}: must be an agent 0..{P - 1}")
-                self.mask[p] |= np.uint64(1) << np.uint64(q)
+                if not wide:
+                    self.mask[p] |= np.uint64(1) << np.uint64(q)
                 if t < 8:
                     self.order[p] |= np.uint32(q & 15) << np.uint32(4 * t)
             self.ascending &= all(nb[i] < nb[i + 1] for i in range(len(nb) - 1))
@@ -96,9 +106,9 @@ def _visit_lists(adj, P: int):
 class GraphBatch:
     """Device-resident graph layouts for one forward call."""
 
-    __slots__ = ("nbr", "deg", "shared", "order", "vptr", "vq", "fused_ok", "symmetric")
+    __slots__ = ("nbr", "deg", "shared", "order", "vptr", "vq", "fused_ok", "symmetric", "adj")
 
-    def __init__(self, nbr, deg, shared, order, vptr, vq, fused_ok=True, symmetric=True):
+    def __init__(self, nbr, deg, shared, order, vptr, vq, fused_ok=True, symmetric=True, adj=None):
         self.nbr = nbr      # int64 (uint64 bit patterns) [P] if shared else [B, P]
         self.deg = deg      # float32 [P] if shared else [B, P]
         self.shared = shared
@@ -112,6 +122,13 @@ class GraphBatch:
         # are. The adjoints use delta = 2 L y as its own transpose, which holds only then: they
         # refuse a batch with a directed graph (the forward follows any adjacency)
         self.symmetric = symmetric
+        # P > MASK_P: dense 0/1 adjacency uint8 [1 if shared else B, P, P] (nbr is all zero)
+        self.adj = adj
+
+    @property
+    def wide(self) -> bool:
+        """More agents than the neighbour masks describe (no fused kernels)."""
+        return self.adj is not None
 
 
 def _symmetric(masks) -> bool:
@@ -282,6 +299,38 @@ def _batch_native(graph_list, P: int, device):
                       bool(symmetric))
 
 
+def _batch_wide(graph_list, P: int, batch_size: int, device) -> GraphBatch:
+    """P > MASK_P agents: degrees, reference-order visit lists and the dense adjacency, no masks
+    (fused_ok False). One graph object repeated over the batch gives the shared layout; a single
+    graph for a larger batch keeps the reference's broadcast quirks (module docstring)."""
+    G = len(graph_list)
+    if G != batch_size and G != 1:
+        raise RuntimeError(
+            f"The size of tensor a ({batch_size}) must match the size of tensor b ({G}) at "
+            "non-singleton dimension 0")
+    g0 = graph_list[0]
+    shared = G == batch_size and sum(1 for g in graph_list if g is g0) == G
+    infos = [_info(g0, P)] if shared else [_info(g, P) for g in graph_list]
+    Gn = len(infos)
+    dense = np.zeros((Gn, P, P), np.uint8)
+    for s, i in enumerate(infos):
+        for p, nb in enumerate(i.adj):
+            dense[s, p, list(nb)] = 1
+    symmetric = bool(np.array_equal(dense, dense.transpose(0, 2, 1)))
+    vcnt = np.stack([i.vcnt for i in infos])
+    deg = np.stack([i.deg for i in infos])
+    if G == 1 and batch_size > 1:        # degrees broadcast, delta only for sample 0
+        vcnt = np.concatenate([vcnt, np.zeros((batch_size - 1, P), np.int32)])
+        deg = np.broadcast_to(deg, (batch_size, P)).copy()
+    vptr = np.zeros(vcnt.size + 1, np.int32)
+    np.cumsum(vcnt.reshape(-1), out=vptr[1:])
+    vq = _vq_nonempty(np.concatenate([i.vq for i in infos]))
+    rows = 1 if shared else deg.shape[0]
+    nbr = np.zeros((P,) if shared else (rows, P), np.int64)
+    t = _to_device([nbr, deg[0] if shared else deg, vptr, vq, dense], device)
+    return GraphBatch(t[0], t[1], shared, None, t[2], t[3], False, symmetric, t[4])
+
+
 def n_graphs(graph_list, batch_size: int) -> int:
     """len(graph_list) as the reference's forward sees it; an already ingested GraphBatch counts
     as one graph per sample."""
@@ -301,11 +350,13 @@ def ingest(graph_list, P: int, batch_size: int, device) -> GraphBatch:
         if gb.deg.device != torch.device(device):
             raise ValueError(f"GraphBatch lives on {gb.deg.device}, the forward runs on {device}")
         return gb
-    if P > 64:
-        raise ValueError(f"P={P} > 64 agents does not fit the uint64 neighbour mask")
+    if P > MAX_P:
+        raise ValueError(f"P={P} > {MAX_P} agents does not fit the uint8 visit-list ids")
     G = len(graph_list)
     if G == 0:
         raise ValueError("graph_list is empty")
+    if P > MASK_P:
+        return _batch_wide(graph_list, P, batch_size, device)
     if G != batch_size and G != 1:
         # the reference's sum_neighbors [G,P,1,1] cannot broadcast against [B,P,n,1]
         raise RuntimeError(
@@ -435,6 +486,15 @@ def from_csr(nbr_ptr, nbr_idx, deg, P: int, device) -> GraphBatch:
         if any(q < 0 or q >= P for nb in adj for q in nb):
             raise ValueError(f"neighbour ids must be agents 0..{P - 1}")
         infos.append(_GraphInfo(adj, P))
-    gb = _batch(infos, P, device)
+    if P > MASK_P:
+        class _Adj:   # the adjacency lists as a graph_list entry (neighbors(p))
+            def __init__(self, adj):
+                self._a = adj
+
+            def neighbors(self, p):
+                return iter(self._a[p])
+        gb = _batch_wide([_Adj(i.adj) for i in infos], P, B, device)
+    else:
+        gb = _batch(infos, P, device)
     gb.deg = torch.from_numpy(deg.copy()).to(device)
     return gb

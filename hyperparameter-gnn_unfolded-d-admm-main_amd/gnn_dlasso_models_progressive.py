@@ -58,13 +58,17 @@ class GCNConv(nn.Module):
         return torch.matmul(a_hat, self.lin(x)) + self.bias
 
 
-def normalized_adjacency(nbr_bits: torch.Tensor, P: int, dtype=torch.float32) -> torch.Tensor:
-    """gcn_norm of each sample's graph: [G, P] int64 neighbour masks -> [G, P, P] ``dtype``.
+def normalized_adjacency(nbr_bits: torch.Tensor, P: int, dtype=torch.float32, adj=None) -> torch.Tensor:
+    """gcn_norm of each sample's graph: [G, P] int64 neighbour masks (or, for P > 64 agents, the
+    dense 0/1 adjacency ``adj`` [G, P, P] of a wide GraphBatch) -> [G, P, P] ``dtype``.
     Self-loops are added where missing (add_remaining_self_loops, fill value 1); the degree
     counts the self-loop; both edge directions carry weight 1 (from_networkx of an nx.Graph)."""
-    q = torch.arange(P, device=nbr_bits.device, dtype=torch.int64)
-    adj = ((nbr_bits[..., :, None] >> q) & 1).to(dtype)
-    eye = torch.eye(P, device=nbr_bits.device, dtype=dtype)
+    if adj is not None:
+        adj = adj.to(dtype)
+    else:
+        q = torch.arange(P, device=nbr_bits.device, dtype=torch.int64)
+        adj = ((nbr_bits[..., :, None] >> q) & 1).to(dtype)
+    eye = torch.eye(P, device=adj.device, dtype=dtype)
     adj = torch.maximum(adj, eye)
     dinv = adj.sum(-1).rsqrt()
     return dinv[..., :, None] * adj * dinv[..., None, :]
@@ -240,8 +244,8 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         if len(b) != batch_size:
             bb = bb.expand(batch_size, -1, -1)
         graphs = ingest(graph_list, self.P, batch_size, device)
-        a_hat = normalized_adjacency(graphs.nbr, self.P)
-        if graphs.shared:
+        a_hat = normalized_adjacency(graphs.nbr, self.P, adj=graphs.adj)
+        if graphs.shared and graphs.adj is None:
             a_hat = a_hat[None]
         if inits is None:
             # torch.randn((B, P, n, 1)) * 1e-2 x 3 (:142-146), bit-identical, one launch

@@ -330,3 +330,43 @@ def test_graph_batch_symmetric_flag():
     assert not ingest([dg] + ers[:3], P, 4, "cpu").symmetric
     assert not ingest([dg] + ers[:79], P, 80, "cpu").symmetric
     assert _symmetric(np.array([0b10, 0b01], np.uint64)) and not _symmetric(np.array([0b10, 0], np.uint64))
+
+
+def test_wide_graph_ingestion_cpu():
+    """P > 64 agents (VERDICT r3 missing #1): ingest() gives degrees, the reference-order visit
+    lists (compute_delta's accumulation order, unfolded_DLASSO.py:127-140), a dense adjacency and
+    no masks; one graph repeated gives the shared layout; from_csr agrees with networkx
+    ingestion; P above the uint8 visit ids is refused."""
+    import networkx as nx
+
+    from dadmm_hip.graph import _visit_lists, from_csr, ingest
+    import oracle as O
+    P, B = 70, 3
+    graphs = [O.connected_er_graph(P, 0.1, seed=90 + s) for s in range(B)]
+    g = ingest(graphs, P, B, "cpu")
+    assert g.wide and not g.shared and not g.fused_ok and g.symmetric
+    assert tuple(g.adj.shape) == (B, P, P) and int(g.nbr.abs().sum()) == 0
+    vptr, vq = g.vptr.numpy(), g.vq.numpy()
+    for s, G in enumerate(graphs):
+        adj = [list(G.neighbors(p)) for p in range(P)]
+        cnt, lst = _visit_lists(adj, P)
+        assert np.array_equal(g.deg[s].numpy(), [len(a) for a in adj])
+        lo, hi = vptr[s * P], vptr[(s + 1) * P]
+        assert np.array_equal(vq[lo:hi], lst)
+        assert np.array_equal(np.diff(vptr[s * P:(s + 1) * P + 1]), cnt)
+        dense = np.zeros((P, P), np.uint8)
+        for p, a in enumerate(adj):
+            dense[p, a] = 1
+        assert np.array_equal(g.adj[s].numpy(), dense)
+    gs = ingest([graphs[0]] * 4, P, 4, "cpu")
+    assert gs.shared and tuple(gs.deg.shape) == (P,) and tuple(gs.adj.shape) == (1, P, P)
+    ptr, idx, deg = O.graph_arrays(graphs, P)
+    gc = from_csr(ptr, idx, deg, P, "cpu")
+    assert gc.wide and np.array_equal(gc.vptr.numpy(), vptr)
+    assert np.array_equal(gc.vq.numpy()[:vptr[-1]], vq[:vptr[-1]])
+    D = nx.DiGraph()
+    D.add_nodes_from(range(P))
+    D.add_edge(0, 69)
+    assert not ingest([D], P, 1, "cpu").symmetric
+    with pytest.raises(ValueError, match="255"):
+        ingest([nx.empty_graph(256)], 256, 1, "cpu")
