@@ -62,7 +62,7 @@ def _fwd(L, d):
 
 
 @pytest.mark.parametrize("kw,code", [
-    (dict(P=0), -1), (dict(P=65), -1), (dict(m=0), -1), (dict(n=-3), -1), (dict(K=-1), -1),
+    (dict(P=0), -1), (dict(P=256), -1), (dict(P=65, n=64, hyp_rows=1), -2), (dict(m=0), -1), (dict(n=-3), -1), (dict(K=-1), -1),
     (dict(variant=2), -1), (dict(hyp_rows=3), -1), (dict(graph_shared=2), -1),
     (dict(m=65), -2), (dict(n=258), -2), (dict(P=7, n=64, hyp_rows=1), -2),
     (dict(P=6, n=256, hyp_rows=6), -2),
@@ -193,10 +193,10 @@ def test_hyper_null_and_misaligned(L):
                                 _fk(4), 4, None) == -1
     # split input without its second pointer
     assert L.dadmm_hyper_linear(8, 8, 4, _fk(0), 4, 4, None, 4, _fk(2), None, _fk(4), 4, None) == -1
-    # GCN: P outside 1..64, missing BatchNorm statistics
+    # GCN: P outside 1..160 (the row tile holds whole samples), missing BatchNorm statistics
     args = lambda P, bn: (4, P, 8, 4, _fk(0), 8, 8, None, 0, _fk(1), _fk(2), _fk(3), 1, bn,
                           _fk(5), _fk(6), _fk(7), 1e-5, 0.01, _fk(8), 4, None)
-    assert L.dadmm_hyper_gcn(*args(65, _fk(4))) == -1
+    assert L.dadmm_hyper_gcn(*args(161, _fk(4))) == -1
     assert L.dadmm_hyper_gcn(*args(5, None)) == -1
     assert L.dadmm_hyper_head(8, 8, 0, _fk(0), 8, _fk(1), _fk(2), 0.1, 0.99, 0.99, 0.99, _fk(3),
                               None) == -1

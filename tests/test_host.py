@@ -78,7 +78,9 @@ def test_ingest_errors():
     with pytest.raises(ValueError):
         ingest([nx.path_graph(5)], 4, 1, "cpu")      # node 4 is not an agent
     with pytest.raises(ValueError):
-        ingest([G], 65, 1, "cpu")
+        ingest([G], 256, 1, "cpu")                   # past the uint8 visit-list ids
+    with pytest.raises(nx.NetworkXError):
+        ingest([G], 65, 1, "cpu")                    # the reference's graph.neighbors(4) raises too
 
 
 def test_ingest_passes_an_ingested_batch_through():
