@@ -40,6 +40,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int THREADS = 256;   // 4 waves
 constexpr int WAVES = 4;
+// gram_kernel's GEMM1 with x staged through LDS once per workgroup (m_pad <= 16 WAVES GQ_MAX)
+#ifndef DADMM_GRAM_XLDS
+#define DADMM_GRAM_XLDS 1
+#endif
+constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -121,6 +126,76 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
     const int s = tile * BT + j;
     const bool sv = s < B;
 
+#if DADMM_GRAM_XLDS
+    if (mode != 1 && MP <= 16 * WAVES * GQ_MAX) {
+        // GEMM1 with the x operand staged once per workgroup: 64-column chunks of the 16 samples'
+        // rows (4 KB) are loaded by all four waves together — lane l of wave w fetches 16 bytes of
+        // sample 4 w + l / 16, i.e. four full 256-byte row segments per wave instruction — and
+        // written to a double-buffered LDS chunk with the column quad XOR-swizzled by the sample
+        // (row sl, quad q at slot sl * 16 + (q ^ sl)), so the MFMA B-operand reads (lane (j, h),
+        // quad 4 t + h of sample j) hit 16 distinct 16-byte bank slots per b128 group. Every
+        // wave then reads x from LDS instead of loading the full x itself (the m-blocks of one
+        // (tile, agent) item share it), and an idle wave (m < 64) still helps load. The MFMA
+        // order is the loop below's (one chain per m-block, columns ascending): unchanged.
+        bool zero = false;
+        const float* xs = x_raw != nullptr ? x_raw : y_source(a, k, zero);
+        float* Xlds = lds + BT * RS;                  // [2][16][64] chunk double buffer
+        const int NC = NP / 64;
+        const uint32_t xbytes = zero ? 0u : (uint32_t)((size_t)B * P * n * 4);
+        const __amdgpu_buffer_rsrc_t rx =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), 0, (int)xbytes, 0x00020000);
+        const int sl = 4 * w + (lane >> 4);           // sample row this lane loads
+        const int qx = (lane & 15) ^ sl;              // its column quad (swizzled slot lane & 15)
+        const int sg = tile * BT + sl;
+        auto ldx = [&](int c) -> f32x4 {
+            const int col = 64 * c + 4 * qx;
+            const uint32_t off = (sg < B && col < n) ? (uint32_t)((((size_t)sg * P + p) * n + col) * 4)
+                                                     : 0x80000000u;
+            return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+        };
+        const int nq = (MP / 16 - w + WAVES - 1) / WAVES;   // this wave's m-blocks (<= GQ_MAX)
+        const int mlim = (m + 15) / 16;
+        f32x4 acc[GQ_MAX], ar[2][GQ_MAX][4];
+        const float* arow[GQ_MAX];
+#pragma unroll
+        for (int g = 0; g < GQ_MAX; ++g) {
+            acc[g] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+            arow[g] = a.A + ((size_t)p * MP + 16 * (w + WAVES * g) + j) * NP + 4 * h;
+        }
+        auto lda = [&](f32x4 (&dst)[GQ_MAX][4], int c) {
+#pragma unroll
+            for (int g = 0; g < GQ_MAX; ++g)
+                if (g < nq && w + WAVES * g < mlim) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) dst[g][t] = *(const f32x4*)(arow[g] + 64 * c + 16 * t);
+                }
+        };
+        f32x4 xr[2];
+        xr[0] = ldx(0);
+        if (NC > 1) xr[1] = ldx(1);
+        lda(ar[0], 0);
+        for (int c = 0; c < NC; ++c) {
+            float* slot = Xlds + (c & 1) * (BT * 64);
+            *(f32x4*)(slot + (sl * 16 + (lane & 15)) * 4) = xr[c & 1];
+            __syncthreads();
+            if (c + 2 < NC) xr[c & 1] = ldx(c + 2);
+            if (c + 1 < NC) lda(ar[(c + 1) & 1], c + 1);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const f32x4 bv = *(const f32x4*)(slot + (j * 16 + ((4 * t + h) ^ j)) * 4);
+#pragma unroll
+                for (int g = 0; g < GQ_MAX; ++g)
+                    if (g < nq && w + WAVES * g < mlim) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc[g] = mfma4(ar[c & 1][g][t][r], bv[r], acc[g]);
+                    }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < GQ_MAX; ++g)
+            if (g < nq) *(f32x4*)(Rlds + j * RS + 16 * (w + WAVES * g) + 4 * h) = acc[g];
+    } else
+#endif
     if (mode != 1) {
         bool zero = false;
         const float* xs = x_raw != nullptr ? x_raw : y_source(a, k, zero);
@@ -580,7 +655,7 @@ hipError_t gnn_launch_check0(const GnnArgs& a, const float* y0, hipStream_t st) 
     return hipGetLastError();
 }
 
-size_t gnn_gram_lds(int m_pad) { return 4 * (size_t)(BT * (m_pad + 4)); }
+size_t gnn_gram_lds(int m_pad) { return 4 * (size_t)(BT * (m_pad + 4) + (DADMM_GRAM_XLDS ? 2 * BT * 64 : 0)); }
 
 hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* out, int mode,
                            hipStream_t st) {
