@@ -68,12 +68,13 @@
 // ds_read_b128 (GEMM1's B operand, GEMM2's R operand, the primal update): a 16-lane b128 group
 // {j = 0-3, 12-15 at h} + {j = 4-11 at h + 1} hits distinct 16-B bank slots iff the row stride is
 // 8 mod 64 floats (slot = (2 j + h) mod 16); +4 (slot = j + h) puts two lanes of every group on
-// one slot (2-way: 8 LDS cycles per read instead of 4)
+// one slot (2-way: 8 LDS cycles per read instead of 4). Measured at H (three interleaved rounds,
+// bit-identical): +8 / +8 0.589-0.648 ms vs +4 / +4 0.604-0.606 ms (profiles/r04/variants_r04c.txt)
 #ifndef DADMM_YS_PAD
-#define DADMM_YS_PAD 4
+#define DADMM_YS_PAD 8
 #endif
 #ifndef DADMM_RS_PAD
-#define DADMM_RS_PAD 4
+#define DADMM_RS_PAD 8
 #endif
 // DADMM_DUAL_B128=1: the deferred dual update reads the lane's 4 rows of a chunk of every agent as
 // one ds_read_b128 each (conflict-free with DADMM_YS_PAD 8) and updates the 4 rows back to back,

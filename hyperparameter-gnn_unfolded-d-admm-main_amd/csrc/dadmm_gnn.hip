@@ -40,9 +40,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int THREADS = 256;   // 4 waves
 constexpr int WAVES = 4;
-// gram_kernel's GEMM1 with x staged through LDS once per workgroup (m_pad <= 16 WAVES GQ_MAX)
+// gram_kernel's GEMM1 with x staged through LDS once per workgroup (m_pad <= 16 WAVES GQ_MAX):
+// bit-identical, but measured slower (configs[2] adjoint 17.8 vs 14.8 ms, configs[4] shard forward
+// 102.8 vs 97.3 ms, profiles/r04/variants_r04c.txt: the chunk barriers serialise the waves), so off
 #ifndef DADMM_GRAM_XLDS
-#define DADMM_GRAM_XLDS 1
+#define DADMM_GRAM_XLDS 0
 #endif
 constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
 

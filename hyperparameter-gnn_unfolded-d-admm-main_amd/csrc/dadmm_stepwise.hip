@@ -38,6 +38,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int SW_THREADS = 256;   // 4 waves
 constexpr int SW_WAVES = 4;
+// per-wave LDS bytes for a sample's visit lists: the worst case 2 P^2 (a complete graph) up to
+// 4 KB; longer lists are read from global memory (P > 45 with dense graphs)
+__host__ __device__ constexpr int sw_vcap(int P) {
+    return ((2 * P * P < 4096 ? 2 * P * P : 4096) + 3) & ~3;
+}
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -222,14 +227,16 @@ __device__ void phase_update(const StepArgs& a, int k, int item, float* ylds) {
     float* yl = ylds + (threadIdx.x >> 6) * (P * 64);   // this wave's [P][64] y_next
     const int lane = threadIdx.x & 63;
     // this wave's copy of the sample's visit lists: starts [P + 1] (relative), entries (bytes)
-    int32_t* vpl = (int32_t*)(ylds + SW_WAVES * P * 64) + (threadIdx.x >> 6) * (P + 1 + (2 * P * P + 3) / 4);
+    int32_t* vpl = (int32_t*)(ylds + SW_WAVES * P * 64) + (threadIdx.x >> 6) * (P + 1 + sw_vcap(P) / 4);
     uint8_t* vql = (uint8_t*)(vpl + P + 1);
     const int g0 = a.graph_shared ? 0 : s * P;
-    {
-        const int v0 = a.vptr[g0], ve = a.vptr[g0 + P];
-        for (int i = lane; i <= P; i += 64) vpl[i] = a.vptr[g0 + i] - v0;
+    const int v0 = a.vptr[g0], ve = a.vptr[g0 + P];
+    // the sample's lists in LDS when they fit the per-wave budget (always for P <= 45; sparse
+    // graphs far beyond), else read from global memory (many agents, dense graphs)
+    const bool vl = ve - v0 <= sw_vcap(P);
+    for (int i = lane; i <= P; i += 64) vpl[i] = a.vptr[g0 + i] - v0;
+    if (vl)
         for (int i = lane; i < ve - v0; i += 64) vql[i] = a.vq[v0 + i];
-    }
 
     bool bad_y = false;
     for (int p = 0; p < P; ++p) {
@@ -255,7 +262,12 @@ __device__ void phase_update(const StepArgs& a, int k, int item, float* ylds) {
         const float yp = yl[p * 64 + lane];
         float acc = 0.0f;
         const int t1 = vpl[p + 1];
-        for (int t = vpl[p]; t < t1; ++t) acc = acc + (yp - yl[(int)vql[t] * 64 + lane]);
+        if (vl) {
+            for (int t = vpl[p]; t < t1; ++t) acc = acc + (yp - yl[(int)vql[t] * 64 + lane]);
+        } else {
+            const uint8_t* __restrict__ vg = a.vq + v0;
+            for (int t = vpl[p]; t < t1; ++t) acc = acc + (yp - yl[(int)vg[t] * 64 + lane]);
+        }
         if (a.variant != 0) acc = clamp_t(acc, -20.0f, 20.0f);             // GNN :229
         if (cv) {
             const size_t off = base + (size_t)p * n;
@@ -398,7 +410,7 @@ out:
 
 size_t grad_lds_bytes(int n_pad, int m_pad) { return 4 * (size_t)(BT * (n_pad + 4) + BT * (m_pad + 4)); }
 size_t update_lds_bytes(int P) {
-    return 4 * ((size_t)SW_WAVES * P * 64 + (size_t)SW_WAVES * (P + 1 + (2 * P * P + 3) / 4));
+    return 4 * ((size_t)SW_WAVES * P * 64 + (size_t)SW_WAVES * (P + 1 + sw_vcap(P) / 4));
 }
 
 }  // namespace

@@ -72,6 +72,14 @@ constexpr int SLOTS = 3;         // y-block ring: the block of step bs + 2 is lo
 #ifndef DADMM_ST_AUX
 #define DADMM_ST_AUX 0
 #endif
+// DADMM_ST_AT_FROM_A=1: GEMM2's A^T fragments are read from the A_pad copy (4-byte loads, four
+// 64-byte row segments per instruction) instead of the At_pad copy: the tile's GEMM1 reads the
+// same 4 KB of A, so the operator the kernel keeps in L2 halves (A_pad and At_pad are the same
+// bytes twice: 2 x 2 MB at configs[2], a whole XCD's L2): 5.85-5.90 vs 6.04-6.10 ms at configs[2],
+// bit-identical (profiles/r04/variants_r04c.txt)
+#ifndef DADMM_ST_AT_FROM_A
+#define DADMM_ST_AT_FROM_A 1
+#endif
 #define DADMM_STR_(x) #x
 #define DADMM_STR(x) DADMM_STR_(x)
 
@@ -260,9 +268,21 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
         const int pc = pin ? p : 0;
         const uint32_t vo = (k >= 0 && k < K && pin) ? vat : 0x80000000u;
         const uint32_t sb = (uint32_t)((((size_t)pc * NP + c0 + 16 * ct) * 64) * 4);
+#if DADMM_ST_AT_FROM_A
+        // lane (j, bq), m-block t: A_p rows 16 t + 4 bq + r, column c0 + 16 ct + j
+        const uint32_t voa = (k >= 0 && k < K && pin) ? (uint32_t)(((4 * bq) * NP + j) * 4) : 0x80000000u;
+        const uint32_t sba = (uint32_t)((((size_t)pc * 64) * NP + c0 + 16 * ct) * 4);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4)
+                r.at[t][r4] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                    dA, voa, sba + (uint32_t)((16 * t + r4) * NP * 4), 0));   // row step in soffset
+#else
 #pragma unroll
         for (int t = 0; t < 4; ++t)
             r.at[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dAt, vo + 64 * t, sb, 0));
+#endif
         const uint32_t off = (pin && col_ok(c0, ct)) ? (uint32_t)(elem(pc, c0, ct) * 4) : 0x80000000u;
         // U_{k-1} (k = 0: U0 itself; k = 1: U_0 = U0)
         r.u = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(

@@ -8,4 +8,5 @@ TAG=r04v1 VARS="build/var/libdadmm_f_*.so" CFG="5 256 64 4096 25 0.5 0 auto" \
 TAG=r04v2 VARS="build/var/libdadmm_adj_*.so build/var/libdadmm_gram_*.so" SCRIPT=scripts/time_adjoint.py \
   CFG="16 512 64 4096 25" ROUNDS=2 bash scripts/r04_variants.sh || exit $?
 TAG=r04v3 VARS="build/var/libdadmm_gram_*.so" SCRIPT=scripts/time_gnn.py ROUNDS=2 bash scripts/r04_variants.sh || exit $?
+TAG=r04v4 VARS="build/var/libdadmm_st_*.so" ROUNDS=3 PMC="FETCH_SIZE" bash scripts/r04_variants.sh || exit $?
 exit 0
