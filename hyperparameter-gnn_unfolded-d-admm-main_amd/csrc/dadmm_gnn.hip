@@ -47,6 +47,10 @@ constexpr int WAVES = 4;
 #define DADMM_GRAM_XLDS 0
 #endif
 constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
+// gram as one wave per (16-sample tile, agent) item, R in registers (gram_w1_kernel; m <= 128)
+#ifndef DADMM_GRAM_W1
+#define DADMM_GRAM_W1 1
+#endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -302,6 +306,110 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) at_cur[t] = at_nxt[t];
+    }
+}
+
+// ---- gram, one wave per item (DADMM_GRAM_W1): the same chains as gram_kernel with the whole item
+// in one wave. GEMM1 keeps every m-block's accumulator (MQ of them) in registers, so each x
+// column block is loaded once per item (gram_kernel's four waves each load all of x for their own
+// m-block) and no R tile goes through LDS: the MFMA accumulator layout (rows 4 h + r of m-block g,
+// sample j) is exactly GEMM2's B-operand layout. No LDS, no barriers: four independent items per
+// 256-thread workgroup. Chains and their order are gram_kernel's (bit-identical).
+template <int MQ>
+__global__ __launch_bounds__(THREADS) void gram_w1_kernel(GnnArgs a, int k, const float* x_raw, float* out,
+                                                          int mode) {
+    const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad, MP = a.m_pad;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int item = blockIdx.x * WAVES + w;
+    const int tiles = (B + BT - 1) / BT;
+    if (item >= tiles * P) return;                 // whole waves only; no barrier below
+    const int tile = item / P, p = item % P;
+    const int j = lane & 15, h = lane >> 4;
+    const int s = tile * BT + j;
+    const bool sv = s < B;
+    const int mbk = (m + 15) / 16;                 // m-blocks holding rows (<= MQ)
+    f32x4 R[MQ];
+#pragma unroll
+    for (int g = 0; g < MQ; ++g) R[g] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    if (mode != 1) {
+        bool zero = false;
+        const float* xs = x_raw != nullptr ? x_raw : y_source(a, k, zero);
+        const uint32_t xbytes = zero ? 0u : (uint32_t)((size_t)B * P * n * 4);
+        const __amdgpu_buffer_rsrc_t rx =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), 0, (int)xbytes, 0x00020000);
+        const uint32_t xoff = sv ? (uint32_t)((((size_t)s * P + p) * n + 4 * h) * 4) : 0x80000000u;
+        auto ldx = [&](int t) -> f32x4 {
+            return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rx, 16 * t + 4 * h < n && sv ? xoff + 64u * t : 0x80000000u, 0, 0));
+        };
+        const float* arow = a.A + ((size_t)p * MP + j) * NP + 4 * h;   // + 16 g NP (m-block g)
+        constexpr int GD = MQ <= 2 ? 4 : 2;        // k-steps in flight (register budget)
+        const int T = NP / 16;
+        f32x4 ar[GD][MQ], xr[GD];
+        auto lda = [&](f32x4 (&dst)[MQ], int t) {
+#pragma unroll
+            for (int g = 0; g < MQ; ++g)
+                if (g < mbk) dst[g] = *(const f32x4*)(arow + (size_t)16 * g * NP + 16 * t);
+        };
+#pragma unroll
+        for (int u = 0; u < GD; ++u) {
+            if (u < T) {
+                lda(ar[u], u);
+                xr[u] = ldx(u);
+            }
+        }
+        for (int t0 = 0; t0 < T; t0 += GD) {
+#pragma unroll
+            for (int u = 0; u < GD; ++u) {
+                const int t = t0 + u;
+                if (t < T) {
+#pragma unroll
+                    for (int g = 0; g < MQ; ++g)
+                        if (g < mbk) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) R[g] = mfma4(ar[u][g][r], xr[u][r], R[g]);
+                        }
+                    if (t + GD < T) {
+                        lda(ar[u], t + GD);
+                        xr[u] = ldx(t + GD);
+                    }
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int g = 0; g < MQ; ++g)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int mi = 16 * g + 4 * h + r;
+                R[g][r] = (sv && mi < m) ? a.b[((size_t)s * P + p) * m + mi] : 0.0f;
+            }
+    }
+    // GEMM2: out = A_p^T R over the n-tiles, one chain per tile over the m-blocks ascending; the A^T
+    // rows of tile nb + 1 load under tile nb's MFMAs
+    const float* atb = a.At + ((size_t)p * NP + j) * MP + 4 * h;
+    const int NT16 = NP / 16;
+    f32x4 at[2][MQ];
+    auto ldt = [&](f32x4 (&dst)[MQ], int nb) {
+#pragma unroll
+        for (int g = 0; g < MQ; ++g)
+            if (g < mbk) dst[g] = *(const f32x4*)(atb + (size_t)16 * nb * MP + 16 * g);
+    };
+    ldt(at[0], 0);
+    for (int nb = 0; nb < NT16; ++nb) {
+        if (nb + 1 < NT16) ldt(at[(nb + 1) & 1], nb + 1);
+        f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int g = 0; g < MQ; ++g)
+            if (g < mbk) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gc = mfma4(at[nb & 1][g][r], R[g][r], gc);
+            }
+        const int n0 = 16 * nb + 4 * h;
+        if (sv && n0 < n) {
+            f32x4* o = (f32x4*)(out + ((size_t)s * P + p) * n + n0);
+            *o = mode == 2 ? *o + gc : gc;
+        }
     }
 }
 
@@ -661,6 +769,14 @@ size_t gnn_gram_lds(int m_pad) { return 4 * (size_t)(BT * (m_pad + 4) + (DADMM_G
 
 hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* out, int mode,
                            hipStream_t st) {
+    const int mbk = (a.m + 15) / 16;
+    if (DADMM_GRAM_W1 && mbk <= 8) {
+        const int items = ((a.B + BT - 1) / BT) * a.P;
+        const int grid = (items + gnn::WAVES - 1) / gnn::WAVES;
+        auto kern = mbk <= 2 ? gnn::gram_w1_kernel<2> : mbk <= 4 ? gnn::gram_w1_kernel<4> : gnn::gram_w1_kernel<8>;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(gnn::THREADS), 0, st, a, k, x_raw, out, mode);
+        return hipGetLastError();
+    }
     const size_t lds = gnn_gram_lds(a.m_pad);
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)gnn::gram_kernel,
