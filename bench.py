@@ -489,6 +489,52 @@ def secondary(O, dev, A, b, x, G, model, P, n, m, K, B, status):
     except Exception as e:
         out["c5_error"] = repr(e)[:300]
     try:
+        # BASELINE configs[3] and configs[4] at their GLOBAL batches on this one GPU (the 8-GPU
+        # runs shard them 8 ways): configs[3] = the headline shape at B = 32768 (fused forward,
+        # Y = 4.2 GB); configs[4] = the GNN model at P=50, n=1024, m=32, K=50, B=8192 (Y = 84 GB),
+        # graphs generated on the device (dadmm_graph_generate)
+        import argparse as _ap
+
+        import gnn_dlasso_models_progressive as GM
+        import unfolded_DLASSO
+        from dadmm_hip.graph import generate_er as _gen
+        B4 = 32768
+        A4, b4, _ = O.make_problem(P, m, n, B4, seed=4444)
+        m4 = unfolded_DLASSO.DLASSO_unfolded(torch.from_numpy(A4)[None].to(dev), make_args(K)).to(dev).eval()
+        b4t = torch.from_numpy(b4)[..., None].to(dev)
+        G4 = [G] * B4
+
+        def f4():
+            with torch.no_grad():
+                m4(b4t, G4)
+        ms4 = _event_ms(f4, 5, warm=2)
+        st("c4_global_forward", m4.last_status)
+        out["c4_global_forward"] = {"B": B4, "P": P, "n": n, "m": m, "K": K, "ms": ms4,
+                                    "units_per_s": B4 * K / (ms4 * 1e-3),
+                                    "note": "BASELINE configs[3]'s whole 8-GPU batch on one GPU"}
+        del m4, b4t, G4
+        P5, n5, m5, B5, K5 = 50, 1024, 32, 8192, 50
+        A5, b5, _ = O.make_problem(P5, m5, n5, B5, seed=5555)
+        args5 = _ap.Namespace(GHN_iter_num=K5, GHyp_hidden=100, DADMM_mode="diff", alpha_max=0.1,
+                              tau_max=0.99, rho_max=0.99, eta_max=0.99)
+        g5 = GM.DLASSO_GNNHyp3_Progressive(torch.from_numpy(A5)[None].to(dev), args5).to(dev).eval()
+        gb5 = _gen(B5, P5, 0.5, 7, dev)
+        b5t = torch.from_numpy(b5)[..., None].to(dev)
+
+        def f5():
+            with torch.no_grad():
+                g5(b5t, gb5)
+        ms5 = _event_ms(f5, 1, warm=1)
+        st("c5_global_forward", g5.last_status)
+        out["c5_global_forward"] = {"B": B5, "P": P5, "n": n5, "m": m5, "K": K5, "hidden": 100,
+                                    "ms": ms5, "units_per_s": B5 * K5 / (ms5 * 1e-3),
+                                    "note": "BASELINE configs[4]'s whole 8-GPU batch on one GPU "
+                                            "(graphed eval forward, device-generated graphs)"}
+        del g5, b5t, gb5
+        torch.cuda.empty_cache()
+    except Exception as e:
+        out["global_error"] = repr(e)[:300]
+    try:
         import unfolded_DLASSO
         from dadmm_hip.ops import backward_raw as _br
         P3, n3, m3, B3, K3 = 16, 512, 64, 4096, 25
