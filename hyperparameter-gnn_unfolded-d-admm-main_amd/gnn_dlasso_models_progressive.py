@@ -260,7 +260,11 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         # training (model.train()): the HIP training-mode hypernetwork (dropout, batch statistics,
         # its backward) — HyperTrainFn
         train_hip = self.hyper_backend == "auto" and hyper_ops.supported_train(self, n)
-        self.last_backend = self._backend_name(fused, train_hip)
+        # eval mode with autograd enabled: the inference kernels forward, torch autograd through
+        # the recomputed composition backward (hyper_ops.HyperEvalFn)
+        eval_grad = (self.hyper_backend == "auto" and grad and not self.training
+                     and hyper_ops.supported(self, n))
+        self.last_backend = "hip-eval-autograd" if eval_grad else self._backend_name(fused, train_hip)
         if fused and self.use_hip_graph and self.on_hyp is None:
             # the plan owns its device state: no per-forward GnnRun (its Y, Atb, G) is built
             return self._forward_graphed(bb, graphs, a_hat.contiguous(), y0, U0, d0, K, H)
@@ -270,9 +274,9 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         Atb = run.Atb[..., :n]
         y, U, D = run.ys[0], run.U0, run.d0
         ys = []
-        if fused or train_hip:
+        if fused or train_hip or eval_grad:
             a_hat = a_hat.contiguous()
-        if fused:
+        if fused or eval_grad:
             enc = self.encoder
             bufs = hyper_ops.HyperBuffers(batch_size, self.P, enc.conv5.lin.out_features,
                                           [self.decoder[i].out_features for i in (0, 4, 8)], H,
@@ -284,6 +288,10 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
                 alpha_k, tau_k, rho_k, eta_k = hyper_ops.hypernetwork_eval(
                     self, AtAy, run.Atb, n, a_hat, not graphs.shared, bufs)
                 hyp_k = bufs.hyp
+            elif eval_grad:
+                hyp_k = hyper_ops.HyperEvalFn.apply(AtAy, run.Atb, a_hat, self, n, not graphs.shared, bufs,
+                                                    *hyper_ops.param_list(self))
+                alpha_k, tau_k, rho_k, eta_k = (hyp_k[:, c].view(batch_size, H, 1, 1) for c in range(4))
             elif train_hip:
                 hyp_k = hyper_ops.hypernetwork_train(self, AtAy, run.Atb, n, a_hat, not graphs.shared,
                                                      defer=True)
