@@ -67,6 +67,20 @@ constexpr int WAVES = 8;
 #define DADMM_BWD_AT_DMA 1
 #endif
 constexpr int BWD_QD = 5;
+// DADMM_BWD_ROT=1: the elementwise phase walks the wave's T2 row tiles in a runtime loop and
+// rotates the carried state (y_bar, U_bar) so that the current tile's rows are always columns
+// 0..3 of the register arrays (static indices), and the shared graph's consensus is the forward's
+// branch-free consensus_fma (0/1 edge multipliers in SGPRs: exactly the forward's delta, so the
+// re-evaluated masks are the forward's). The unrolled tile loop let the compiler interleave the
+// two tiles' temporaries: 256 VGPRs + 231 spilled at H; this form: 13 spilled.
+#ifndef DADMM_BWD_ROT
+#define DADMM_BWD_ROT 1
+#endif
+#if DADMM_BWD_ROT
+#define BWD_ROW(e, r) (r)
+#else
+#define BWD_ROW(e, r) (e)
+#endif
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n folded at compile time
     switch (n) {
@@ -156,6 +170,29 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
             if (has_tiles) *(f32x4*)(Glds + (p * BT + j) * YS + n0) = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
         }
     }
+    // the shared graph's edges as 0/1 multipliers (uniform), mf[a][b] = (b in N(a)); the adjoint
+    // needs an undirected graph (dadmm_backward refuses others), for which this is the forward's
+    // consensus_fma operand
+    float mf[P][P];
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int p = 0; p < P; ++p) mf[q][p] = (GRAPH == GRAPH_SHARED && ((msk[q] >> p) & 1u)) ? 1.0f : 0.0f;
+    auto cons = [&](const float (&x)[P][4], float (&o)[P][4], const uint32_t (&mk_)[P]) {
+        if constexpr (GRAPH == GRAPH_SHARED && DADMM_BWD_ROT) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float yy[P][1], dd[P][1];
+#pragma unroll
+                for (int p = 0; p < P; ++p) yy[p][0] = x[p][r];
+                consensus_fma<P>(yy, dd, mf);
+#pragma unroll
+                for (int p = 0; p < P; ++p) o[p][r] = dd[p][0];
+            }
+        } else {
+            consensus_any<P, GRAPH>(x, o, mk_, ord);
+        }
+    };
     float rh_next[P];   // rho_{k+1} (0 at k = K-1: no later iteration reads delta_K)
 #pragma unroll
     for (int p = 0; p < P; ++p) rh_next[p] = 0.0f;
@@ -210,7 +247,11 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
             const rsrc_t ruk = make_rsrc(a.Urec + (size_t)k * S, state_bytes);
             const rsrc_t rgy = make_rsrc(a.gY + (size_t)k * S, state_bytes);
             const rsrc_t rd0 = make_rsrc(a.d0, state_bytes);
+#if DADMM_BWD_ROT
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
             for (int tt = 0; tt < T2; ++tt) {
                 const int n0 = (w * T2 + tt) * 16 + 4 * h;
                 const bool ok = n0 < n;
@@ -226,7 +267,7 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 #pragma unroll
                     for (int r = 0; r < 4; ++r) t1[p][r] = v[r];
                 }
-                consensus_any<P, GRAPH>(t1, t2, mk, ord);
+                cons(t1, t2, mk);
                 const uint32_t md1 = clamp_delta(t2, a.variant);
                 fence();
                 // dual update adjoint (:98-99); t1 = d_bar
@@ -238,20 +279,20 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int e = 4 * tt + r;
-                        yb[p][e] = yb[p][e] + vg[r];                          // + gY[k]
+                        yb[p][BWD_ROW(e, r)] = yb[p][BWD_ROW(e, r)] + vg[r];  // + gY[k]
                         const float wv = vu[r] + t2[p][r] * et[p];
-                        const float wb = inside(wv, -vclip, vclip) ? Ub[p][e] : 0.0f;
+                        const float wb = inside(wv, -vclip, vclip) ? Ub[p][BWD_ROW(e, r)] : 0.0f;
                         part[p][3] += wb * t2[p][r];
                         const float db = gprev[r] * rh_next[p] + wb * et[p];
                         t1[p][r] = ((md1 >> (4 * p + r)) & 1u) ? db : 0.0f;
-                        Ub[p][e] = wb;
+                        Ub[p][BWD_ROW(e, r)] = wb;
                     }
                 }
-                consensus_any<P, GRAPH>(t1, t2, mk, ord);   // t2 = 2 L d_bar
+                cons(t1, t2, mk);   // t2 = 2 L d_bar
 #pragma unroll
                 for (int p = 0; p < P; ++p)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) yb[p][4 * tt + r] += t2[p][r];
+                    for (int r = 0; r < 4; ++r) yb[p][BWD_ROW(4 * tt + r, r)] += t2[p][r];
                 fence();
                 // t1 = y_k; t2 = delta_k (k > 0: formed from y_k as the forward did; k = 0: d0)
 #pragma unroll
@@ -261,7 +302,7 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                     for (int r = 0; r < 4; ++r) t1[p][r] = v[r];
                 }
                 if (k > 0) {
-                    consensus_any<P, GRAPH>(t1, t2, mk, ord);
+                    cons(t1, t2, mk);
                     clamp_delta(t2, a.variant);
                 } else {
 #pragma unroll
@@ -284,18 +325,34 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                         const float gr = vgr[r];
                         const float g = tclamp(gr, -gclip, gclip);
                         const float z = yk - al[p] * g;
-                        const float zb = inside(z, -vclip, vclip) ? yb[p][e] : 0.0f;
+                        const float zb = inside(z, -vclip, vclip) ? yb[p][BWD_ROW(e, r)] : 0.0f;
                         part[p][0] -= zb * g;
                         const float grb = inside(gr, -gclip, gclip) ? -al[p] * zb : 0.0f;
                         const float sg = sign_times(yk, 1.0f);
                         part[p][1] += grb * sg;
                         part[p][2] += grb * t2[p][r];
-                        Ub[p][e] = Ub[p][e] + grb * dg[p];
-                        yb[p][e] = zb;
+                        Ub[p][BWD_ROW(e, r)] = Ub[p][BWD_ROW(e, r)] + grb * dg[p];
+                        yb[p][BWD_ROW(e, r)] = zb;
                         gbv[r] = ok ? grb : 0.0f;
                     }
                     *(f32x4*)(Glds + (p * BT + j) * YS + n0) = gbv;
                 }
+#if DADMM_BWD_ROT
+                // rotate: the next tile's carried state moves to rows 0..3 (T2 rotations: identity)
+#pragma unroll
+                for (int p = 0; p < P; ++p)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float y0v = yb[p][r], u0v = Ub[p][r];
+#pragma unroll
+                        for (int t2 = 0; t2 + 1 < T2; ++t2) {
+                            yb[p][4 * t2 + r] = yb[p][4 * (t2 + 1) + r];
+                            Ub[p][4 * t2 + r] = Ub[p][4 * (t2 + 1) + r];
+                        }
+                        yb[p][4 * (T2 - 1) + r] = y0v;
+                        Ub[p][4 * (T2 - 1) + r] = u0v;
+                    }
+#endif
             }
         }
         __syncthreads();
@@ -488,7 +545,7 @@ backward_fn_ptr pick_nt(int nt, int graph) {
 backward_fn_ptr find_backward(int P, int nt, int graph) {
 #ifdef DADMM_ONLY_H   // compile-time experiments: instantiate the headline shape only
     return (P == 5 && nt == 4 && graph == GRAPH_SHARED) ? &bwd::launch<5, 4, GRAPH_SHARED> : nullptr;
-#endif
+#else
     switch (P) {
         case 1: return bwd::pick_nt<1>(nt, graph);
         case 2: return bwd::pick_nt<2>(nt, graph);
@@ -498,6 +555,7 @@ backward_fn_ptr find_backward(int P, int nt, int graph) {
         case 6: return bwd::pick_nt<6>(nt, graph);
         default: return nullptr;
     }
+#endif
 }
 
 hipError_t launch_backward_reduce(const float* partial, float* dhyp, int nwg, int K, int P, int H,
