@@ -47,9 +47,11 @@ constexpr int WAVES = 4;
 #define DADMM_GRAM_XLDS 0
 #endif
 constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
-// gram as one wave per (16-sample tile, agent) item, R in registers (gram_w1_kernel; m <= 128)
+// gram as one wave per (16-sample tile, agent) item, R in registers (gram_w1_kernel; m <= 128):
+// bit-identical, measured no faster (configs[2] adjoint 14.5-14.6 vs 14.5-14.9 ms, configs[4]
+// shard forward 97.1-97.6 vs 96.8-97.3 ms, profiles/r04/variants_r04d.txt), so off
 #ifndef DADMM_GRAM_W1
-#define DADMM_GRAM_W1 1
+#define DADMM_GRAM_W1 0
 #endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
