@@ -33,6 +33,9 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 #ifndef DADMM_ADJ_V4
 #define DADMM_ADJ_V4 1
 #endif
+#ifndef DADMM_ADJ_PF
+#define DADMM_ADJ_PF 1
+#endif
 
 __device__ __forceinline__ float tclamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 __device__ __forceinline__ bool inside(float x, float lo, float hi) { return x >= lo && x <= hi; }
@@ -456,6 +459,16 @@ __global__ __launch_bounds__(THREADS) void adj_update_v4(AdjArgs a, int k, int i
             const int p = 4 * g + ag;
             if (4 * g < P && p < P) *(f32x4v*)(xs + p * 64 + 4 * cq) = ld(y1, p);
         }
+        // DADMM_ADJ_PF: the second phase's operands (y_k rows, Grec[k]) issued now, so that phase
+        // does not start with another HBM round trip
+        f32x4v ykr[NG], grr[NG];
+        if (DADMM_ADJ_PF) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                ykr[g] = ld(yk, 4 * g + ag);
+                grr[g] = ld(Grk, 4 * g + ag);
+            }
+        }
         __builtin_amdgcn_wave_barrier();
         f32x4v ybr[NG], ubr[NG];
         // dual-update adjoint of iteration k (:95-99): the group's loads in flight together, then
@@ -492,7 +505,7 @@ __global__ __launch_bounds__(THREADS) void adj_update_v4(AdjArgs a, int k, int i
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
             const int p = 4 * g + ag;
-            if (4 * g < P && p < P) *(f32x4v*)(xs + p * 64 + 4 * cq) = ld(yk, p);
+            if (4 * g < P && p < P) *(f32x4v*)(xs + p * 64 + 4 * cq) = DADMM_ADJ_PF ? ykr[g] : ld(yk, p);
         }
         __builtin_amdgcn_wave_barrier();
         // y_bar += 2 L d_bar; primal-update and gradient-clamp adjoint (:73-93)
@@ -502,7 +515,7 @@ __global__ __launch_bounds__(THREADS) void adj_update_v4(AdjArgs a, int k, int i
             const int p = 4 * g + ag;
             const bool pv = p < P;
             const int pc = pv ? p : 0;
-            const f32x4v gr = ld(Grk, p);
+            const f32x4v gr = DADMM_ADJ_PF ? grr[g] : ld(Grk, p);
             f32x4v dk = k == 0 ? ld(a.d0, p) : z4;
             const f32x4v tv = pv ? visit_sum4(ds, vpl, vql, p, cq) : z4;
             if (k > 0 && pv) {

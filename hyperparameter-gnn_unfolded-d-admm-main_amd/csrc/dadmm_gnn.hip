@@ -53,6 +53,10 @@ constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
 #ifndef DADMM_GRAM_W1
 #define DADMM_GRAM_W1 0
 #endif
+// gram_kernel mode 2: the out rows prefetched one GEMM2 unit ahead
+#ifndef DADMM_GRAM_OPF
+#define DADMM_GRAM_OPF 1
+#endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -279,9 +283,22 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
     const int units = (NP / 16 - w + WAVES - 1) / WAVES * MG;
     if (units > 0) load_at(at_cur, 0);
     f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
+    // mode 2 (out += ...): the out rows of the unit that completes a tile are loaded one unit
+    // ahead (a load issued just before its add left the HBM latency exposed once per tile)
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        out, 0, (mode == 2 && DADMM_GRAM_OPF) ? (int)((size_t)B * P * n * 4) : 0, 0x00020000);
+    auto ldo = [&](int u) -> f32x4 {
+        const int nb = w + WAVES * (u / MG), mg = u % MG, n0 = 16 * nb + 4 * h;
+        const uint32_t off = (mg == MG - 1 && sv && n0 < n) ? (uint32_t)((((size_t)s * P + p) * n + n0) * 4)
+                                                           : 0x80000000u;
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ro, off, 0, 0));
+    };
+    f32x4 ocur = {0.0f, 0.0f, 0.0f, 0.0f}, onxt = ocur;
+    if (DADMM_GRAM_OPF && mode == 2 && units > 0) ocur = ldo(0);
     for (int u = 0; u < units; ++u) {
         const int nb = w + WAVES * (u / MG), mg = u % MG;
         if (u + 1 < units) load_at(at_nxt, u + 1);
+        if (DADMM_GRAM_OPF && mode == 2 && u + 1 < units) onxt = ldo(u + 1);
         if (mg == 0) {
             gc = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -304,8 +321,9 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
         const int n0 = 16 * nb + 4 * h;
         if (mg == MG - 1 && sv && n0 < n) {
             f32x4* o = (f32x4*)(out + ((size_t)s * P + p) * n + n0);
-            *o = mode == 2 ? *o + gc : gc;
+            *o = mode == 2 ? (DADMM_GRAM_OPF ? ocur : *o) + gc : gc;
         }
+        ocur = onxt;
 #pragma unroll
         for (int t = 0; t < 4; ++t) at_cur[t] = at_nxt[t];
     }
