@@ -19,7 +19,8 @@
  * Layouts (B batch, P agents, m rows per agent, n signal dim, K unrolled iterations):
  *   A      [P][m][n]        per-agent sensing matrices (reference A[0], shape [1,P,m,n])
  *   b      [B][P][m]        measurements              (reference b,    shape [B,P,m,1])
- *   nbr    [B][P] uint64    bit q of nbr[s][p] set <=> q in graph_list[s].neighbors(p)  (P <= 64);
+ *   nbr    [B][P] uint64    bit q of nbr[s][p] set <=> q in graph_list[s].neighbors(p)  (P <= 64;
+ *                           read only by the fused kernels: any valid pointer past 64 agents);
  *                           neighbours are visited in ascending order (networkx order for
  *                           erdos_renyi_graph); [P] when dims.graph_shared
  *   nbr_order [B][P] uint32 (nullable) graph.neighbors(p) in adjacency order, 4 bits per id,
@@ -40,8 +41,11 @@
  * Compiled configurations of dadmm_forward (fused): P <= 6 (P <= 5 at n > 128), m <= 64,
  * n <= 256, n % 4 == 0 (callers zero-pad n otherwise: zero columns of A are inert),
  * B*P*n*4 < 2^31. Anything else returns DADMM_EUNSUPPORTED; dadmm_forward_tiled covers
- * P <= 64, m <= 128, and dadmm_forward_stepwise every P <= 64, m <= 1024, n % 4 == 0
+ * P <= 255, m <= 128, and dadmm_forward_stepwise every P <= 140, m <= 1024, n % 4 == 0
  * (the reference's defaults m = 100, n = 500, configurations.py:6-9, run on the tiled path).
+ * Agents are limited by the visit lists' uint8 ids (255) and by the kernels' per-wave LDS rows
+ * (the stepwise update: 4 waves x P x 64 floats; longer visit lists than 4 KB per wave are walked
+ * from global memory): a shape whose LDS would not fit returns an error instead of launching.
  */
 #ifndef DADMM_H_
 #define DADMM_H_
@@ -256,7 +260,8 @@ int dadmm_graph_generate(int32_t B, int32_t P, float prob, uint64_t seed, int32_
 /* Bytes of device scratch dadmm_adjoint needs for `d` (256-byte aligned pointer). */
 size_t dadmm_adjoint_scratch_bytes(const dadmm_dims* d);
 
-/* The same adjoint as dadmm_backward for EVERY shape (P <= 64, m <= 1024, n % 4 == 0): the state
+/* The same adjoint as dadmm_backward for EVERY shape (P <= 255 within the LDS budget: 4, 2 or 1
+ * waves per workgroup by agent count; m <= 1024, n % 4 == 0): the state
  * (dL/dy, dL/dU, the later iteration's gradient adjoint) lives in `scratch`, two launches per
  * reverse iteration (elementwise + consensus adjoint per (sample, 64 columns); the forward's
  * factored Gram pair for A^T A gr_bar). Takes the stepwise path's visit lists (the reference's
@@ -285,8 +290,8 @@ int dadmm_adjoint(const dadmm_dims* d, const void* op, const int32_t* visit_ptr,
  * guards are the reference's batch-global NaN/Inf resets (:150-156, :216-218, :235-237), decided
  * on the device through `flags` (dadmm_gnn_flag_bytes(K) bytes): no host synchronisation.
  * Graph operands are the stepwise path's visit lists and degrees; H = dims.hyp_rows (P for
- * 'diff', 1 for 'same'); dims.variant selects the clamps (1 for this model). Shapes: P <= 64,
- * m <= 1024, n % 4 == 0. */
+ * 'diff', 1 for 'same'); dims.variant selects the clamps (1 for this model). Shapes: P <= 255
+ * (the step kernel stages P x 128 floats per workgroup), m <= 1024, n % 4 == 0. */
 size_t dadmm_gnn_flag_bytes(int32_t K);
 int dadmm_gnn_begin(const dadmm_dims* d, const void* op, const float* b, const float* y0,
                     const float* U0, float* Atb, int32_t* flags, void* stream);
