@@ -8,7 +8,7 @@ TAG=${TAG:-prof}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline"
+BENCH="bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline ${BENCH_EXTRA:-}"
 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- \
     python3 $BENCH > "$OUT/bench_kt.json" 2> "$OUT/kt.err"
 rc=$?; echo "kernel-trace rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$OUT/kt.err"; exit $rc; }
