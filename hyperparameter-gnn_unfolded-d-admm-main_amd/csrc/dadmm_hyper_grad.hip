@@ -52,7 +52,8 @@ __global__ __launch_bounds__(64 * WV) void wgrad_kernel(WgradArgs a) {
     const int tl = xcd_tile(blockIdx.x, gridDim.x);
     const int kt = tl % gk, nt = (tl / gk) % gn, split = tl / (gk * gn);
     const int n0 = nt * TN, k0 = kt * TK;
-    const int steps = (a.R + 3) / 4;
+    const int sb = (a.R + 3) / 4;                  // row steps per batch block
+    const int steps = sb * a.nb;
     const int per = (steps + a.splits - 1) / a.splits;
     const int s_begin = split * per;
     const int s_end = s_begin + per < steps ? s_begin + per : steps;
@@ -61,12 +62,14 @@ __global__ __launch_bounds__(64 * WV) void wgrad_kernel(WgradArgs a) {
     int nc[2];
     const float* xs[2];
     int ldx[2];
+    bool k_lo[2];   // column from x1 (else x2)
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
         int n = n0 + 16 * b + i;
         nc[b] = n < a.N ? n : a.N - 1;
         int k = k0 + 16 * b + i;
         k = k < a.K ? k : a.K - 1;
+        k_lo[b] = k < a.K1;
         if (k < a.K1) {
             xs[b] = a.x1 + k;
             ldx[b] = a.ld1;
@@ -85,12 +88,13 @@ __global__ __launch_bounds__(64 * WV) void wgrad_kernel(WgradArgs a) {
     // wave w: steps s_begin + w, + WV, ...
     float ra[RING][2], rb[RING][2];
     auto load = [&](int u, int st) {
-        const int r = 4 * st + h;
+        const int bb = a.nb > 1 ? st / sb : 0;
+        const int r = 4 * (st - bb * sb) + h;
         const bool ok = st < s_end && r < a.R;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            ra[u][b] = ok ? a.dz[(size_t)r * a.ldz + nc[b]] : 0.0f;
-            rb[u][b] = ok ? xs[b][(size_t)r * ldx[b]] : 0.0f;
+            ra[u][b] = ok ? a.dz[(size_t)bb * a.zs + (size_t)r * a.ldz + nc[b]] : 0.0f;
+            rb[u][b] = ok ? xs[b][(size_t)bb * (k_lo[b] ? a.s1 : a.s2) + (size_t)r * ldx[b]] : 0.0f;
         }
     };
     const int first = s_begin + w;
@@ -195,23 +199,26 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(const float* __restrict
 // adds the 16 slice sums in slice order through LDS — a fixed order, deterministic run to run.
 constexpr int CS_C = 16, CS_S = THREADS / CS_C;
 __global__ __launch_bounds__(THREADS) void colsum_kernel(const float* __restrict__ part, int G, int R, int C,
-                                                         float* __restrict__ out, int beta) {
+                                                         float* __restrict__ out, int beta, int nb,
+                                                         size_t pstride) {
     __shared__ float red[CS_S][CS_C + 1];
     const int cb = (C + CS_C - 1) / CS_C;
     const int g = blockIdx.x / cb, c0 = (blockIdx.x % cb) * CS_C;
     const int cl = threadIdx.x % CS_C, sl = threadIdx.x / CS_C;
     const int c = c0 + cl < C ? c0 + cl : C - 1;
-    const float* p = part + (size_t)g * R * C + c;
     float s = 0.0f;
-    int r = sl;
-    for (; r + 7 * CS_S < R; r += 8 * CS_S) {
-        float v[8];
+    for (int bb = 0; bb < nb; ++bb) {   // batch blocks (deferred training gradients), in order
+        const float* p = part + (size_t)bb * pstride + (size_t)g * R * C + c;
+        int r = sl;
+        for (; r + 7 * CS_S < R; r += 8 * CS_S) {
+            float v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(r + u * CS_S) * C];
+            for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(r + u * CS_S) * C];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s += v[u];
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; r < R; r += CS_S) s += p[(size_t)r * C];
     }
-    for (; r < R; r += CS_S) s += p[(size_t)r * C];
     red[sl][cl] = s;
     __syncthreads();
     if (sl == 0 && c0 + cl < C) {
@@ -285,9 +292,11 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_colsum(const float* part, int G, int R, int C, float* out, int beta, hipStream_t st) {
+hipError_t launch_colsum(const float* part, int G, int R, int C, float* out, int beta, hipStream_t st, int nb,
+                         size_t pstride) {
     const int blocks = G * ((C + hgrad::CS_C - 1) / hgrad::CS_C);
-    hipLaunchKernelGGL(hgrad::colsum_kernel, dim3(blocks), dim3(hgrad::THREADS), 0, st, part, G, R, C, out, beta);
+    hipLaunchKernelGGL(hgrad::colsum_kernel, dim3(blocks), dim3(hgrad::THREADS), 0, st, part, G, R, C, out, beta,
+                       nb, pstride);
     return hipGetLastError();
 }
 

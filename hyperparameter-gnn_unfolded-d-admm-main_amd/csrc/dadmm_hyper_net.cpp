@@ -99,6 +99,37 @@ int check_net(const dadmm_hyper_net* net, int B) {
     return DADMM_OK;
 }
 
+// Deferred parameter gradients (dadmm_hyper_train_backward_deferred / dadmm_hyper_train_wgrad):
+// the per-iteration gradient operands in one block of `dsave`, floats, 4-aligned slices
+struct DSave {
+    float* dz;          // [B][4H] head gradient (fc's dZ)
+    float* dv[3];       // [B][dec_width_j] decoder blocks' dZ
+    float* pdec[3];     // decoder LayerNorm partials (dadmm_hyper_rownorm_bwd_part_bytes)
+    float* pnorm;       // encoder LayerNorm partials
+    float* dZ[5];       // [B P][width_i] GCN layers' dZ
+    float* pgcn[5];     // [3][B][width_i] GCN BatchNorm / bias partials
+};
+inline size_t up4(size_t f) { return (f + 3) & ~(size_t)3; }
+size_t dsave_layout(const dadmm_hyper_net* net, int B, DSave* d, float* base) {
+    const int P = net->P, rows = B * P;
+    size_t off = 0;
+    auto take = [&](float** slot, size_t floats) {
+        if (base) *slot = base + off;
+        off += up4(floats);
+    };
+    take(&d->dz, (size_t)B * 4 * net->H);
+    for (int j = 0; j < 3; ++j) {
+        take(&d->dv[j], (size_t)B * net->dec_width[j]);
+        take(&d->pdec[j], dadmm_hyper_rownorm_bwd_part_bytes(B, net->dec_width[j]) / 4);
+    }
+    take(&d->pnorm, dadmm_hyper_rownorm_bwd_part_bytes(rows, net->width[4]) / 4);
+    for (int i = 0; i < 5; ++i) {
+        take(&d->dZ[i], (size_t)rows * net->width[i]);
+        take(&d->pgcn[i], (size_t)3 * B * net->width[i]);
+    }
+    return off;
+}
+
 #define TRY(call)                       \
     do {                                \
         const int rc_ = (call);         \
@@ -161,70 +192,166 @@ int dadmm_hyper_train_forward(const dadmm_hyper_net* net, int32_t B, const float
     return DADMM_OK;
 }
 
-int dadmm_hyper_train_backward(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
-                               const float* ahat, int32_t ahat_per_sample, uint64_t seed,
-                               const dadmm_hyper_saved* sv, const float* dhyp, const dadmm_hyper_grads* g,
-                               float* dAtAy, void* work, void* stream) {
+static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
+                          const float* ahat, int32_t ahat_per_sample, uint64_t seed, const dadmm_hyper_saved* sv,
+                          const float* dhyp, const dadmm_hyper_grads* g, float* dAtAy, void* work, float* dsave,
+                          void* stream) {
     if (check_net(net, B) != DADMM_OK || !sv || !dhyp || !g || !dAtAy || !work) return DADMM_EINVAL;
     if (B == 0) return DADMM_OK;
     Work w;
     layout(net, B, &w, (char*)work);
+    // dsave: the gradient operands go to the iteration's block and the parameter-gradient GEMMs /
+    // sums are left to dadmm_hyper_train_wgrad (one batched launch per parameter for all iterations)
+    DSave d;
+    const bool defer = dsave != nullptr;
+    if (defer) dsave_layout(net, B, &d, dsave);
     const int P = net->P, n = net->n, rows = B * P, H4 = 4 * net->H;
     if (n & 15) return DADMM_EUNSUPPORTED;
+    float* dzh = defer ? d.dz : w.dz;
     // head (sigmoid, clamps, maxima) -> d logits
     TRY(dadmm_hyper_head_act(1, B, net->H, sv->z, dhyp, net->maxv[0], net->maxv[1], net->maxv[2],
-                             net->maxv[3], w.dz, stream));
+                             net->maxv[3], dzh, stream));
     // fc: dW, db; dx = dz fc
     const int hid = net->dec_width[2];
-    TRY(dadmm_hyper_wgrad(B, H4, hid, w.dz, H4, sv->dec_y[2], hid, hid, nullptr, 0, g->fc_w, g->fc_b, 1, w.wscr,
-                          stream));
+    if (!defer)
+        TRY(dadmm_hyper_wgrad(B, H4, hid, dzh, H4, sv->dec_y[2], hid, hid, nullptr, 0, g->fc_w, g->fc_b, 1, w.wscr,
+                              stream));
     float* dx = w.dx[0];
-    TRY(dadmm_hyper_linear(B, H4, hid, w.dz, H4, H4, nullptr, 0, g->fc_wt, nullptr, dx, hid, stream));
+    TRY(dadmm_hyper_linear(B, H4, hid, dzh, H4, H4, nullptr, 0, g->fc_wt, nullptr, dx, hid, stream));
     // decoder blocks, last to first
     for (int j = 2; j >= 0; --j) {
         const int N = net->dec_width[j];
         const int Kin = j > 0 ? net->dec_width[j - 1] : P * net->width[4];
         const float* xin = j > 0 ? sv->dec_y[j - 1] : sv->e;
+        float* dv = defer ? d.dv[j] : w.dv;
+        float* part = defer ? d.pdec[j] : w.part;
         TRY(dadmm_hyper_rownorm_bwd(B, N, dx, sv->dec_xd[j], net->ln_w[j], net->ln_b[j], net->ln_eps[j], 1,
-                                    net->dec_slope[j], net->dec_drop[j], seed, 4 + j, w.dv, w.part, stream));
-        const int nblk = (int)(dadmm_hyper_rownorm_bwd_part_bytes(B, N) / (4 * 2 * (size_t)N));
-        TRY(dadmm_hyper_colsum(w.part, 1, nblk, 2 * N, g->ln_wb[j], 1, stream));
-        TRY(dadmm_hyper_wgrad(B, N, Kin, w.dv, N, xin, Kin, Kin, nullptr, 0, g->dec_w[j], g->dec_b[j], 1, w.wscr,
-                              stream));
+                                    net->dec_slope[j], net->dec_drop[j], seed, 4 + j, dv, part, stream));
+        if (!defer) {
+            const int nblk = (int)(dadmm_hyper_rownorm_bwd_part_bytes(B, N) / (4 * 2 * (size_t)N));
+            TRY(dadmm_hyper_colsum(part, 1, nblk, 2 * N, g->ln_wb[j], 1, stream));
+            TRY(dadmm_hyper_wgrad(B, N, Kin, dv, N, xin, Kin, Kin, nullptr, 0, g->dec_w[j], g->dec_b[j], 1, w.wscr,
+                                  stream));
+        }
         float* nx = dx == w.dx[0] ? w.dx[1] : w.dx[0];
-        TRY(dadmm_hyper_linear(B, N, Kin, w.dv, N, N, nullptr, 0, g->dec_wt[j], nullptr, nx, Kin, stream));
+        TRY(dadmm_hyper_linear(B, N, Kin, dv, N, N, nullptr, 0, g->dec_wt[j], nullptr, nx, Kin, stream));
         dx = nx;
     }
     // self.norm backward (no dropout, no activation): dx [B][P 4h] = [rows][4h]
     const int C = net->width[4];
     {
         float* nx = dx == w.dx[0] ? w.dx[1] : w.dx[0];
+        float* part = defer ? d.pnorm : w.part;
         TRY(dadmm_hyper_rownorm_bwd(rows, C, dx, sv->y[4], net->norm_w, net->norm_b, net->norm_eps, 0, 0.0f, 0.0f,
-                                    seed, 99, nx, w.part, stream));
-        const int nblk = (int)(dadmm_hyper_rownorm_bwd_part_bytes(rows, C) / (4 * 2 * (size_t)C));
-        TRY(dadmm_hyper_colsum(w.part, 1, nblk, 2 * C, g->norm_wb, 1, stream));
+                                    seed, 99, nx, part, stream));
+        if (!defer) {
+            const int nblk = (int)(dadmm_hyper_rownorm_bwd_part_bytes(rows, C) / (4 * 2 * (size_t)C));
+            TRY(dadmm_hyper_colsum(part, 1, nblk, 2 * C, g->norm_wb, 1, stream));
+        }
         dx = nx;
     }
     // GCN layers, last to first: dZ (gcn backward), [dgamma, dbeta, dbias], dW, dX
     for (int i = 4; i >= 0; --i) {
         const int N = net->width[i];
-        float* dZ = dx == w.dx[0] ? w.dx[1] : w.dx[0];
+        float* dZ = defer ? d.dZ[i] : (dx == w.dx[0] ? w.dx[1] : w.dx[0]);
+        float* part = defer ? d.pgcn[i] : w.part;
         TRY(dadmm_hyper_gcn_train_bwd(B, P, N, dx, sv->m[i], sv->mean[i], sv->var[i], net->bn_w[i],
                                       net->bn_eps[i], ahat, ahat_per_sample, LEAKY, i < 4 ? net->drop_enc : 0.0f,
-                                      seed, i, dZ, w.part, stream));
-        TRY(dadmm_hyper_colsum(w.part, 3, B, N, g->bn_wbc[i], 1, stream));
+                                      seed, i, dZ, part, stream));
+        if (!defer) TRY(dadmm_hyper_colsum(part, 3, B, N, g->bn_wbc[i], 1, stream));
         if (i > 0) {
             const int Kin = net->width[i - 1];
-            TRY(dadmm_hyper_wgrad(rows, N, Kin, dZ, N, sv->y[i - 1], Kin, Kin, nullptr, 0, g->conv_w[i], nullptr,
-                                  1, w.wscr, stream));
+            if (!defer)
+                TRY(dadmm_hyper_wgrad(rows, N, Kin, dZ, N, sv->y[i - 1], Kin, Kin, nullptr, 0, g->conv_w[i],
+                                      nullptr, 1, w.wscr, stream));
             // dX into the buffer dx held (gcn backward consumed it)
             TRY(dadmm_hyper_linear(rows, N, Kin, dZ, N, N, nullptr, 0, g->conv_wt[i], nullptr, dx, Kin, stream));
         } else {
             // layer 1's input cat(AtAy, Atb); only d AtAy (its first n columns) flows back
-            TRY(dadmm_hyper_wgrad(rows, N, 2 * n, dZ, N, AtAy, net->ld, n, Atb, net->ld, g->conv_w[0], nullptr,
-                                  1, w.wscr, stream));
+            if (!defer)
+                TRY(dadmm_hyper_wgrad(rows, N, 2 * n, dZ, N, AtAy, net->ld, n, Atb, net->ld, g->conv_w[0], nullptr,
+                                      1, w.wscr, stream));
             TRY(dadmm_hyper_linear(rows, N, n, dZ, N, N, nullptr, 0, g->conv_wt[0], nullptr, dAtAy, net->ld,
                                    stream));
+        }
+    }
+    return DADMM_OK;
+}
+
+int dadmm_hyper_train_backward(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
+                               const float* ahat, int32_t ahat_per_sample, uint64_t seed,
+                               const dadmm_hyper_saved* sv, const float* dhyp, const dadmm_hyper_grads* g,
+                               float* dAtAy, void* work, void* stream) {
+    return train_backward(net, B, AtAy, Atb, ahat, ahat_per_sample, seed, sv, dhyp, g, dAtAy, work, nullptr,
+                          stream);
+}
+
+size_t dadmm_hyper_train_dsave_floats(const dadmm_hyper_net* net, int32_t B) {
+    if (check_net(net, B) != DADMM_OK) return 0;
+    DSave d;
+    return dsave_layout(net, B, &d, nullptr);
+}
+
+int dadmm_hyper_train_backward_deferred(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
+                                        const float* ahat, int32_t ahat_per_sample, uint64_t seed,
+                                        const dadmm_hyper_saved* sv, const float* dhyp, const dadmm_hyper_grads* g,
+                                        float* dAtAy, void* work, float* dsave, void* stream) {
+    if (!dsave || ((uintptr_t)dsave & 15)) return DADMM_EINVAL;
+    return train_backward(net, B, AtAy, Atb, ahat, ahat_per_sample, seed, sv, dhyp, g, dAtAy, work, dsave,
+                          stream);
+}
+
+int dadmm_hyper_train_wgrad(const dadmm_hyper_net* net, int32_t B, int32_t iters, const float* AtAy,
+                            int64_t atay_stride, const float* Atb, const dadmm_hyper_saved* sv0, int64_t sv_stride,
+                            const float* dsave, int64_t dsave_stride, const dadmm_hyper_grads* g, void* stream) {
+    if (check_net(net, B) != DADMM_OK || iters < 0 || !AtAy || !Atb || !sv0 || !dsave || !g) return DADMM_EINVAL;
+    if (B == 0 || iters == 0) return DADMM_OK;
+    if (net->n & 15) return DADMM_EUNSUPPORTED;
+    DSave d;
+    dsave_layout(net, B, &d, const_cast<float*>(dsave));
+    const int P = net->P, n = net->n, rows = B * P, H4 = 4 * net->H;
+    const hipStream_t st = (hipStream_t)stream;
+    // one batched weight gradient: nb = iters blocks, no row splits (no scratch)
+    auto wg = [&](int R, int N, int K, const float* dz, int ldz, const float* x1, int ld1, int K1, size_t s1,
+                  const float* x2, int ld2, size_t s2, float* gw, float* gb) -> int {
+        dadmm::WgradArgs a{dz, x1, K1 < K ? x2 : x1, gw, gb, nullptr, nullptr, R, N, K, K1, ldz, ld1,
+                           K1 < K ? ld2 : ld1, 1, 1};
+        a.nb = iters;
+        a.zs = (size_t)dsave_stride;
+        a.s1 = s1;
+        a.s2 = K1 < K ? s2 : s1;
+        return dadmm::launch_wgrad(a, st) == hipSuccess ? DADMM_OK : DADMM_EHIP;
+    };
+    auto cs = [&](const float* part, int G, int R, int C, float* out) -> int {
+        return dadmm::launch_colsum(part, G, R, C, out, 1, st, iters, (size_t)dsave_stride) == hipSuccess
+                   ? DADMM_OK : DADMM_EHIP;
+    };
+    const size_t ss = (size_t)sv_stride;
+    const int hid = net->dec_width[2];
+    TRY(wg(B, H4, hid, d.dz, H4, sv0->dec_y[2], hid, hid, ss, nullptr, 0, 0, g->fc_w, g->fc_b));
+    for (int j = 2; j >= 0; --j) {
+        const int N = net->dec_width[j];
+        const int Kin = j > 0 ? net->dec_width[j - 1] : P * net->width[4];
+        const float* xin = j > 0 ? sv0->dec_y[j - 1] : sv0->e;
+        const int nblk = (int)(dadmm_hyper_rownorm_bwd_part_bytes(B, N) / (4 * 2 * (size_t)N));
+        TRY(cs(d.pdec[j], 1, nblk, 2 * N, g->ln_wb[j]));
+        TRY(wg(B, N, Kin, d.dv[j], N, xin, Kin, Kin, ss, nullptr, 0, 0, g->dec_w[j], g->dec_b[j]));
+    }
+    {
+        const int C = net->width[4];
+        const int nblk = (int)(dadmm_hyper_rownorm_bwd_part_bytes(rows, C) / (4 * 2 * (size_t)C));
+        TRY(cs(d.pnorm, 1, nblk, 2 * C, g->norm_wb));
+    }
+    for (int i = 4; i >= 0; --i) {
+        const int N = net->width[i];
+        TRY(cs(d.pgcn[i], 3, B, N, g->bn_wbc[i]));
+        if (i > 0) {
+            const int Kin = net->width[i - 1];
+            TRY(wg(rows, N, Kin, d.dZ[i], N, sv0->y[i - 1], Kin, Kin, ss, nullptr, 0, 0, g->conv_w[i], nullptr));
+        } else {
+            // layer 1's input cat(AtAy_k, Atb): AtAy of iteration k at AtAy + k atay_stride, Atb shared
+            TRY(wg(rows, N, 2 * n, d.dZ[0], N, AtAy, net->ld, n, (size_t)atay_stride, Atb, net->ld, 0,
+                   g->conv_w[0], nullptr));
         }
     }
     return DADMM_OK;

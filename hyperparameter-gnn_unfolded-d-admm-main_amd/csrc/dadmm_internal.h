@@ -318,11 +318,16 @@ struct WgradArgs {
     float* scratch;         // [splits][N][K] when splits > 1
     float* scratch_bias;    // [splits][N] when splits > 1 and gbias
     int R, N, K, K1, ldz, ld1, ld2, splits, beta;
+    // batches (deferred training gradients): nb blocks of R rows, block b at dz + b zs,
+    // x1 + b s1, x2 + b s2 (floats); nb = 1 for one block
+    int nb = 1;
+    size_t zs = 0, s1 = 0, s2 = 0;
 };
 int wgrad_splits(int R, int N, int K);
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st);
 // out [G][C] (+)= sum over r of part [G][R][C] (fixed order)
-hipError_t launch_colsum(const float* part, int G, int R, int C, float* out, int beta, hipStream_t st);
+hipError_t launch_colsum(const float* part, int G, int R, int C, float* out, int beta, hipStream_t st,
+                         int nb = 1, size_t pstride = 0);
 // out [cols][rows] = in [rows][cols]
 hipError_t launch_transpose(const float* in, int rows, int cols, float* out, hipStream_t st);
 

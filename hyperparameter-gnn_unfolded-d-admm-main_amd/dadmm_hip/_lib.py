@@ -54,6 +54,9 @@ EXPORTED_SYMBOLS = (
     "dadmm_hyper_train_work_bytes",
     "dadmm_hyper_train_forward",
     "dadmm_hyper_train_backward",
+    "dadmm_hyper_train_dsave_floats",
+    "dadmm_hyper_train_backward_deferred",
+    "dadmm_hyper_train_wgrad",
     "dadmm_gnn_flag_bytes",
     "dadmm_gnn_begin",
     "dadmm_gnn_gram",
@@ -229,6 +232,16 @@ def load() -> ctypes.CDLL:
     L.dadmm_hyper_train_backward.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, vp, i32, u64,
                                              ctypes.POINTER(HyperSaved), vp, ctypes.POINTER(HyperGrads),
                                              vp, vp, vp]
+    L.dadmm_hyper_train_dsave_floats.restype = ctypes.c_size_t
+    L.dadmm_hyper_train_dsave_floats.argtypes = [ctypes.POINTER(HyperNet), i32]
+    L.dadmm_hyper_train_backward_deferred.restype = ctypes.c_int
+    L.dadmm_hyper_train_backward_deferred.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, vp, i32, u64,
+                                                      ctypes.POINTER(HyperSaved), vp, ctypes.POINTER(HyperGrads),
+                                                      vp, vp, vp, vp]
+    L.dadmm_hyper_train_wgrad.restype = ctypes.c_int
+    L.dadmm_hyper_train_wgrad.argtypes = [ctypes.POINTER(HyperNet), i32, i32, vp, ctypes.c_int64, vp,
+                                          ctypes.POINTER(HyperSaved), ctypes.c_int64, vp, ctypes.c_int64,
+                                          ctypes.POINTER(HyperGrads), vp]
     # training-mode parameter gradients (csrc/dadmm_hyper_grad.hip)
     L.dadmm_hyper_wgrad_scratch_bytes.restype = ctypes.c_size_t
     L.dadmm_hyper_wgrad_scratch_bytes.argtypes = [i32, i32, i32]

@@ -58,9 +58,10 @@ class GnnRun:
                 ctypes.byref(self.d), _ptr(self.op.workspace), _ptr(self.b), _ptr(self.y0),
                 _ptr(self.U0), _ptr(self.Atb), _ptr(self.flags), _stream(self.dev)))
 
-    def gram(self, k: int, x: torch.Tensor = None) -> torch.Tensor:
-        """A^T A y_k (guard-resolved y_k) or, with ``x``, A^T A x."""
-        out = torch.empty((self.B, self.P, self.op.n_store), device=self.dev)
+    def gram(self, k: int, x: torch.Tensor = None, out: torch.Tensor = None) -> torch.Tensor:
+        """A^T A y_k (guard-resolved y_k) or, with ``x``, A^T A x; into ``out`` if given."""
+        if out is None:
+            out = torch.empty((self.B, self.P, self.op.n_store), device=self.dev)
         if x is not None:
             x = _pad_n(x.float(), self.op.n_store).contiguous()
         with torch.cuda.device(self.dev):
@@ -158,8 +159,9 @@ class GnnTrainFn(torch.autograd.Function):
     ONE autograd node: per iteration A^T A y_k (dadmm_gnn_gram), the hypernetwork
     (dadmm_hyper_train_forward, one library call) and the D-ADMM step (dadmm_gnn_step); the
     backward walks the iterations in reverse with dadmm_gnn_step_backward,
-    dadmm_hyper_train_backward (parameter gradients added in place into the pass's flat buffer,
-    hyper_ops._GradAccumulator) and A^T A for the gram's input gradient. Replaces K x (GramFn,
+    dadmm_hyper_train_backward_deferred (the parameter gradients' operands saved per iteration) and
+    A^T A for the gram's input gradient, then ONE dadmm_hyper_train_wgrad call adds the parameter
+    gradients of all K iterations into the pass's flat buffer (hyper_ops._GradAccumulator). Replaces K x (GramFn,
     HyperTrainFn, StepFn) nodes and the engine's per-iteration gradient sums — the training step
     is then bound by the GPU, not by the host.
 
@@ -180,13 +182,15 @@ class GnnTrainFn(torch.autograd.Function):
         arena = torch.empty(K * plan.per, device=dev)
         svs = [plan.saved(arena, k) for k in range(K)]
         U, D = run.U0, run.d0
-        Us, Ds, As = [U], [D], []
+        Us, Ds = [U], [D]
+        # the K gram outputs in one [K, B, P, ns] block: the deferred weight gradient of the first
+        # GCN layer reads them at a fixed stride
+        As = torch.empty((K, run.B, run.P, run.op.n_store), device=dev)
         with torch.cuda.device(dev):
             for k in range(K):
-                AtAy = run.gram(k)
+                AtAy = run.gram(k, out=As[k])
                 plan.forward(AtAy, run.Atb, a_hat, per_sample, seeds[k], svs[k], stream)
                 _, U, D = run.step(k, AtAy, plan.hyp(arena, k), U, D)
-                As.append(AtAy)
                 Us.append(U)
                 Ds.append(D)
         run.finish()
@@ -210,6 +214,9 @@ class GnnTrainFn(torch.autograd.Function):
         # this node's own accumulator: its sums are returned to autograd below
         acc = hyper_ops._GradAccumulator(ctx.model, dev)
         g = acc.grads_struct()
+        # parameter gradients deferred: each iteration's operands go to a block of dsave and one
+        # dadmm_hyper_train_wgrad call sums all K iterations' (one launch per parameter, not K)
+        dsave = torch.empty(K * plan.dsave_per, device=dev)
         gY = gY.contiguous() if gY is not None else None
         gy1 = gY[K - 1] if gY is not None else None
         gU1 = gd1 = None
@@ -220,8 +227,8 @@ class GnnTrainFn(torch.autograd.Function):
                                                          gy1, gU1, gd1)
                 if k == K - 1 and ghyp_last is not None:
                     ghyp.add_(ghyp_last)
-                dA = plan.backward(ctx.As[k], run.Atb, ctx.a_hat, ctx.per_sample, ctx.seeds[k], ctx.svs[k], ghyp,
-                                   g, stream)
+                dA = plan.backward_deferred(ctx.As[k], run.Atb, ctx.a_hat, ctx.per_sample, ctx.seeds[k],
+                                            ctx.svs[k], ghyp, g, dsave, k, stream)
                 if k == 0:   # y_0, U_0, delta_0 are the random inits: no gradient
                     break
                 gA.add_(dA)
@@ -229,6 +236,7 @@ class GnnTrainFn(torch.autograd.Function):
                 if gY is not None:
                     gy.add_(gY[k - 1])
                 gy1, gU1, gd1 = gy, gU, gd
+            plan.wgrad(K, ctx.As, run.Atb, ctx.arena, dsave, g, stream)
         ctx.arena = ctx.svs = ctx.As = ctx.Us = ctx.Ds = None
         grads = tuple(acc.view(p) if p.requires_grad else None for p in ctx.params)
         ctx.params = None

@@ -527,6 +527,7 @@ class NativeHyperPlan:
             raise ValueError("dadmm_hyper_train_work_bytes: hypernetwork dimensions not supported")
         self.work = torch.empty(nbytes // 4 + 4, device=dev)
         self.dAtAy = None
+        self.dsave_per = L.dadmm_hyper_train_dsave_floats(ctypes.byref(net), B)   # floats, multiple of 4
 
     @staticmethod
     def get(model, B, P, n, ns, dev):
@@ -578,6 +579,26 @@ class NativeHyperPlan:
             ctypes.byref(self.net), self.B, _ptr(AtAy), _ptr(Atb), _ptr(ahat), int(per_sample), seed,
             ctypes.byref(sv), _ptr(dhyp), ctypes.byref(g), _ptr(self.dAtAy), _ptr(self.work), stream))
         return self.dAtAy
+
+    def backward_deferred(self, AtAy, Atb, ahat, per_sample, seed, sv, dhyp, g, dsave, k, stream):
+        """backward with the parameter gradients deferred: their operands go to block k of
+        ``dsave`` (blocks of ``dsave_per`` floats) for one ``wgrad`` call after the last iteration."""
+        if self.dAtAy is None:
+            self.dAtAy = torch.zeros((self.B, self.P, self.ns), device=self.dev)
+        _lib.check("dadmm_hyper_train_backward_deferred", self.L.dadmm_hyper_train_backward_deferred(
+            ctypes.byref(self.net), self.B, _ptr(AtAy), _ptr(Atb), _ptr(ahat), int(per_sample), seed,
+            ctypes.byref(sv), _ptr(dhyp), ctypes.byref(g), _ptr(self.dAtAy), _ptr(self.work),
+            ctypes.c_void_p(dsave.data_ptr() + 4 * k * self.dsave_per), stream))
+        return self.dAtAy
+
+    def wgrad(self, iters, As, Atb, arena, dsave, g, stream):
+        """Add the parameter gradients of ``iters`` deferred iterations (As [iters, B, P, ns], the
+        saved blocks of ``arena``, the operand blocks of ``dsave``) into ``g``'s accumulators."""
+        assert As.is_contiguous() and As.shape[0] >= iters
+        _lib.check("dadmm_hyper_train_wgrad", self.L.dadmm_hyper_train_wgrad(
+            ctypes.byref(self.net), self.B, iters, _ptr(As), As[0].numel(), _ptr(Atb),
+            ctypes.byref(self.saved(arena, 0)), self.per, _ptr(dsave), self.dsave_per, ctypes.byref(g),
+            stream))
 
 
 def _native_forward(ctx, L, AtAy, Atb, ahat, model, n, per_sample, seed, defer):

@@ -517,6 +517,28 @@ int dadmm_hyper_train_backward(const dadmm_hyper_net* net, int32_t B, const floa
                                const float* ahat, int32_t ahat_per_sample, uint64_t seed,
                                const dadmm_hyper_saved* sv, const float* dhyp, const dadmm_hyper_grads* g,
                                float* dAtAy, void* work, void* stream);
+/* Deferred parameter gradients (round 4): dadmm_hyper_train_backward_deferred is the same backward
+ * of one iteration, except that instead of accumulating the parameter gradients it writes their
+ * operands (every layer's dZ and the normalisation partial sums) into `dsave`, one block of
+ * dadmm_hyper_train_dsave_floats(net, B) floats per iteration (16-byte aligned); the input
+ * gradients (dX, d AtAy) are computed as before. After the last (reverse) iteration,
+ * dadmm_hyper_train_wgrad accumulates (+=) the parameter gradients of all `iters` iterations into
+ * `g` at once — one batched weight-gradient GEMM per linear, one batched column sum per
+ * normalisation — reading iteration k's activations at sv0 + k sv_stride floats (the saved
+ * blocks of dadmm_hyper_train_forward, equally spaced), its gradient operands at
+ * dsave + k dsave_stride and its AtAy at AtAy + k atay_stride (Atb shared). Replaces ~19
+ * launches per iteration by ~19 in all (gnn_dlasso_progressive.py:207-214's backward at small
+ * batches is bound by launches, not by work). */
+size_t dadmm_hyper_train_dsave_floats(const dadmm_hyper_net* net, int32_t B);
+int dadmm_hyper_train_backward_deferred(const dadmm_hyper_net* net, int32_t B, const float* AtAy,
+                                        const float* Atb, const float* ahat, int32_t ahat_per_sample,
+                                        uint64_t seed, const dadmm_hyper_saved* sv, const float* dhyp,
+                                        const dadmm_hyper_grads* g, float* dAtAy, void* work, float* dsave,
+                                        void* stream);
+int dadmm_hyper_train_wgrad(const dadmm_hyper_net* net, int32_t B, int32_t iters, const float* AtAy,
+                            int64_t atay_stride, const float* Atb, const dadmm_hyper_saved* sv0,
+                            int64_t sv_stride, const float* dsave, int64_t dsave_stride,
+                            const dadmm_hyper_grads* g, void* stream);
 
 #ifdef __cplusplus
 }
