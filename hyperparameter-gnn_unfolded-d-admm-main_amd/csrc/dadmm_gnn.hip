@@ -433,6 +433,134 @@ __global__ __launch_bounds__(THREADS) void gram_w1_kernel(GnnArgs a, int k, cons
     }
 }
 
+// ---- gram with the agent's operator resident in LDS (round 4, the default where it fits) ---------
+// gram_kernel re-reads A_p and A_p^T from L2 for every (16-sample tile, agent) item and runs one
+// dependent MFMA chain per wave (PMC at configs[2]: MFMA busy 0.25, waves half the time stalled on
+// issue). Here a workgroup owns ONE agent and a run of tiles: A_p's rows (16 MQ x n_pad) are copied
+// into LDS once (row stride n_pad + 4 floats: the GEMM2 fragment gathers, rows 4 h + r apart, land
+// in 64 distinct banks) and every wave runs whole items as gram_w1_kernel does — GEMM1 with the MQ
+// m-block chains interleaved and R kept in registers (the accumulator layout is GEMM2's B operand),
+// GEMM2 with two n-tiles' chains interleaved — reading both operand fragments from LDS; only the x
+// and out streams touch HBM (x through a GX-deep register ring, mode 2's out rows two n-tile pairs
+// ahead). 16 waves (four per SIMD) hide the stream latency. Chains and their order are
+// gram_kernel's: GEMM1 from +0 over the columns in 16-blocks (0,4,8,12,1,... inside), GEMM2 from +0
+// over the m-blocks ascending — bit-identical output.
+#ifndef DADMM_GRAM_LDS
+#define DADMM_GRAM_LDS 1
+#endif
+constexpr int GL_WAVES = 16;
+__host__ __device__ constexpr size_t gram_lds_bytes(int mq, int n_pad) { return 4 * (size_t)16 * mq * (n_pad + 4); }
+
+template <int MQ>
+__global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int k, const float* x_raw, float* out,
+                                                                 int mode, int tpw) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int GX = 4;                          // x k-steps in flight
+    const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad, MP = a.m_pad;
+    const int LS = NP + 4;
+    const int p = blockIdx.x % P, grp = blockIdx.x / P;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = lane & 15, h = lane >> 4;
+    constexpr int mbk = MQ;                        // m-blocks holding rows (the host picks MQ = ceil(m / 16))
+    const int T = NP / 16;                         // 16-column steps
+    const int tiles = (B + BT - 1) / BT;
+
+    // A_p rows [0, 16 mbk) -> LDS (rows past m are the operator's zero padding)
+    {
+        const int q4 = NP / 4, total = 16 * mbk * q4;
+        const float* src = a.A + (size_t)p * MP * NP;
+        for (int i = threadIdx.x; i < total; i += 64 * GL_WAVES) {
+            const int r = i / q4, c = i - r * q4;
+            *(f32x4*)(lds + r * LS + 4 * c) = *(const f32x4*)(src + (size_t)r * NP + 4 * c);
+        }
+    }
+    bool zero = false;
+    const float* xs = x_raw != nullptr ? x_raw : y_source(a, k, zero);
+    const uint32_t sbytes = (uint32_t)((size_t)B * P * n * 4);
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), 0, zero ? 0 : (int)sbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)sbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t roi = __builtin_amdgcn_make_buffer_rsrc(out, 0, mode == 2 ? (int)sbytes : 0, 0x00020000);
+    __syncthreads();
+
+    const int t_end = min(tiles, (grp + 1) * tpw);
+    for (int tile = grp * tpw + w; tile < t_end; tile += GL_WAVES) {
+        const int s = tile * BT + j;
+        const bool sv = s < B;
+        const uint32_t rowoff = sv ? (uint32_t)(((size_t)s * P + p) * n * 4) : 0x80000000u;
+        // GEMM1: R[g] = A_p[16 g + j, :] x, MQ chains interleaved
+        f32x4 R[MQ];
+#pragma unroll
+        for (int g = 0; g < MQ; ++g) R[g] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        auto ldx = [&](int t) -> f32x4 {
+            const uint32_t off = (t < T && 16 * t + 4 * h < n && sv) ? rowoff + (uint32_t)(64 * t + 16 * h) : 0x80000000u;
+            return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+        };
+        auto lda = [&](f32x4 (&dst)[MQ], int t) {
+#pragma unroll
+            for (int g = 0; g < MQ; ++g)
+                dst[g] = *(const f32x4*)(lds + (16 * g + j) * LS + 16 * t + 4 * h);
+        };
+        f32x4 xr[GX], af[2][MQ];
+#pragma unroll
+        for (int u = 0; u < GX; ++u) xr[u] = ldx(u);
+        lda(af[0], 0);
+        for (int t0 = 0; t0 < T; t0 += GX) {
+#pragma unroll
+            for (int u = 0; u < GX; ++u) {
+                const int t = t0 + u;
+                if (t < T) {
+                    if (t + 1 < T) lda(af[(u + 1) & 1], t + 1);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int g = 0; g < MQ; ++g) R[g] = mfma4(af[u & 1][g][r], xr[u][r], R[g]);
+                }
+                xr[u] = ldx(t + GX);
+            }
+        }
+        // GEMM2: out rows of n-tiles nb, nb + 1 = A_p^T R, one chain per n-tile over the m-blocks
+        const int NT = T;
+        auto ldt = [&](f32x4 (&dst)[MQ], int nb) {
+#pragma unroll
+            for (int g = 0; g < MQ; ++g)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    dst[g][r] = lds[(16 * g + 4 * h + r) * LS + 16 * nb + j];
+        };
+        auto ldo = [&](int nb) -> f32x4 {
+            const uint32_t off = (nb < NT && 16 * nb + 4 * h < n && sv) ? rowoff + (uint32_t)(64 * nb + 16 * h) : 0x80000000u;
+            return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(roi, off, 0, 0));
+        };
+        // mode 2's out rows two pairs ahead (oc: this pair, on: the next)
+        f32x4 oc0 = ldo(0), oc1 = ldo(1), on0 = ldo(2), on1 = ldo(3);
+        for (int n0 = 0; n0 < NT; n0 += 2) {
+            f32x4 at0[MQ], at1[MQ];
+            ldt(at0, n0);
+            ldt(at1, n0 + 1 < NT ? n0 + 1 : n0);
+            f32x4 g0 = {0.0f, 0.0f, 0.0f, 0.0f}, g1 = g0;
+#pragma unroll
+            for (int g = 0; g < MQ; ++g)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    g0 = mfma4(at0[g][r], R[g][r], g0);
+                    g1 = mfma4(at1[g][r], R[g][r], g1);
+                }
+            const f32x4 o0 = mode == 2 ? oc0 + g0 : g0;
+            const f32x4 o1 = mode == 2 ? oc1 + g1 : g1;
+            const uint32_t s0 = (16 * n0 + 4 * h < n && sv) ? rowoff + (uint32_t)(64 * n0 + 16 * h) : 0x80000000u;
+            const uint32_t s1 = (n0 + 1 < NT && 16 * (n0 + 1) + 4 * h < n && sv)
+                                    ? rowoff + (uint32_t)(64 * (n0 + 1) + 16 * h) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, o0), ro, s0, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, o1), ro, s1, 0, 0);
+            oc0 = on0;
+            oc1 = on1;
+            on0 = ldo(n0 + 4);
+            on1 = ldo(n0 + 5);
+        }
+    }
+}
+
 // ---- step: gradient, primal update, consensus and dual update of (sample, 128 columns) ----------
 // One workgroup per (sample, UCB = 128 columns). A lane owns 4 columns of one agent row; a wave
 // instruction covers two agent rows (lanes 0-31 and 32-63), so every global access is a 16-byte
@@ -790,6 +918,46 @@ size_t gnn_gram_lds(int m_pad) { return 4 * (size_t)(BT * (m_pad + 4) + (DADMM_G
 hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* out, int mode,
                            hipStream_t st) {
     const int mbk = (a.m + 15) / 16;
+    const int mq = mbk;
+    if (DADMM_GRAM_LDS && mode != 1 && mbk >= 1 && mbk <= 4 && gnn::gram_lds_bytes(mq, a.n_pad) <= 160 * 1024) {
+        // workgroups = P x S splits of the tiles; S minimises (rounds of workgroups over the CUs) x
+        // (tiles each wave runs), preferring fewer workgroups on a tie
+        static int cus = 0;
+        if (cus == 0) {
+            int dev = 0;
+            hipDeviceProp_t prop;
+            cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                      ? prop.multiProcessorCount : 256;
+        }
+        const int tiles = (a.B + BT - 1) / BT;
+        int best_s = 1;
+        long best = -1;
+        for (int S = 1; S <= (tiles + gnn::GL_WAVES - 1) / gnn::GL_WAVES; ++S) {
+            const int tpw = (tiles + S - 1) / S;
+            const long cost = (long)((a.P * S + cus - 1) / cus) * ((tpw + gnn::GL_WAVES - 1) / gnn::GL_WAVES);
+            if (best < 0 || cost < best) {
+                best = cost;
+                best_s = S;
+            }
+        }
+        const int tpw = (tiles + best_s - 1) / best_s;
+        const size_t lds = gnn::gram_lds_bytes(mq, a.n_pad);
+        const void* kern = mq == 1 ? (const void*)gnn::gram_lds_kernel<1>
+                         : mq == 2 ? (const void*)gnn::gram_lds_kernel<2>
+                         : mq == 3 ? (const void*)gnn::gram_lds_kernel<3> : (const void*)gnn::gram_lds_kernel<4>;
+        hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        const dim3 grid(a.P * best_s), block(64 * gnn::GL_WAVES);
+        if (mq == 1)
+            hipLaunchKernelGGL(gnn::gram_lds_kernel<1>, grid, block, lds, st, a, k, x_raw, out, mode, tpw);
+        else if (mq == 2)
+            hipLaunchKernelGGL(gnn::gram_lds_kernel<2>, grid, block, lds, st, a, k, x_raw, out, mode, tpw);
+        else if (mq == 3)
+            hipLaunchKernelGGL(gnn::gram_lds_kernel<3>, grid, block, lds, st, a, k, x_raw, out, mode, tpw);
+        else
+            hipLaunchKernelGGL(gnn::gram_lds_kernel<4>, grid, block, lds, st, a, k, x_raw, out, mode, tpw);
+        return hipGetLastError();
+    }
     if (DADMM_GRAM_W1 && mbk <= 8) {
         const int items = ((a.B + BT - 1) / BT) * a.P;
         const int grid = (items + gnn::WAVES - 1) / gnn::WAVES;
