@@ -710,6 +710,7 @@ static int hyper_input(int32_t rows, int32_t K, int32_t N, const float* x1, int3
     a->ld2 = ld2;
     a->K1 = K1;
     a->W = W;
+    a->ldw = K;
     a->y = const_cast<float*>(y);
     a->ldy = ldy;
     a->rows = rows;
@@ -745,6 +746,40 @@ int dadmm_hyper_gcn(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1,
     if (rc) return rc;
     if (!bias || !ahat || !bn_mean || !bn_var || !bn_weight || !bn_bias)
         return fail(DADMM_EINVAL, "a required pointer is NULL");
+    a.bias = bias;
+    a.B = B;
+    a.P = P;
+    a.ahat = ahat;
+    a.ahat_per_sample = ahat_per_sample ? 1 : 0;
+    a.bn_mean = bn_mean;
+    a.bn_var = bn_var;
+    a.bn_w = bn_weight;
+    a.bn_b = bn_bias;
+    a.bn_eps = bn_eps;
+    a.slope = slope;
+    hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_GCN, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "gcn launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_hyper_gcn_ex(int32_t B, int32_t P, int32_t K, int32_t N, const float* x, int32_t ldx,
+                       const float* W, int32_t ldw, const float* addend, int32_t ld_add, const float* bias,
+                       const float* ahat, int32_t ahat_per_sample, const float* bn_mean,
+                       const float* bn_var, const float* bn_weight, const float* bn_bias, float bn_eps,
+                       float slope, int32_t raw, float* y, int32_t ldy, void* stream) {
+    if (B < 0 || P < 1 || P > 160) return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d (P <= 160)", B, P);
+    dadmm::HyperArgs a;
+    int rc = hyper_input(B * P, K, N, x, ldx, K, nullptr, 0, W, y, ldy, &a);
+    if (rc) return rc;
+    if (ldw < K || (ldw & 3)) return fail(DADMM_EUNSUPPORTED, "ldw=%d must be >= K=%d and a multiple of 4", ldw, K);
+    if (!ahat || (!raw && (!bias || !bn_mean || !bn_var || !bn_weight || !bn_bias)))
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (addend && (ld_add < N || (ld_add & 3) || !aligned16(addend)))
+        return fail(DADMM_EUNSUPPORTED, "addend needs ld_add >= N, ld_add %% 4 == 0 and 16-byte alignment");
+    a.ldw = ldw;
+    a.addend = addend;
+    a.ld_add = ld_add;
+    a.raw = raw ? 1 : 0;
     a.bias = bias;
     a.B = B;
     a.P = P;

@@ -456,7 +456,7 @@ __global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int 
                                                                  int mode, int tpw) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int GX = 4;                          // x k-steps in flight
-    const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad, MP = a.m_pad;
+    const int P = a.P, n = a.n, B = a.B, NP = a.n_pad, MP = a.m_pad;
     const int LS = NP + 4;
     const int p = blockIdx.x % P, grp = blockIdx.x / P;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
     for (int c = 0; c < 2; ++c) {
         int n = col0 + 16 * (2 * wcol + c) + j;
         n = n < a.N ? n : a.N - 1;
-        ow[c] = (size_t)n * K + 4 * h;
+        ow[c] = (size_t)n * a.ldw + 4 * h;
     }
 
     const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
         const int kq = 4 * (lane >> 4);
         const rsrc_t rx1 = make_rsrc(a.x1 + (size_t)row0 * a.ld1, (size_t)rows_t * a.ld1 * 4);
         const rsrc_t rx2 = make_rsrc(SPLIT ? a.x2 + (size_t)row0 * a.ld2 : a.x1, SPLIT ? (size_t)rows_t * a.ld2 * 4 : 0);
-        const rsrc_t rw = make_rsrc(a.W, (size_t)a.N * K * 4);
+        const rsrc_t rw = make_rsrc(a.W, (size_t)a.N * a.ldw * 4);
         uint32_t o1[NBW], o2[NBW];
 #pragma unroll
         for (int i = 0; i < NBW; ++i) {
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             } else {
                 int nn = col0 + 16 * (q - NBA) + j;
                 nn = nn < a.N ? nn : a.N - 1;
-                o1[i] = o2[i] = (uint32_t)(((size_t)nn * K + kq) * 4);
+                o1[i] = o2[i] = (uint32_t)(((size_t)nn * a.ldw + kq) * 4);
             }
         }
         auto dma = [&](int t) {
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             }
             return;
         }
-        if (threadIdx.x < TN) {
+        if (threadIdx.x < TN && !a.raw) {
             const int col = col0 + threadIdx.x < a.N ? col0 + threadIdx.x : a.N - 1;
             const float sc = (1.0f / sqrtf(a.bn_var[col] + a.bn_eps)) * a.bn_w[col];
             colp[threadIdx.x] = a.bias[col];
@@ -512,12 +512,24 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
         }
         __syncthreads();
         mix([&](int r, int c, const f32x4& v) {
-            f32x4 o;
+            f32x4 o, ad = zero;
+            if (a.addend != nullptr) {   // e.g. layer 1's Atb half, formed once per forward
+                const float* src = a.addend + (size_t)(row0 + r) * a.ld_add + col0 + c;
+                if (c + 4 <= cols) {
+                    ad = *(const f32x4*)src;
+                } else {
+                    for (int e = 0; e < cols - c; ++e) ad[e] = src[e];
+                }
+            }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                float t = v[e] + colp[c + e];
-                t = t > 0.0f ? t : t * a.slope;
-                o[e] = (t - colp[TN + c + e]) * colp[2 * TN + c + e] + colp[3 * TN + c + e];
+                float t = a.addend != nullptr ? v[e] + ad[e] : v[e];
+                if (!a.raw) {
+                    t = t + colp[c + e];
+                    t = t > 0.0f ? t : t * a.slope;
+                    t = (t - colp[TN + c + e]) * colp[2 * TN + c + e] + colp[3 * TN + c + e];
+                }
+                o[e] = t;
             }
             float* dst = a.y + (size_t)(row0 + r) * a.ldy + col0 + c;
             if (c + 4 <= cols) {

@@ -206,7 +206,8 @@ struct HyperArgs {
     const float* x1;        // input columns [0, K1): row r at x1 + r * ld1
     const float* x2;        // input columns [K1, K): row r at x2 + r * ld2 (nullable if K1 == K)
     int ld1, ld2, K1;
-    const float* W;         // [N][K] (nn.Linear.weight)
+    const float* W;         // [N][ldw] (nn.Linear.weight; ldw = K unless a column slice of it)
+    int ldw;
     const float* bias;      // [N] (nullable for EPI_BIAS)
     float* y;               // [rows][ldy]
     int ldy;
@@ -231,6 +232,10 @@ struct HyperArgs {
     float drop_p;           // dropout probability (0: none)
     uint64_t seed;          // dropout stream: keep(site, row, col) = hash(seed, site, row, col) >= p
     int site;
+    // GCN (inference) only: addend [rows][ld_add] added to the mix A_hat (x W^T) before the bias
+    // (nullable); raw != 0: y = A_hat (x W^T) (+ addend), no bias / leaky_relu / BatchNorm
+    const float* addend;
+    int ld_add, raw;
 };
 
 // Counter-based dropout mask shared by the training forward and backward kernels (the backward

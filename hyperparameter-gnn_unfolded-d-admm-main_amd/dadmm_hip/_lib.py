@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -36,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "dadmm_adjoint_scratch_bytes",
     "dadmm_adjoint",
     "dadmm_hyper_gcn",
+    "dadmm_hyper_gcn_ex",
     "dadmm_hyper_linear",
     "dadmm_hyper_rownorm",
     "dadmm_hyper_head",
@@ -197,6 +198,8 @@ def load() -> ctypes.CDLL:
         f.argtypes = args
     for name, args in (("dadmm_hyper_gcn", [i32] * 4 + [vp, i32, i32, vp, i32] + [vp] * 3 + [i32]
                         + [vp] * 4 + [f32, f32, vp, i32, vp]),
+                       ("dadmm_hyper_gcn_ex", [i32] * 4 + [vp, i32, vp, i32, vp, i32, vp, vp, i32]
+                        + [vp] * 4 + [f32, f32, i32, vp, i32, vp]),
                        ("dadmm_hyper_linear", [i32] * 3 + [vp, i32, i32, vp, i32, vp, vp, vp, i32, vp]),
                        ("dadmm_hyper_rownorm", [i32, i32, vp, vp, vp, f32, i32, f32, vp, vp]),
                        ("dadmm_hyper_head", [i32, i32, i32, vp, i32, vp, vp] + [f32] * 4 + [vp, vp]),

@@ -19,6 +19,7 @@ masks from the seed instead of storing them.
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 
 import torch
@@ -99,6 +100,28 @@ class HyperBuffers:
         self.scratch = [torch.empty(max(L.dadmm_hyper_linear_ln_scratch_bytes(B, k, w), 16) // 4,
                                     device=device) for k, w in zip(ins, dec_widths)]
         self.hyp = torch.empty((B, 4, H), device=device)
+        self.c1 = None          # layer 1's Atb half, A_hat (Atb W1[:, n:]^T) (hypernetwork_eval_prepare)
+
+
+def hypernetwork_eval_prepare(model, Atb, n, ahat, per_sample, bufs: HyperBuffers):
+    """Once per forward: layer 1's input is cat(AtAy_k, Atb) (:165) and Atb does not change between
+    iterations, so its half of the GCNConv, A_hat (Atb W1[:, n:]^T), is formed here once (raw
+    dadmm_hyper_gcn_ex) and every iteration's layer 1 runs its GEMM over AtAy_k alone (half the
+    K depth) with this term added before the bias. Needs n % 16 == 0 (the in-place cat layout)."""
+    if n % 16 or os.environ.get("DADMM_HYPER_ATB_HOIST", "1") == "0":   # (the env switch: A/B timing)
+        bufs.c1 = None
+        return
+    L = _lib.load()
+    B, P, ns = Atb.shape
+    conv = model.encoder.conv1
+    N = conv.lin.out_features
+    if bufs.c1 is None or bufs.c1.shape != (B * P, N):
+        bufs.c1 = torch.empty((B * P, N), device=Atb.device)
+    w = conv.lin.weight
+    with torch.cuda.device(Atb.device):
+        _lib.check("dadmm_hyper_gcn_ex", L.dadmm_hyper_gcn_ex(
+            B, P, n, N, _ptr(Atb), ns, w.data_ptr() + 4 * n, w.shape[1], None, 0, None, _ptr(ahat),
+            int(per_sample), None, None, None, None, 0.0, 0.0, 1, _ptr(bufs.c1), N, _stream(Atb.device)))
 
 
 def hypernetwork_eval(model, AtAy, Atb, n, ahat, per_sample, bufs: HyperBuffers):
@@ -121,6 +144,15 @@ def hypernetwork_eval(model, AtAy, Atb, n, ahat, per_sample, bufs: HyperBuffers)
         for i, (conv, bn) in enumerate(zip(convs, bns)):
             N = conv.lin.out_features
             y = bufs.x[i & 1]
+            if i == 0 and bufs.c1 is not None and K1 < K:
+                # the AtAy half only; the Atb half comes from hypernetwork_eval_prepare
+                w = conv.lin.weight
+                _lib.check("dadmm_hyper_gcn_ex", L.dadmm_hyper_gcn_ex(
+                    B, P, K1, N, _ptr(x1), ld1, _ptr(w), w.shape[1], _ptr(bufs.c1), N, _ptr(conv.bias),
+                    _ptr(ahat), int(per_sample), _ptr(bn.running_mean), _ptr(bn.running_var),
+                    _ptr(bn.weight), _ptr(bn.bias), float(bn.eps), LEAKY_SLOPE, 0, _ptr(y), y.shape[1], stream))
+                x1, ld1, K1, x2, ld2, K = y, y.shape[1], N, None, 0, N
+                continue
             _lib.check("dadmm_hyper_gcn", L.dadmm_hyper_gcn(
                 B, P, K, N, _ptr(x1), ld1, K1, _ptr(x2), ld2, _ptr(conv.lin.weight),
                 _ptr(conv.bias), _ptr(ahat), int(per_sample), _ptr(bn.running_mean),

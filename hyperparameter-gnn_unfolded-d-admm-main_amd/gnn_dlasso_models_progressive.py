@@ -282,6 +282,8 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
                                           [self.decoder[i].out_features for i in (0, 4, 8)], H,
                                           device)
             a_hat = a_hat.contiguous()
+        if fused:
+            hyper_ops.hypernetwork_eval_prepare(self, run.Atb, n, a_hat, not graphs.shared, bufs)
         for k in range(K):
             AtAy = GramFn.apply(y, run, k)
             if fused:
@@ -406,6 +408,7 @@ class _EvalGraphPlan:
         def body():
             run = self.run_
             run.begin()
+            hyper_ops.hypernetwork_eval_prepare(model, run.Atb, n, self.ahat, per_sample, self.bufs)
             y, U, D = run.ys[0], run.U0, run.d0
             for k in range(K):
                 AtAy = run.gram(k)

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 12
+#define DADMM_ABI_VERSION 13
 
 enum {
     DADMM_OK = 0,
@@ -363,6 +363,19 @@ int dadmm_hyper_gcn(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1,
                     const float* ahat, int32_t ahat_per_sample, const float* bn_mean,
                     const float* bn_var, const float* bn_weight, const float* bn_bias, float bn_eps,
                     float slope, float* y, int32_t ldy, void* stream);
+/* dadmm_hyper_gcn_ex: the same GCN layer on x [B*P][K] (row stride ldx) with a column slice of
+ *   the weight (W [N][ldw], ldw >= K: e.g. GCNConv.lin.weight + n for the Atb half of layer 1) and an
+ *   optional addend [B*P][ld_add] added to the mix before the bias:
+ *     raw == 0: y = BN(leaky(A_hat (x W^T) + addend + bias));   raw != 0: y = A_hat (x W^T) + addend
+ *   (bias / BatchNorm pointers unused and nullable when raw). Layer 1's input cat(AtAy, Atb) then
+ *   splits into a per-iteration GEMM over AtAy and a once-per-forward raw term over Atb, which
+ *   does not change between iterations (gnn_dlasso_models_progressive.py:165: Atb is loop-invariant).
+ *   Replaces: conv1 of graph_conv (:52-68) on cat(AtAy, Atb) (same value; f32 summation order differs). */
+int dadmm_hyper_gcn_ex(int32_t B, int32_t P, int32_t K, int32_t N, const float* x, int32_t ldx,
+                       const float* W, int32_t ldw, const float* addend, int32_t ld_add, const float* bias,
+                       const float* ahat, int32_t ahat_per_sample, const float* bn_mean,
+                       const float* bn_var, const float* bn_weight, const float* bn_bias, float bn_eps,
+                       float slope, int32_t raw, float* y, int32_t ldy, void* stream);
 int dadmm_hyper_linear(int32_t rows, int32_t K, int32_t N, const float* x1, int32_t ld1,
                        int32_t K1, const float* x2, int32_t ld2, const float* W, const float* bias,
                        float* y, int32_t ldy, void* stream);
@@ -385,8 +398,8 @@ int dadmm_hyper_linear_ln(int32_t rows, int32_t K, int32_t N, const float* x, in
 /* ---- GNN hypernetwork, training mode ---------------------------------------------------------
  * The same hypernetwork with model.train() semantics (gnn_dlasso_models_progressive.py:52-72:
  * Dropout(0.1) active, BatchNorm1d on each sample's own batch statistics over its P nodes) and the
- * pieces of its backward that are not plain GEMMs (the caller runs dW = dZ^T X and dX = dZ W on
- * hipBLASLt). Dropout masks come from a counter-based stream: element (row, col) of dropout site
+ * pieces of its backward (dW = dZ^T X on dadmm_hyper_wgrad, dX = dZ W on dadmm_hyper_linear with
+ * the transposed weight; no hipBLASLt). Dropout masks come from a counter-based stream: element (row, col) of dropout site
  * `site` is kept iff hash(seed, site, row, col) >= drop_p * 2^32 (drop_hash in the sources); the
  * backward regenerates them. Results agree with torch's autograd of the same modules (given the
  * same masks) to f32 rounding; the reference's own dropout draws are not reproducible anywhere.

@@ -105,6 +105,39 @@ def test_gcn_layer_matches_torch(cuda, L, B, P, K, N, per_sample):
     _close(y, want, K)
 
 
+@pytest.mark.parametrize("B,P,n,N,per_sample", [(7, 5, 256, 100, True), (40, 50, 512, 100, True),
+                                                (9, 16, 64, 20, False), (3, 2, 16, 8, True)])
+def test_gcn_ex_split_layer_matches_torch(cuda, L, B, P, n, N, per_sample):
+    """Layer 1 as the model's eval path runs it (hypernetwork_eval_prepare): the raw Atb half
+    A_hat (xb W[:, n:]^T) once, then the AtAy half's GEMM with that term added before the bias,
+    against torch's GCNConv on cat(xa, xb)."""
+    from dadmm_hip.graph import ingest
+    G = B if per_sample else 1
+    graphs = [O.connected_er_graph(P, 0.4, seed=7 * i + P) for i in range(G)]
+    gb = ingest(graphs, P, G, cuda)
+    ahat = _ahat(gb.nbr.reshape(G, P), P, cuda)
+    gen = torch.Generator(device=cuda).manual_seed(B * P + N + n)
+    xa = torch.randn(B * P, n + 4, device=cuda, generator=gen)     # padded rows (ld = n + 4)
+    xb = torch.randn(B * P, n + 4, device=cuda, generator=gen)
+    W = torch.randn(N, 2 * n, device=cuda, generator=gen) / np.sqrt(2 * n)
+    bias, rm, bw, bb = (torch.randn(N, device=cuda, generator=gen) for _ in range(4))
+    rv = torch.rand(N, device=cuda, generator=gen) + 0.5
+    c1 = torch.empty(B * P, N, device=cuda)
+    rc = L.dadmm_hyper_gcn_ex(B, P, n, N, _p(xb), n + 4, W.data_ptr() + 4 * n, 2 * n, None, 0, None, _p(ahat),
+                              int(per_sample), None, None, None, None, 0.0, 0.0, 1, _p(c1), N, _s())
+    assert rc == 0, L.dadmm_last_error()
+    zb = torch.matmul(ahat, F.linear(xb[:, :n], W[:, n:]).view(B, P, N)).reshape(B * P, N)
+    _close(c1, zb, n)
+    y = torch.empty(B * P, N, device=cuda)
+    rc = L.dadmm_hyper_gcn_ex(B, P, n, N, _p(xa), n + 4, _p(W), 2 * n, _p(c1), N, _p(bias), _p(ahat),
+                              int(per_sample), _p(rm), _p(rv), _p(bw), _p(bb), 1e-5, 0.01, 0, _p(y), N, _s())
+    assert rc == 0, L.dadmm_last_error()
+    x = torch.cat([xa[:, :n], xb[:, :n]], dim=1)
+    z = torch.matmul(ahat, F.linear(x, W).view(B, P, N)) + bias
+    want = F.batch_norm(F.leaky_relu(z).reshape(B * P, N), rm, rv, bw, bb, False, 0.0, 1e-5)
+    _close(y, want, 2 * n)
+
+
 @pytest.mark.parametrize("rows,C,act", [(5, 400, False), (1024, 400, True), (3, 2048, True),
                                         (70, 36, False)])
 def test_rownorm_matches_torch(cuda, L, rows, C, act):
