@@ -28,6 +28,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "dadmm_internal.h"
 
@@ -541,6 +542,220 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
     }
 }
 
+// ---- GCN layer (inference) on v_mfma_f32_32x32x2_f32, round 4 --------------------------------
+// linear_kernel's 16x16x4 tiles move 256 operand bytes per 2048-flop MFMA and its 160-row tiles
+// ran the configs[4] 400-wide layers at ~0.43 of the f32 MFMA peak. Here: 256-row x 64-column
+// tiles (5 whole samples of 50 nodes: 98 % of the rows used), 8 waves in a 4 x 2 layout, each
+// wave 64 x 32 (two 32x32 accumulators, 4096 flop per MFMA from one A and one B VGPR). The k
+// dimension streams in 16-wide stages through a DQ-deep LDS ring filled by LDS-DMA (A 16 KB +
+// W 4 KB per stage, lane-linear 1 KB pieces whose 16-byte chunks are XOR-swizzled by row, so
+// every ds_read_b128 fragment read is bank-conflict free); a lane's b128 read feeds four MFMAs
+// (k = 4 kh + s within an 8-wide sub-step: the sum order differs from torch's, not the value
+// beyond f32 rounding). Columns past K, rows past the tile and columns past N load as zeros
+// (buffer range checks), so the loop is branch-free. The epilogue is linear_kernel's inference
+// GCN epilogue (mix with A_hat, the optional addend, bias, leaky_relu, BatchNorm) on the 256-row
+// Z tile.
+constexpr int G32_TM = 256, G32_WAVES = 8, G32_DQ = 4;
+constexpr int G32_STAGE = (G32_TM + TN) * 16;                  // floats per ring stage
+#ifndef DADMM_G32_AHAT_LDS
+#define DADMM_G32_AHAT_LDS 0
+#endif
+#ifndef DADMM_G32_ABL_MIX
+#define DADMM_G32_ABL_MIX 0     // timing builds only: the mix reduced to one node (wrong results)
+#endif
+__host__ __device__ constexpr size_t g32_lds_bytes(int S_t, int P) {
+    const size_t ring = 4 * (size_t)G32_DQ * G32_STAGE;
+    const size_t epi = 4 * ((size_t)G32_TM * ZS + (DADMM_G32_AHAT_LDS ? (((size_t)S_t * P * P + 3) & ~(size_t)3) : 0) + 4 * TN);
+    return ring > epi ? ring : epi;
+}
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(64 * G32_WAVES) void gcn32_kernel(HyperArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float zt[];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = w >> 1, wc = w & 1;
+    const int gn = a.gn;
+    const int tl = xcd_tile(blockIdx.x, gridDim.x);
+    const int ct = tl % gn, rt = tl / gn;
+    const int P = a.P;
+    const int s0 = rt * a.S_t;
+    const int ns = a.B - s0 < a.S_t ? a.B - s0 : a.S_t;
+    const int row0 = s0 * P, rows_t = ns * P;
+    const int col0 = ct * TN;
+    const int K = a.K, T = (K + 15) / 16;
+
+    // LDS-DMA sources: wave w copies A pieces 2w, 2w + 1 (16 rows each) and, for w < 4, W piece w
+    const rsrc_t rx = make_rsrc(a.x1 + (size_t)row0 * a.ld1, (size_t)rows_t * a.ld1 * 4);
+    const rsrc_t rw = make_rsrc(a.W, (size_t)a.N * a.ldw * 4);
+    const int pos = lane & 3;
+    uint32_t oa[2], ka[2], ow = 0, kw = 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = 16 * (2 * w + i) + (lane >> 2);
+        const int chunk = pos ^ ((r >> 2) & 3);
+        oa[i] = r < rows_t ? (uint32_t)(((size_t)r * a.ld1 + 4 * chunk) * 4) : 0x80000000u;
+        ka[i] = (uint32_t)(4 * chunk);                  // the chunk's first k within a stage
+    }
+    const bool wdma = w < 4;
+    {
+        const int c = 16 * (w & 3) + (lane >> 2);
+        const int chunk = pos ^ ((c >> 2) & 3);
+        ow = col0 + c < a.N ? (uint32_t)(((size_t)(col0 + c) * a.ldw + 4 * chunk) * 4) : 0x80000000u;
+        kw = (uint32_t)(4 * chunk);
+    }
+    const int nper = wdma ? 3 : 2;                      // this wave's DMAs per stage
+    auto dma = [&](int t) {
+        float* st = zt + (t % G32_DQ) * G32_STAGE;
+        const int k0 = 16 * t;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            dma16(rx, st + (2 * w + i) * 256, (k0 + (int)ka[i] < K) ? oa[i] + 4u * k0 : 0x80000000u);
+        if (wdma) dma16(rw, st + G32_TM * 16 + (w & 3) * 256, (k0 + (int)kw < K) ? ow + 4u * k0 : 0x80000000u);
+    };
+    // fragment reads of sub-step c (k 8c .. 8c + 7) of stage t: lane (i = lane & 31, kh = lane >> 5)
+    const int fi = lane & 31, kh = lane >> 5;
+    int fa[2], fb;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+        const int R = 64 * wr + 32 * rb + fi;
+        fa[rb] = 4 * R;
+    }
+    const int Cc = 32 * wc + fi;
+    fb = 4 * Cc;
+    auto swz = [](int rc) { return (rc >> 2) & 3; };
+    const int sa0 = swz(64 * wr + fi), sb0 = swz(Cc);   // (32 rb does not change the swizzle)
+    struct Frag {
+        f32x4 a[2], b;
+    };
+    auto frag = [&](Frag& f, int t, int c) {
+        const float* st = zt + (t % G32_DQ) * G32_STAGE;
+        const int chunk = 2 * c + kh;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) f.a[rb] = *(const f32x4*)(st + 4 * (fa[rb] + (chunk ^ sa0)));
+        f.b = *(const f32x4*)(st + G32_TM * 16 + 4 * (fb + (chunk ^ sb0)));
+    };
+    f32x16 acc[2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[rb][e] = 0.0f;
+    auto mma = [&](const Frag& f) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) acc[rb] = mfma32(f.a[rb][s], f.b[s], acc[rb]);
+    };
+    if (T > 0) {
+        const int pre = T < G32_DQ ? T : G32_DQ;
+        for (int u = 0; u < pre; ++u) dma(u);
+        wait_vm(nper * (pre - 1));
+        lds_barrier();
+        Frag f0, f1;
+        frag(f0, 0, 0);
+        for (int u = 0; u < T; ++u) {
+            // stage u's sub-step 0 is in f0; read sub-step 1, then wait for stage u + 1 (this
+            // wave's copies, then every wave's) and refill stage u's slot once all have read it
+            frag(f1, u, 1);
+            mma(f0);
+            int younger = G32_DQ - 2 < T - 2 - u ? G32_DQ - 2 : T - 2 - u;
+            younger = younger > 0 ? younger : 0;
+            wait_vm(nper * younger);
+            lds_barrier();
+            if (u + G32_DQ < T) dma(u + G32_DQ);
+            if (u + 1 < T) frag(f0, u + 1, 0);
+            mma(f1);
+        }
+        lds_barrier();   // the ring's last reads before the epilogue reuses the LDS
+    }
+    // Z tile: acc[rb] register e = row (e & 3) + 8 (e >> 2) + 4 kh of row block rb, column fi
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+            zt[(64 * wr + 32 * rb + (e & 3) + 8 * (e >> 2) + 4 * kh) * ZS + 32 * wc + fi] = acc[rb][e];
+    const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+#if DADMM_G32_AHAT_LDS
+    float* ahs = zt + G32_TM * ZS;                       // [S_t][P][P]
+    float* colp = ahs + ((a.S_t * P * P + 3) & ~3);
+    const float* agl = a.ahat + (a.ahat_per_sample ? (size_t)s0 * P * P : 0);
+    if (a.ahat_per_sample) {
+        for (int i = threadIdx.x; i < ns * P * P; i += 64 * G32_WAVES) ahs[i] = agl[i];
+    } else {
+        for (int i = threadIdx.x; i < P * P; i += 64 * G32_WAVES)
+            for (int sl = 0; sl < ns; ++sl) ahs[sl * P * P + i] = agl[i];
+    }
+    const int ahs_stride = P * P;
+#else
+    // A_hat read through the vector cache (the 16 lanes of a column quad group share each word):
+    // the LDS then holds only the ring / Z tile, so two workgroups fit on a CU and one's epilogue
+    // runs beside the other's MFMA loop
+    const float* ahs = a.ahat + (a.ahat_per_sample ? (size_t)s0 * P * P : 0);
+    const int ahs_stride = a.ahat_per_sample ? P * P : 0;
+    float* colp = zt + G32_TM * ZS;
+#endif
+    if (threadIdx.x < TN && !a.raw) {
+        const int col = col0 + threadIdx.x < a.N ? col0 + threadIdx.x : a.N - 1;
+        const float sc = (1.0f / sqrtf(a.bn_var[col] + a.bn_eps)) * a.bn_w[col];
+        colp[threadIdx.x] = a.bias[col];
+        colp[TN + threadIdx.x] = a.bn_mean[col];
+        colp[2 * TN + threadIdx.x] = sc;
+        colp[3 * TN + threadIdx.x] = a.bn_b[col];
+    }
+    __syncthreads();
+    const int cols = a.N - col0 < TN ? a.N - col0 : TN;
+    const int ng = (P + 3) >> 2;
+    for (int task = threadIdx.x; task < ns * ng * (TN / 4); task += 64 * G32_WAVES) {
+        const int cq = task % (TN / 4), rest = task / (TN / 4);
+        const int g = rest % ng, sl = rest / ng;
+        const int c = 4 * cq;
+        if (c >= cols) continue;
+        const float* at[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) at[e] = ahs + sl * ahs_stride + (4 * g + e < P ? 4 * g + e : P - 1) * P;
+        const float* zc = zt + sl * P * ZS + c;
+        f32x4 v[4] = {zero, zero, zero, zero};
+        for (int q = 0; q < (DADMM_G32_ABL_MIX ? 1 : P); ++q) {
+            const f32x4 z = *(const f32x4*)(zc + q * ZS);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = __builtin_elementwise_fma((f32x4)(at[e][q]), z, v[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (4 * g + e >= P) continue;
+            const int r = sl * P + 4 * g + e;
+            f32x4 o, ad = zero;
+            if (a.addend != nullptr) {
+                const float* src = a.addend + (size_t)(row0 + r) * a.ld_add + col0 + c;
+                if (c + 4 <= cols) {
+                    ad = *(const f32x4*)src;
+                } else {
+                    for (int q = 0; q < cols - c; ++q) ad[q] = src[q];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float t = a.addend != nullptr ? v[e][q] + ad[q] : v[e][q];
+                if (!a.raw) {
+                    t = t + colp[c + q];
+                    t = t > 0.0f ? t : t * a.slope;
+                    t = (t - colp[TN + c + q]) * colp[2 * TN + c + q] + colp[3 * TN + c + q];
+                }
+                o[q] = t;
+            }
+            float* dst = a.y + (size_t)(row0 + r) * a.ldy + col0 + c;
+            if (c + 4 <= cols) {
+                *(f32x4*)dst = o;
+            } else {
+                for (int q = 0; q < cols - c; ++q) dst[q] = o[q];
+            }
+        }
+    }
+}
+
 // LayerNorm over the C columns of every row (biased variance, like torch), then optionally
 // LeakyReLU(slope); one wave per row, the row held in registers (C <= 64 * 4 * CH).
 constexpr int CH = 8;
@@ -720,10 +935,38 @@ static int pick_split_tiles(HyperArgs& a, int K, int& splits) {
     return wr;
 }
 
+// the 32x32x2 GCN kernel (gcn32_kernel) for inference GCN layers on an unsplit input whose grid
+// of 256-row tiles still covers the CUs; DADMM_GCN32=0 in the environment selects linear_kernel
+// (A/B timing)
+static bool try_gcn32(HyperArgs& a, hipStream_t st, hipError_t& err) {
+    static int enabled = -1;
+    if (enabled < 0) {
+        const char* e = getenv("DADMM_GCN32");
+        enabled = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    if (!enabled || a.K1 < a.K || a.P < 1 || a.P > hyper::G32_TM) return false;
+    const int S_t = hyper::G32_TM / a.P;
+    const long gm = (a.B + S_t - 1) / S_t, gn = (a.N + hyper::TN - 1) / hyper::TN;
+    if (gm * gn < 256) return false;
+    const size_t lds = hyper::g32_lds_bytes(S_t, a.P);
+    if (lds > 160 * 1024) return false;
+    a.S_t = S_t;
+    a.gm = (int)gm;
+    a.gn = (int)gn;
+    err = hipFuncSetAttribute((const void*)hyper::gcn32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (err == hipSuccess) {
+        hipLaunchKernelGGL(hyper::gcn32_kernel, dim3((unsigned)(gm * gn)), dim3(64 * hyper::G32_WAVES), lds, st, a);
+        err = hipGetLastError();
+    }
+    return true;
+}
+
 hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st) {
     const int units = (epi == HYPER_EPI_GCN || epi == HYPER_EPI_GCN_TRAIN) ? a.B : a.rows;
     if (units <= 0 || a.N <= 0) return hipSuccess;
     if (a.K1 < a.K && (a.K1 & 15)) return hipErrorInvalidValue;
+    hipError_t gerr = hipSuccess;
+    if (epi == HYPER_EPI_GCN && try_gcn32(a, st, gerr)) return gerr;
     int wr = 0;
     if (epi == HYPER_EPI_BIAS && a.splits > 1) {
         int sp = 0;

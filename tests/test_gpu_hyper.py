@@ -81,7 +81,11 @@ def _ahat(nbr, P, dev):
 @pytest.mark.parametrize("B,P,K,N,per_sample", [(7, 5, 512, 100, True), (33, 5, 100, 200, False),
                                                 (9, 16, 200, 400, True), (3, 50, 400, 400, True),
                                                 (1, 1, 8, 4, False), (40, 2, 64, 36, True),
-                                                (512, 50, 1024, 100, True)])   # DMA ring, 128 rows
+                                                (512, 50, 1024, 100, True),    # DMA ring, 128 rows
+                                                # gcn32_kernel (32x32x2 MFMA, 256-row tiles): 400-wide
+                                                # layers of configs[4], a K tail (100 % 16), shared graph
+                                                (1024, 50, 400, 400, True), (1024, 50, 100, 200, True),
+                                                (2000, 16, 200, 200, False)])
 def test_gcn_layer_matches_torch(cuda, L, B, P, K, N, per_sample):
     from dadmm_hip.graph import ingest
     G = B if per_sample else 1
@@ -106,7 +110,8 @@ def test_gcn_layer_matches_torch(cuda, L, B, P, K, N, per_sample):
 
 
 @pytest.mark.parametrize("B,P,n,N,per_sample", [(7, 5, 256, 100, True), (40, 50, 512, 100, True),
-                                                (9, 16, 64, 20, False), (3, 2, 16, 8, True)])
+                                                (9, 16, 64, 20, False), (3, 2, 16, 8, True),
+                                                (1024, 50, 1024, 100, True)])   # gcn32_kernel
 def test_gcn_ex_split_layer_matches_torch(cuda, L, B, P, n, N, per_sample):
     """Layer 1 as the model's eval path runs it (hypernetwork_eval_prepare): the raw Atb half
     A_hat (xb W[:, n:]^T) once, then the AtAy half's GEMM with that term added before the bias,
