@@ -576,13 +576,21 @@ __global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int 
 //   guard flags themselves.
 constexpr int UP_CH = 4;
 constexpr int UCB = 128;
+// DADMM_STEP_KEEPU=1: the step keeps phase 1's U rows in registers for phase 2 (one fewer HBM
+// stream) — 97 instead of 82 VGPRs, four instead of five waves per SIMD: 86.1-86.4 vs 84.7-85.0 ms
+// at the configs[4] shard forward (profiles/r04/variants_r04o_step_keepu.txt), so off
+#ifndef DADMM_STEP_KEEPU
+#define DADMM_STEP_KEEPU 0
+#endif
 // LDS bytes for one sample's visit lists: at most 2 P entries per agent (each incident edge is
 // visited from both of its ends; a self-loop twice), one byte each
 __host__ __device__ constexpr int update_visit_words(int P) { return (2 * P * P + 3) / 4; }
 __host__ __device__ constexpr size_t update_lds_bytes(int P) {
     return 4 * ((size_t)P * UCB + (size_t)(P + 1) + update_visit_words(P));
 }
-template <bool FUSED>
+// KEEPU (fused pass, P <= 64): phase 1's U rows stay in registers for the dual update of phase 2
+// instead of being read from HBM a second time (one of the pass's nine 4-byte streams per element)
+template <bool FUSED, bool KEEPU = false>
 __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, float* lds) {
     // row pairs in flight per wave: the fused pass streams 5 state tensors, so fewer pairs keep
     // its registers at 4+ waves per SIMD
@@ -616,7 +624,9 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
     // row pairs: wave w handles pairs w, w + 4, ...; lane half selects the row of the pair
     bool bad_y = false, bad_g = false;
-    for (int q0 = w; 2 * q0 < P; q0 += WAVES * UP_CH) {
+    constexpr int UMAX = KEEPU ? 4 : 1;               // 2 * WAVES * UP_CH * UMAX = 64 rows
+    f32x4 ukeep[UMAX][UP_CH];
+    auto phase1 = [&](int q0, int it) {
         f32x4 gv[UP_CH], yv[UP_CH];
         if constexpr (FUSED) {
             f32x4 tv[UP_CH], bv[UP_CH], uv[UP_CH], dv[UP_CH];
@@ -632,6 +642,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
                     if (!uzero) uv[u] = *(const f32x4*)(U + off);
                     dv[u] = *(const f32x4*)(a.D + off);
                 }
+                if constexpr (KEEPU) ukeep[it][u] = uv[u];
             }
 #pragma unroll
             for (int u = 0; u < UP_CH; ++u) {
@@ -678,15 +689,26 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
                 *(f32x4*)(yl + p * UCB + cl) = v;
             }
         }
+    };
+    if constexpr (KEEPU) {
+#pragma unroll
+        for (int it = 0; it < UMAX; ++it)
+            if (2 * (w + it * WAVES * UP_CH) < P) phase1(w + it * WAVES * UP_CH, it);
+    } else {
+        for (int q0 = w; 2 * q0 < P; q0 += WAVES * UP_CH) phase1(q0, 0);
     }
     __syncthreads();
     bool bad_u = false;
-    for (int q0 = w; 2 * q0 < P; q0 += WAVES * UP_CH) {
+    auto phase2 = [&](int q0, int it) {
         f32x4 uv[UP_CH];
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
             const int p = 2 * (q0 + WAVES * u) + half;
-            uv[u] = (p < P && cv && !uzero) ? *(const f32x4*)(U + base + (size_t)p * n) : z4;
+            if constexpr (KEEPU) {
+                uv[u] = ukeep[it][u];
+            } else {
+                uv[u] = (p < P && cv && !uzero) ? *(const f32x4*)(U + base + (size_t)p * n) : z4;
+            }
         }
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
@@ -713,6 +735,13 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
             *(f32x4*)(a.U_next + off) = un;
             *(f32x4*)(a.D_next + off) = acc;
         }
+    };
+    if constexpr (KEEPU) {
+#pragma unroll
+        for (int it = 0; it < UMAX; ++it)
+            if (2 * (w + it * WAVES * UP_CH) < P) phase2(w + it * WAVES * UP_CH, it);
+    } else {
+        for (int q0 = w; 2 * q0 < P; q0 += WAVES * UP_CH) phase2(q0, 0);
     }
     if (FUSED) {
         flag_or(a.flags + GNN_F_GBAD(k), bad_g);
@@ -727,7 +756,10 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
 // the fused pass: one workgroup per item
 __global__ __launch_bounds__(THREADS) void step_kernel(GnnArgs a, int k) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    update_item<true>(a, k, blockIdx.x, lds);
+    if (DADMM_STEP_KEEPU && a.P <= 2 * WAVES * 2 * 4)
+        update_item<true, true>(a, k, blockIdx.x, lds);
+    else
+        update_item<true>(a, k, blockIdx.x, lds);
 }
 
 // the resolve: a short grid (every workgroup reads one flag word); the g = 0 update, if needed,
