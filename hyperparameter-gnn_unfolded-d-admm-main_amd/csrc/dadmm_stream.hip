@@ -80,6 +80,14 @@ constexpr int SLOTS = 3;         // y-block ring: the block of step bs + 2 is lo
 #ifndef DADMM_ST_AT_FROM_A
 #define DADMM_ST_AT_FROM_A 1
 #endif
+// DADMM_ST_DELAY=1: a tile's U / Y (and recording) stores are issued after the NEXT tile's operand
+// loads, so that no wait for those loads includes them (vector-memory operations complete in
+// order and vmcnt counts stores): the stores get two tiles instead of one to drain. Bit-identical,
+// but the held values raise the spills 7 -> 17 VGPRs: 5.99-6.04 vs 5.87-5.89 ms at configs[2]
+// (profiles/r04/variants_r04p_stream_delay.txt), so off
+#ifndef DADMM_ST_DELAY
+#define DADMM_ST_DELAY 0
+#endif
 #define DADMM_STR_(x) #x
 #define DADMM_STR(x) DADMM_STR_(x)
 
@@ -318,6 +326,32 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
     // or an out-of-range offset disables one), because the compiler's wait analysis turns a memory
     // operation on one path of a merge into a full vmcnt wait after it. GEMM2 and the update run
     // in the phases without a primal update too (on A^T = 0; nothing is stored).
+    // the previous tile's stores (DADMM_ST_DELAY): values, offsets (out of range = none) and phase
+    typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+    struct Pend {
+        f32x4 u, y, g;
+        uint32_t su, sy;
+        int k;
+    } pend;
+    pend.u = pend.y = pend.g = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    pend.su = pend.sy = 0x80000000u;
+    pend.k = 0;
+    auto flush = [&]() {
+        const int pk = pend.k;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend.u),
+                                               make_rsrc(pk == K ? a.U_out : a.Ubuf[0], (DADMM_ST_ABL & 8) ? 0u : s_bytes),
+                                               pend.su, 0, DADMM_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend.y),
+                                               make_rsrc(a.Y + (size_t)(pk < K ? pk : 0) * S, (DADMM_ST_ABL & 8) ? 0u : s_bytes),
+                                               pend.sy, 0, DADMM_ST_AUX);
+        if constexpr (REC) {
+            const size_t kS = (size_t)(pk < K ? pk : 0) * S;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend.g), make_rsrc(a.Grec + kS, s_bytes),
+                                                   pend.sy, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend.u), make_rsrc(a.Urec + kS, s_bytes),
+                                                   pend.sy, 0, 0);
+        }
+    };
     auto compute = [&](int k, int c0, const float* ys, int i, Ring& r, auto&& pre, auto&& mid) {
         const int ai = i / CT, ct = i % CT;
         const int p = w + NW * ai;
@@ -383,6 +417,7 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
         // the next tile's A^T rows, U, d0 and A rows: issued at one program point (outside the branch)
         pre();
         mid();
+        if (DADMM_ST_DELAY) flush();   // the previous tile's stores, behind this tile's loads
         f32x4 dv = k == 0 ? r.d : acc;
         if (k >= 1 && a.variant != 0) {
 #pragma unroll
@@ -398,9 +433,10 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
         bad_u0 |= k == 0 && okc && !finite4(uv);
         // U_k after the next tile's A rows are issued: vector-memory operations complete in order,
         // so a load issued after a store waits for it
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, uv),
-                                               make_rsrc(k == K ? a.U_out : a.Ubuf[0], (DADMM_ST_ABL & 8) ? 0u : s_bytes),
-                                               k >= 1 ? soff : 0x80000000u, 0, DADMM_ST_AUX);
+        if (!DADMM_ST_DELAY)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, uv),
+                                                   make_rsrc(k == K ? a.U_out : a.Ubuf[0], (DADMM_ST_ABL & 8) ? 0u : s_bytes),
+                                                   k >= 1 ? soff : 0x80000000u, 0, DADMM_ST_AUX);
         const bool upd = k >= 0 && k < K;
         f32x4 yn, grc;
 #pragma unroll
@@ -416,10 +452,19 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
             bad_y |= upd && okc && !finitef(v);
             yn[r4] = okc ? v : 0.0f;
         }
+        if (DADMM_ST_DELAY) {
+            pend.u = uv;
+            pend.y = yn;
+            pend.g = grc;
+            pend.su = k >= 1 ? soff : 0x80000000u;
+            pend.sy = upd ? soff : 0x80000000u;
+            pend.k = k;
+        } else {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, yn),
                                                make_rsrc(a.Y + (size_t)(upd ? k : 0) * S, (DADMM_ST_ABL & 8) ? 0u : s_bytes),
                                                upd ? soff : 0x80000000u, 0, DADMM_ST_AUX);
-        if constexpr (REC) {   // the adjoint's trajectory: Grec[k] (pre-clamp gradient), Urec[k] = U_k
+        }
+        if constexpr (REC && !DADMM_ST_DELAY) {   // the adjoint's trajectory: Grec[k] (pre-clamp gradient), Urec[k] = U_k
             const size_t kS = (size_t)(upd ? k : 0) * S;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, grc),
                                                    make_rsrc(a.Grec + kS, s_bytes), upd ? soff : 0x80000000u, 0, 0);
@@ -531,6 +576,7 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
             slot = slot == SLOTS - 1 ? 0 : slot + 1;
         }
     }
+    if (DADMM_ST_DELAY) flush();
     status |= (bad_y0 ? 1u : 0u) | (bad_u0 ? 2u : 0u) | (bad_g ? 4u : 0u) | ((bad_y || bad_h) ? 8u : 0u);
     if (a.status != nullptr) {
         uint32_t ws = status;
