@@ -563,9 +563,22 @@ constexpr int G32_STAGE = (G32_TM + TN) * 16;                  // floats per rin
 #ifndef DADMM_G32_ABL_MIX
 #define DADMM_G32_ABL_MIX 0     // timing builds only: the mix reduced to one node (wrong results)
 #endif
+// DADMM_G32_MFMA_MIX=1: the per-sample mix sum_q A_hat[p][q] Z[q] runs on v_mfma_f32_16x16x4_f32
+// instead of VALU fma: output blocks of 16 rows x 16 columns, each summing over the node range of
+// the samples its rows belong to (A_hat entries of other samples are zero: a block-diagonal
+// operand, ~1.3 samples' width per block), Z from LDS (row stride ZM = 80 floats: the four k rows
+// of a fragment read land 16 banks apart), A_hat through the vector cache. Bit-identical to the
+// VALU mix (an f32 MFMA is an fma chain in k order, and the zero entries leave it unchanged), but
+// slower: 91.9-92.0 vs 84.1-84.2 ms at the configs[4] shard forward (per-lane A_hat gathers and
+// one dependent chain per block; profiles/r04/variants_r04q_mfma_mix.txt), so off
+#ifndef DADMM_G32_MFMA_MIX
+#define DADMM_G32_MFMA_MIX 0
+#endif
+constexpr int ZM = 80;
 __host__ __device__ constexpr size_t g32_lds_bytes(int S_t, int P) {
     const size_t ring = 4 * (size_t)G32_DQ * G32_STAGE;
-    const size_t epi = 4 * ((size_t)G32_TM * ZS + (DADMM_G32_AHAT_LDS ? (((size_t)S_t * P * P + 3) & ~(size_t)3) : 0) + 4 * TN);
+    const size_t epi = DADMM_G32_MFMA_MIX ? 4 * (size_t)G32_TM * ZM
+        : 4 * ((size_t)G32_TM * ZS + (DADMM_G32_AHAT_LDS ? (((size_t)S_t * P * P + 3) & ~(size_t)3) : 0) + 4 * TN);
     return ring > epi ? ring : epi;
 }
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -671,6 +684,73 @@ __global__ __launch_bounds__(64 * G32_WAVES) void gcn32_kernel(HyperArgs a) {
         }
         lds_barrier();   // the ring's last reads before the epilogue reuses the LDS
     }
+#if DADMM_G32_MFMA_MIX
+    {
+        // Z tile [256][ZM]: acc[rb] register e = row (e & 3) + 8 (e >> 2) + 4 kh of row block rb, column fi
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                zt[(64 * wr + 32 * rb + (e & 3) + 8 * (e >> 2) + 4 * kh) * ZM + 32 * wc + fi] = acc[rb][e];
+        __syncthreads();
+        const int j = lane & 15, h = lane >> 4;
+        const int cols = a.N - col0 < TN ? a.N - col0 : TN;
+        const float* ahb = a.ahat + (a.ahat_per_sample ? (size_t)s0 * P * P : 0);
+        const int ahs = a.ahat_per_sample ? P * P : 0;
+        // 16 row blocks x 4 column blocks; wave w takes blocks w, w + 8, ...
+        for (int blk = w; blk < 64; blk += G32_WAVES) {
+            const int rb = blk >> 2, cb = blk & 3;
+            const int R0 = 16 * rb;
+            if (R0 >= rows_t || 16 * cb >= cols) continue;   // wave-uniform
+            const int slo = R0 / P, shi = min((R0 + 15) / P, ns - 1);
+            const int q0 = slo * P, q1 = (shi + 1) * P;        // the block's node range
+            // this lane's A row (tile row R0 + j) and its sample's node range
+            const int r = R0 + j;
+            const int sr = min(r / P, ns - 1);
+            const int qa = sr * P, qb = qa + P;
+            const bool rv = r < rows_t;
+            const float* arow = ahb + (size_t)sr * ahs + (size_t)(r - qa) * P - qa;   // arow[q] = A_hat[r][q - qa]
+            const int zc = 16 * cb + j;
+            f32x4 m = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (int qt = q0; qt < q1; qt += 16) {             // four k-steps per trip (wave-uniform)
+                float av[4], bv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int qq = qt + 4 * u + h;                 // k-step u's slot h
+                    av[u] = (rv && qq >= qa && qq < qb) ? arow[qq] : 0.0f;
+                    bv[u] = qq < q1 ? zt[qq * ZM + zc] : 0.0f;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) m = mfma4(av[u], bv[u], m);
+            }
+            // lane (j, h) holds rows R0 + 4 h + e of column col0 + 16 cb + j
+            const int col = col0 + zc;
+            if (col < a.N) {
+                float bias = 0.0f, bmean = 0.0f, bsc = 1.0f, bsh = 0.0f;
+                if (!a.raw) {
+                    bias = a.bias[col];
+                    bmean = a.bn_mean[col];
+                    bsc = (1.0f / sqrtf(a.bn_var[col] + a.bn_eps)) * a.bn_w[col];
+                    bsh = a.bn_b[col];
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int rr = R0 + 4 * h + e;
+                    if (rr >= rows_t) continue;
+                    float t = m[e];
+                    if (a.addend != nullptr) t = t + a.addend[(size_t)(row0 + rr) * a.ld_add + col];
+                    if (!a.raw) {
+                        t = t + bias;
+                        t = t > 0.0f ? t : t * a.slope;
+                        t = (t - bmean) * bsc + bsh;
+                    }
+                    a.y[(size_t)(row0 + rr) * a.ldy + col] = t;
+                }
+            }
+        }
+        return;
+    }
+#endif
     // Z tile: acc[rb] register e = row (e & 3) + 8 (e >> 2) + 4 kh of row block rb, column fi
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
