@@ -962,6 +962,9 @@ hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* o
                       ? prop.multiProcessorCount : 256;
         }
         const int tiles = (a.B + BT - 1) / BT;
+        // a workgroup per (agent, run of tiles) at >= one tile per wave: too few workgroups to
+        // spread over the CUs at small P x B (P = 5, B = 1024: 20) -> gram_kernel's items instead
+        if ((long)a.P * ((tiles + gnn::GL_WAVES - 1) / gnn::GL_WAVES) * 2 < cus) goto item_kernel;
         int best_s = 1;
         long best = -1;
         for (int S = 1; S <= (tiles + gnn::GL_WAVES - 1) / gnn::GL_WAVES; ++S) {
@@ -990,6 +993,7 @@ hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* o
             hipLaunchKernelGGL(gnn::gram_lds_kernel<4>, grid, block, lds, st, a, k, x_raw, out, mode, tpw);
         return hipGetLastError();
     }
+item_kernel:
     if (DADMM_GRAM_W1 && mbk <= 8) {
         const int items = ((a.B + BT - 1) / BT) * a.P;
         const int grid = (items + gnn::WAVES - 1) / gnn::WAVES;
