@@ -560,6 +560,9 @@ constexpr int G32_STAGE = (G32_TM + TN) * 16;                  // floats per rin
 #ifndef DADMM_G32_AHAT_LDS
 #define DADMM_G32_AHAT_LDS 0
 #endif
+#ifndef DADMM_G32_MIX_PF
+#define DADMM_G32_MIX_PF 1
+#endif
 #ifndef DADMM_G32_ABL_MIX
 #define DADMM_G32_ABL_MIX 0     // timing builds only: the mix reduced to one node (wrong results)
 #endif
@@ -798,7 +801,34 @@ __global__ __launch_bounds__(64 * G32_WAVES) void gcn32_kernel(HyperArgs a) {
         for (int e = 0; e < 4; ++e) at[e] = ahs + sl * ahs_stride + (4 * g + e < P ? 4 * g + e : P - 1) * P;
         const float* zc = zt + sl * P * ZS + c;
         f32x4 v[4] = {zero, zero, zero, zero};
-        for (int q = 0; q < (DADMM_G32_ABL_MIX ? 1 : P); ++q) {
+        int q = 0;
+#if DADMM_G32_MIX_PF
+        // A_hat words four nodes at a time, the next four in flight under this group's fma (the
+        // loads go through the vector cache: one dependent round trip per group without it)
+        typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+        const int P4 = DADMM_G32_ABL_MIX ? 0 : (P & ~3);
+        if (P4 > 0) {
+            f32x4 an[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) an[e] = *(const f32x4u*)at[e];
+            for (; q < P4; q += 4) {
+                f32x4 ac[4];
+                const int qn = q + 4 < P4 ? q + 4 : q;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    ac[e] = an[e];
+                    an[e] = *(const f32x4u*)(at[e] + qn);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const f32x4 z = *(const f32x4*)(zc + (q + u) * ZS);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = __builtin_elementwise_fma((f32x4)(ac[e][u]), z, v[e]);
+                }
+            }
+        }
+#endif
+        for (; q < (DADMM_G32_ABL_MIX ? 1 : P); ++q) {
             const f32x4 z = *(const f32x4*)(zc + q * ZS);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = __builtin_elementwise_fma((f32x4)(at[e][q]), z, v[e]);
