@@ -85,6 +85,9 @@ def test_recurrence_bit_exact_given_hypernetwork_outputs(cuda, mode, per_sample)
 @pytest.mark.parametrize("P,m,n,B,K", [
     (13, 40, 200, 9, 3),    # n past one 128-column update block, m = 40: a partial gram m-block
     (50, 32, 1024, 2, 2),   # BASELINE configs[4]'s agent count and signal length
+    # enough (agent, tile) work for the LDS-resident gram (gram_lds_kernel): three m-blocks (m = 40),
+    # n_pad > n, a partial last 16-sample tile and several tiles per workgroup
+    (16, 40, 200, 1990, 2),
 ])
 def test_recurrence_bit_exact_larger_shapes(cuda, P, m, n, B, K):
     """The update kernel's column blocks / agent-row pairs and the gram kernel's operand ring and
