@@ -1056,7 +1056,9 @@ static bool try_gcn32(HyperArgs& a, hipStream_t st, hipError_t& err) {
         const char* e = getenv("DADMM_GCN32");
         enabled = (e != nullptr && e[0] == '0') ? 0 : 1;
     }
-    if (!enabled || a.K1 < a.K || a.P < 1 || a.P > hyper::G32_TM) return false;
+    // (small P: linear_kernel's 160-row tiles hold 32 whole samples with little padding and the mix
+    // is short; at P = 5, B = 4096 gcn32 measured 14.2-14.3 vs 13.9 ms, profiles/r04/variants_r04v_p5.txt)
+    if (!enabled || a.K1 < a.K || a.P < 32 || a.P > hyper::G32_TM) return false;
     const int S_t = hyper::G32_TM / a.P;
     const long gm = (a.B + S_t - 1) / S_t, gn = (a.N + hyper::TN - 1) / hyper::TN;
     if (gm * gn < 256) return false;
