@@ -30,6 +30,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int THREADS = 256;
 constexpr int TN = 32, TK = 32;   // output tile (n x k) per workgroup; its waves split the rows
 constexpr int RING = 8;           // row steps (4 rows each) of operands in flight per wave
+#ifndef DADMM_WGRAD2
+#define DADMM_WGRAD2 1            // 0: wgrad_kernel (32 x 32 tiles, 16x16x4 MFMA) for A/B builds
+#endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -182,6 +185,154 @@ __global__ __launch_bounds__(64 * WV) void wgrad_kernel(WgradArgs a) {
     }
 }
 
+// ---- wgrad on 32x32x2 MFMA with coalesced row operands (round 4, the default) -------------------
+// wgrad_kernel's lanes load one float of 16-column segments (64-byte pieces) and its 32 x 32 tiles
+// cannot split the rows of the deferred batched gradients, so a 400 x 400 weight over B P K rows
+// ran on 169 workgroups: the gradients took ~40 % of the B = 4096 training step. Here: 64 x 64
+// output tiles, 4 waves each owning the whole tile (four 32x32 accumulators: 4096 flop per MFMA,
+// 16 flop per operand byte) over interleaved row-pair steps; lane (i, kh) of a step reads row
+// 2 s + kh of dZ and X at columns c0 + i and c0 + 32 + i, so each half-wave load is one contiguous
+// 128-byte row segment. The rows split over S workgroups per tile (partial tiles in scratch, added
+// in split order by reduce_kernel: deterministic); the four waves' partials add through LDS in a
+// fixed tree. The bias column sums come from the same dZ reads (k-tile 0).
+constexpr int W2_T = 64, W2_WAVES = 4, W2_RING = 8;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(64 * W2_WAVES) void wgrad2_kernel(WgradArgs a) {
+    __shared__ float red[2][4 * 16 + 1][64];          // two waves' partial tiles (+ bias) per tree level
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = lane & 31, kh = lane >> 5;
+    const int gn = (a.N + W2_T - 1) / W2_T, gk = (a.K + W2_T - 1) / W2_T;
+    const int tl = xcd_tile(blockIdx.x, gridDim.x);
+    const int kt = tl % gk, nt = (tl / gk) % gn, split = tl / (gk * gn);
+    const int n0 = nt * W2_T, k0 = kt * W2_T;
+    const int spb = (a.R + 1) / 2;                    // row-pair steps per batch block
+    const int steps = spb * a.nb;
+    const int per = (steps + a.splits - 1) / a.splits;
+    const int s_begin = split * per;
+    const int s_end = s_begin + per < steps ? s_begin + per : steps;
+
+    // this lane's operand columns (clamped: columns past N / K compute garbage, never stored)
+    int nc[2];
+    const float* xs[2];
+    int ldx[2];
+    size_t sx[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int n = n0 + 32 * b + i;
+        nc[b] = n < a.N ? n : a.N - 1;
+        int k = k0 + 32 * b + i;
+        k = k < a.K ? k : a.K - 1;
+        if (k < a.K1) {
+            xs[b] = a.x1 + k;
+            ldx[b] = a.ld1;
+            sx[b] = a.s1;
+        } else {
+            xs[b] = a.x2 + (k - a.K1);
+            ldx[b] = a.ld2;
+            sx[b] = a.s2;
+        }
+    }
+    const bool do_bias = a.gbias != nullptr && kt == 0;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.0f;
+    float bsum[2] = {0.0f, 0.0f};
+    float ra[W2_RING][2], rb[W2_RING][2];
+    auto load = [&](int u, int st) {
+        const int bb = a.nb > 1 ? st / spb : 0;
+        const int r = 2 * (st - bb * spb) + kh;
+        const bool ok = st < s_end && r < a.R;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            ra[u][b] = ok ? a.dz[(size_t)bb * a.zs + (size_t)r * a.ldz + nc[b]] : 0.0f;
+            rb[u][b] = ok ? xs[b][(size_t)bb * sx[b] + (size_t)r * ldx[b]] : 0.0f;
+        }
+    };
+    const int first = s_begin + w;
+#pragma unroll
+    for (int u = 0; u < W2_RING; ++u) load(u, first + W2_WAVES * u);
+    for (int st = first; st < s_end; st += W2_WAVES * W2_RING) {
+#pragma unroll
+        for (int u = 0; u < W2_RING; ++u) {
+            if (st + W2_WAVES * u < s_end) {
+#pragma unroll
+                for (int x = 0; x < 2; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y) acc[x][y] = mfma32(ra[u][x], rb[u][y], acc[x][y]);
+                if (do_bias) {
+                    bsum[0] += ra[u][0];
+                    bsum[1] += ra[u][1];
+                }
+            }
+            load(u, st + W2_WAVES * (u + W2_RING));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // bias: the wave's two row halves (lanes i and i + 32), in order
+#pragma unroll
+    for (int b = 0; b < 2; ++b) bsum[b] = bsum[b] + __shfl_down(bsum[b], 32);
+    // lane (i, kh) carries column n0 + 32 kh + i (lanes 0..31 hold both halves' sums)
+    const float b1 = __shfl(bsum[1], i);
+    float bcol = kh ? b1 : bsum[0];
+    // fixed pairwise tree over the waves (wave w adds wave w + half's partials)
+#pragma unroll
+    for (int half = W2_WAVES / 2; half >= 1; half /= 2) {
+        if (w >= half && w < 2 * half) {
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) red[w - half][(2 * x + y) * 16 + e][lane] = acc[x][y][e];
+            red[w - half][64][lane] = bcol;
+        }
+        __syncthreads();
+        if (w < half) {
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) acc[x][y][e] += red[w][(2 * x + y) * 16 + e][lane];
+            bcol += red[w][64][lane];
+        }
+        __syncthreads();
+    }
+    if (w > 0) return;
+    // acc[x][y] register e: G row n0 + 32 x + (e & 3) + 8 (e >> 2) + 4 kh, column k0 + 32 y + i
+    float* out = a.splits > 1 ? a.scratch + (size_t)split * a.N * a.K : a.g;
+    const bool accum = a.splits == 1 && a.beta != 0;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            const int k = k0 + 32 * y + i;
+            if (k >= a.K) continue;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int n = n0 + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * kh;
+                if (n >= a.N) continue;
+                float* o = out + (size_t)n * a.K + k;
+                *o = accum ? *o + acc[x][y][e] : acc[x][y][e];
+            }
+        }
+    if (do_bias) {
+        const int n = n0 + 32 * kh + i;
+        if (n < a.N) {
+            if (a.splits > 1) a.scratch_bias[(size_t)split * a.N + n] = bcol;
+            else a.gbias[n] = a.beta != 0 ? a.gbias[n] + bcol : bcol;
+        }
+    }
+}
+
 // dst[i] (+)= sum_s src[s][i], s in order
 __global__ __launch_bounds__(THREADS) void reduce_kernel(const float* __restrict__ src, int splits, size_t count,
                                                          float* __restrict__ dst, int beta) {
@@ -262,6 +413,14 @@ int wgrad_waves(int tiles) { return tiles >= 256 ? 4 : tiles >= 128 ? 8 : 16; }
 }
 
 int wgrad_splits(int R, int N, int K) {
+    if (DADMM_WGRAD2) {
+        // 64 x 64 tiles; rows split until ~4 workgroups per CU or each wave walks < 64 row pairs
+        const long tiles = (long)((N + hgrad::W2_T - 1) / hgrad::W2_T) * ((K + hgrad::W2_T - 1) / hgrad::W2_T);
+        const long steps = ((long)R + 1) / 2;
+        int s = 1;
+        while (tiles * s * 2 <= 1024 && steps / (hgrad::W2_WAVES * s * 2) >= 64 && s < 64) s *= 2;
+        return s;
+    }
     const int tiles = ((N + hgrad::TN - 1) / hgrad::TN) * ((K + hgrad::TK - 1) / hgrad::TK);
     const int steps = (R + 3) / 4;
     const int wv = wgrad_waves(tiles);
@@ -273,12 +432,17 @@ int wgrad_splits(int R, int N, int K) {
 }
 
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st) {
+    if (DADMM_WGRAD2) {
+        const int tiles = ((a.N + hgrad::W2_T - 1) / hgrad::W2_T) * ((a.K + hgrad::W2_T - 1) / hgrad::W2_T);
+        hipLaunchKernelGGL(hgrad::wgrad2_kernel, dim3(tiles * a.splits), dim3(64 * hgrad::W2_WAVES), 0, st, a);
+    } else {
     const int tiles = ((a.N + hgrad::TN - 1) / hgrad::TN) * ((a.K + hgrad::TK - 1) / hgrad::TK);
     const dim3 grid(tiles * a.splits);
     switch (wgrad_waves(tiles)) {
         case 4: hipLaunchKernelGGL(hgrad::wgrad_kernel<4>, grid, dim3(256), 0, st, a); break;
         case 8: hipLaunchKernelGGL(hgrad::wgrad_kernel<8>, grid, dim3(512), 0, st, a); break;
         default: hipLaunchKernelGGL(hgrad::wgrad_kernel<16>, grid, dim3(1024), 0, st, a); break;
+    }
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || a.splits == 1) return e;

@@ -301,21 +301,48 @@ int dadmm_hyper_train_backward_deferred(const dadmm_hyper_net* net, int32_t B, c
                           stream);
 }
 
+// the (R, N, K) of every batched weight gradient of one deferred pass, in launch order
+extern "C++" template <class F>
+static int for_each_wgrad(const dadmm_hyper_net* net, int32_t B, F&& f) {
+    const int P = net->P, n = net->n, rows = B * P, H4 = 4 * net->H;
+    TRY(f(B, H4, net->dec_width[2]));
+    for (int j = 2; j >= 0; --j) TRY(f(B, net->dec_width[j], j > 0 ? net->dec_width[j - 1] : P * net->width[4]));
+    for (int i = 4; i >= 0; --i) TRY(f(rows, net->width[i], i > 0 ? net->width[i - 1] : 2 * n));
+    return DADMM_OK;
+}
+
+size_t dadmm_hyper_train_wgrad_scratch_bytes(const dadmm_hyper_net* net, int32_t B, int32_t iters) {
+    if (!net || B < 1 || iters < 1) return 0;
+    size_t best = 0;
+    for_each_wgrad(net, B, [&](int R, int N, int K) -> int {
+        const int s = dadmm::wgrad_splits(R * iters, N, K);
+        const size_t b = s > 1 ? 4 * (size_t)s * N * (K + 1) : 0;
+        best = b > best ? b : best;
+        return DADMM_OK;
+    });
+    return best;
+}
+
 int dadmm_hyper_train_wgrad(const dadmm_hyper_net* net, int32_t B, int32_t iters, const float* AtAy,
                             int64_t atay_stride, const float* Atb, const dadmm_hyper_saved* sv0, int64_t sv_stride,
-                            const float* dsave, int64_t dsave_stride, const dadmm_hyper_grads* g, void* stream) {
+                            const float* dsave, int64_t dsave_stride, const dadmm_hyper_grads* g, void* scratch,
+                            void* stream) {
     if (check_net(net, B) != DADMM_OK || iters < 0 || !AtAy || !Atb || !sv0 || !dsave || !g) return DADMM_EINVAL;
     if (B == 0 || iters == 0) return DADMM_OK;
     if (net->n & 15) return DADMM_EUNSUPPORTED;
+    if (scratch && ((uintptr_t)scratch & 15)) return DADMM_EINVAL;
     DSave d;
     dsave_layout(net, B, &d, const_cast<float*>(dsave));
     const int P = net->P, n = net->n, rows = B * P, H4 = 4 * net->H;
     const hipStream_t st = (hipStream_t)stream;
-    // one batched weight gradient: nb = iters blocks, no row splits (no scratch)
+    // one batched weight gradient: nb = iters blocks; the rows split over workgroups when a scratch
+    // (dadmm_hyper_train_wgrad_scratch_bytes) is given, partials added in split order
     auto wg = [&](int R, int N, int K, const float* dz, int ldz, const float* x1, int ld1, int K1, size_t s1,
                   const float* x2, int ld2, size_t s2, float* gw, float* gb) -> int {
-        dadmm::WgradArgs a{dz, x1, K1 < K ? x2 : x1, gw, gb, nullptr, nullptr, R, N, K, K1, ldz, ld1,
-                           K1 < K ? ld2 : ld1, 1, 1};
+        const int S = scratch ? dadmm::wgrad_splits(R * iters, N, K) : 1;
+        float* part = S > 1 ? (float*)scratch : nullptr;
+        dadmm::WgradArgs a{dz, x1, K1 < K ? x2 : x1, gw, gb, part, S > 1 ? part + (size_t)S * N * K : nullptr,
+                           R, N, K, K1, ldz, ld1, K1 < K ? ld2 : ld1, S, 1};
         a.nb = iters;
         a.zs = (size_t)dsave_stride;
         a.s1 = s1;

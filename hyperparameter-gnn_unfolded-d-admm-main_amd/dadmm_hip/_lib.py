@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "dadmm_hyper_train_dsave_floats",
     "dadmm_hyper_train_backward_deferred",
     "dadmm_hyper_train_wgrad",
+    "dadmm_hyper_train_wgrad_scratch_bytes",
     "dadmm_gnn_flag_bytes",
     "dadmm_gnn_begin",
     "dadmm_gnn_gram",
@@ -244,7 +245,9 @@ def load() -> ctypes.CDLL:
     L.dadmm_hyper_train_wgrad.restype = ctypes.c_int
     L.dadmm_hyper_train_wgrad.argtypes = [ctypes.POINTER(HyperNet), i32, i32, vp, ctypes.c_int64, vp,
                                           ctypes.POINTER(HyperSaved), ctypes.c_int64, vp, ctypes.c_int64,
-                                          ctypes.POINTER(HyperGrads), vp]
+                                          ctypes.POINTER(HyperGrads), vp, vp]
+    L.dadmm_hyper_train_wgrad_scratch_bytes.restype = ctypes.c_size_t
+    L.dadmm_hyper_train_wgrad_scratch_bytes.argtypes = [ctypes.POINTER(HyperNet), i32, i32]
     # training-mode parameter gradients (csrc/dadmm_hyper_grad.hip)
     L.dadmm_hyper_wgrad_scratch_bytes.restype = ctypes.c_size_t
     L.dadmm_hyper_wgrad_scratch_bytes.argtypes = [i32, i32, i32]

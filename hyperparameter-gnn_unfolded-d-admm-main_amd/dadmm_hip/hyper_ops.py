@@ -559,6 +559,7 @@ class NativeHyperPlan:
             raise ValueError("dadmm_hyper_train_work_bytes: hypernetwork dimensions not supported")
         self.work = torch.empty(nbytes // 4 + 4, device=dev)
         self.dAtAy = None
+        self.wscratch = None
         self.dsave_per = L.dadmm_hyper_train_dsave_floats(ctypes.byref(net), B)   # floats, multiple of 4
 
     @staticmethod
@@ -627,10 +628,14 @@ class NativeHyperPlan:
         """Add the parameter gradients of ``iters`` deferred iterations (As [iters, B, P, ns], the
         saved blocks of ``arena``, the operand blocks of ``dsave``) into ``g``'s accumulators."""
         assert As.is_contiguous() and As.shape[0] >= iters
+        nbytes = self.L.dadmm_hyper_train_wgrad_scratch_bytes(ctypes.byref(self.net), self.B, iters)
+        if nbytes and (self.wscratch is None or 4 * self.wscratch.numel() < nbytes):
+            self.wscratch = torch.empty(nbytes // 4, device=self.dev)   # row-split partials, grown
+        scr = self.wscratch if nbytes else None
         _lib.check("dadmm_hyper_train_wgrad", self.L.dadmm_hyper_train_wgrad(
             ctypes.byref(self.net), self.B, iters, _ptr(As), As[0].numel(), _ptr(Atb),
             ctypes.byref(self.saved(arena, 0)), self.per, _ptr(dsave), self.dsave_per, ctypes.byref(g),
-            stream))
+            _ptr(scr), stream))
 
 
 def _native_forward(ctx, L, AtAy, Atb, ahat, model, n, per_sample, seed, defer):

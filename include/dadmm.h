@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 13
+#define DADMM_ABI_VERSION 14
 
 enum {
     DADMM_OK = 0,
@@ -551,7 +551,12 @@ int dadmm_hyper_train_backward_deferred(const dadmm_hyper_net* net, int32_t B, c
 int dadmm_hyper_train_wgrad(const dadmm_hyper_net* net, int32_t B, int32_t iters, const float* AtAy,
                             int64_t atay_stride, const float* Atb, const dadmm_hyper_saved* sv0,
                             int64_t sv_stride, const float* dsave, int64_t dsave_stride,
-                            const dadmm_hyper_grads* g, void* stream);
+                            const dadmm_hyper_grads* g, void* scratch, void* stream);
+/* Row-split scratch of dadmm_hyper_train_wgrad (ABI 14): with `scratch` of at least this many bytes
+ * (16-byte aligned) each weight gradient's rows spread over several workgroups per output tile and
+ * the partials are added in a fixed order (deterministic); with scratch == NULL one workgroup walks
+ * every row of its tile. 0 when no gradient splits. */
+size_t dadmm_hyper_train_wgrad_scratch_bytes(const dadmm_hyper_net* net, int32_t B, int32_t iters);
 
 #ifdef __cplusplus
 }

@@ -44,9 +44,9 @@ def _keep(seed, site, rows, cols, p, dev):
     return torch.from_numpy((_drop_hash(seed, site, rows, cols) >= thr).astype(np.float32)).to(dev)
 
 
-def _model(dev, P, n, hidden, mode, seed=0):
+def _model(dev, P, n, hidden, mode, seed=0, B=64):
     import gnn_dlasso_models_progressive as G
-    A, b, _ = O.make_problem(P, 16, n, 64, seed=seed + 5)
+    A, b, _ = O.make_problem(P, 16, n, max(B, 64), seed=seed + 5)
     torch.manual_seed(seed)
     args = argparse.Namespace(GHN_iter_num=3, GHyp_hidden=hidden, DADMM_mode=mode, alpha_max=0.1,
                               tau_max=0.99, rho_max=0.99, eta_max=0.99)
@@ -326,7 +326,7 @@ def test_wgrad_colsum_transpose_kernels(cuda, R, N, K, K1, beta):
 def _train_pair(cuda, P, n, hidden, mode, shared, B=12, seed=11):
     """(HIP model, torch-backend copy) with dropout off, graphs, inits, b and a label."""
     import copy
-    model, A, b = _model(cuda, P, n, hidden, mode, seed=seed)
+    model, A, b = _model(cuda, P, n, hidden, mode, seed=seed, B=B)
     for mod in [model.encoder.dropout] + [model.decoder[i] for i in (1, 5, 9)]:
         mod.p = 0.0
     ref = copy.deepcopy(model)
@@ -369,6 +369,31 @@ def test_whole_forward_node_modes(cuda, mode, shared):
     l2.backward()
     for (name, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
         assert p1.grad is not None, name
+        _close(p1.grad, p2.grad, rel=5e-3, name=name)
+
+
+def test_whole_forward_node_split_weight_gradients(cuda):
+    """At B = 256, K = 4 the deferred weight gradients (dadmm_hyper_train_wgrad over rows x iters)
+    split their rows over several workgroups per output tile (the plan's row-split scratch is
+    allocated): the gradients still equal the torch backend's, and a second pass gives the same
+    bits (the partials are added in a fixed order)."""
+    import gnn_dlasso_utils as U
+    from dadmm_hip import hyper_ops
+    P, n, hidden, K, B = 5, 32, 8, 4, 256
+    model, ref, graphs, inits, bt, label = _train_pair(cuda, P, n, hidden, "diff", False, B=B)
+    grads = []
+    for _ in range(2):
+        model.zero_grad()
+        Y1, _ = model(bt, graphs, K, inits=inits)
+        U.compute_loss(Y1, label)[1].backward()
+        grads.append([p.grad.clone() for p in model.parameters()])
+    plans = hyper_ops._cache(model)["plans"]
+    assert any(pl.wscratch is not None for pl in plans.values())
+    for g1, g2 in zip(*grads):
+        assert torch.equal(g1, g2)
+    Y2, _ = ref(bt, graphs, K, inits=inits)
+    U.compute_loss(Y2, label)[1].backward()
+    for (name, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
         _close(p1.grad, p2.grad, rel=5e-3, name=name)
 
 
