@@ -209,11 +209,13 @@ __global__ __launch_bounds__(64 * W2_WAVES) void wgrad2_kernel(WgradArgs a) {
     const int tl = xcd_tile(blockIdx.x, gridDim.x);
     const int kt = tl % gk, nt = (tl / gk) % gn, split = tl / (gk * gn);
     const int n0 = nt * W2_T, k0 = kt * W2_T;
-    const int spb = (a.R + 1) / 2;                    // row-pair steps per batch block
+    // rows in full pairs; an odd R leaves each block's last row to the tail below
+    const int spb = a.R / 2;                          // row-pair steps per batch block
     const int steps = spb * a.nb;
     const int per = (steps + a.splits - 1) / a.splits;
     const int s_begin = split * per;
     const int s_end = s_begin + per < steps ? s_begin + per : steps;
+    const int wv = __builtin_amdgcn_readfirstlane(w);
 
     // this lane's operand columns (clamped: columns past N / K compute garbage, never stored)
     int nc[2];
@@ -245,35 +247,90 @@ __global__ __launch_bounds__(64 * W2_WAVES) void wgrad2_kernel(WgradArgs a) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.0f;
     float bsum[2] = {0.0f, 0.0f};
-    float ra[W2_RING][2], rb[W2_RING][2];
-    auto load = [&](int u, int st) {
-        const int bb = a.nb > 1 ? st / spb : 0;
-        const int r = 2 * (st - bb * spb) + kh;
-        const bool ok = st < s_end && r < a.R;
+    auto consume = [&](const float (&za)[2], const float (&xb)[2]) {
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            ra[u][b] = ok ? a.dz[(size_t)bb * a.zs + (size_t)r * a.ldz + nc[b]] : 0.0f;
-            rb[u][b] = ok ? xs[b][(size_t)bb * sx[b] + (size_t)r * ldx[b]] : 0.0f;
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) acc[x][y] = mfma32(za[x], xb[y], acc[x][y]);
+        if (do_bias) {
+            bsum[0] += za[0];
+            bsum[1] += za[1];
         }
     };
-    const int first = s_begin + w;
+    // The load cursor: the lane's four operand pointers at row 2 loc + kh of batch block bb, the
+    // wave's next load step. Every load of the ring is unconditional from a valid row (the cursor
+    // stays on the last step of the range once it gets there; those slots are never consumed), so
+    // the compiler keeps one wait per slot instead of a full drain per step; the cursor moves by a
+    // pointer add per operand, a block change (uniform branch) re-seeks.
+    const float* pz[2];
+    const float* px[2];
+    int lbb = 0, lloc = 0, lst = 0;
+    auto seek = [&](int st) {
+        lst = st;
+        lbb = st / spb;
+        lloc = st - lbb * spb;
+        const size_t r = (size_t)(2 * lloc + kh);
 #pragma unroll
-    for (int u = 0; u < W2_RING; ++u) load(u, first + W2_WAVES * u);
-    for (int st = first; st < s_end; st += W2_WAVES * W2_RING) {
+        for (int b = 0; b < 2; ++b) {
+            pz[b] = a.dz + (size_t)lbb * a.zs + r * a.ldz + nc[b];
+            px[b] = xs[b] + (size_t)lbb * sx[b] + r * ldx[b];
+        }
+    };
+    auto advance = [&]() {
+        if (lst + W2_WAVES >= s_end) return;          // stay on the last step of the range
+        lst += W2_WAVES;
+        lloc += W2_WAVES;
+        if (lloc >= spb) {
+            seek(lst);
+        } else {
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                pz[b] += (size_t)(2 * W2_WAVES) * a.ldz;
+                px[b] += (size_t)(2 * W2_WAVES) * ldx[b];
+            }
+        }
+    };
+    const int first = s_begin + wv;
+    if (first < s_end) {
+        float ra[W2_RING][2], rb[W2_RING][2];
+        seek(first);
 #pragma unroll
         for (int u = 0; u < W2_RING; ++u) {
-            if (st + W2_WAVES * u < s_end) {
 #pragma unroll
-                for (int x = 0; x < 2; ++x)
-#pragma unroll
-                    for (int y = 0; y < 2; ++y) acc[x][y] = mfma32(ra[u][x], rb[u][y], acc[x][y]);
-                if (do_bias) {
-                    bsum[0] += ra[u][0];
-                    bsum[1] += ra[u][1];
-                }
+            for (int b = 0; b < 2; ++b) {
+                ra[u][b] = *pz[b];
+                rb[u][b] = *px[b];
             }
-            load(u, st + W2_WAVES * (u + W2_RING));
+            advance();
             __builtin_amdgcn_sched_barrier(0);
+        }
+        for (int st = first; st < s_end; st += W2_WAVES * W2_RING) {
+#pragma unroll
+            for (int u = 0; u < W2_RING; ++u) {
+                if (st + W2_WAVES * u < s_end) consume(ra[u], rb[u]);
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    ra[u][b] = *pz[b];
+                    rb[u][b] = *px[b];
+                }
+                advance();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    // odd R: each block's last row (split 0, the waves taking blocks in turn; the kh = 1 half of
+    // the step is that row again with dZ zeroed)
+    if ((a.R & 1) && split == 0) {
+        for (int bb = wv; bb < a.nb; bb += W2_WAVES) {
+            const size_t r = (size_t)(a.R - 1);
+            float za[2], xb[2];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                za[b] = a.dz[(size_t)bb * a.zs + r * a.ldz + nc[b]];
+                xb[b] = xs[b][(size_t)bb * sx[b] + r * ldx[b]];
+                za[b] = kh ? 0.0f : za[b];
+            }
+            consume(za, xb);
         }
     }
     // bias: the wave's two row halves (lanes i and i + 32), in order

@@ -372,15 +372,25 @@ def test_whole_forward_node_modes(cuda, mode, shared):
         _close(p1.grad, p2.grad, rel=5e-3, name=name)
 
 
-def test_whole_forward_node_split_weight_gradients(cuda):
-    """At B = 256, K = 4 the deferred weight gradients (dadmm_hyper_train_wgrad over rows x iters)
-    split their rows over several workgroups per output tile (the plan's row-split scratch is
-    allocated): the gradients still equal the torch backend's, and a second pass gives the same
-    bits (the partials are added in a fixed order)."""
+@pytest.mark.parametrize("B", [256, 51])
+def test_whole_forward_node_split_weight_gradients(cuda, B):
+    """The deferred weight gradients (dadmm_hyper_train_wgrad over rows x iterations, one launch
+    per parameter) against the per-iteration ones (an on_hyp hook selects HyperTrainFn, whose
+    backward adds each iteration's gradients as it goes): the same dZ operands summed in another
+    order, so they agree to f32 rounding of the sums. At B = 256, K = 4 the rows split over several
+    workgroups per output tile (the plan's row-split scratch is allocated); at B = 51 every batch
+    block has an odd row count (255 rows: the kernel's odd-row tail per block). A second pass gives
+    the same bits (the partials are added in a fixed order); at B = 256 the gradients also equal
+    the torch backend's. (At B = 51, K = 4 both HIP paths sit 1e-2 from torch: a sample whose
+    five-node BatchNorm amplifies f32 rounding, not a kernel difference.)"""
+    import copy
+
     import gnn_dlasso_utils as U
     from dadmm_hip import hyper_ops
-    P, n, hidden, K, B = 5, 32, 8, 4, 256
+    P, n, hidden, K = 5, 32, 8, 4
     model, ref, graphs, inits, bt, label = _train_pair(cuda, P, n, hidden, "diff", False, B=B)
+    per_iter = copy.deepcopy(model)
+    per_iter.on_hyp = lambda *a: None
     grads = []
     for _ in range(2):
         model.zero_grad()
@@ -388,13 +398,19 @@ def test_whole_forward_node_split_weight_gradients(cuda):
         U.compute_loss(Y1, label)[1].backward()
         grads.append([p.grad.clone() for p in model.parameters()])
     plans = hyper_ops._cache(model)["plans"]
-    assert any(pl.wscratch is not None for pl in plans.values())
+    assert any(pl.wscratch is not None for pl in plans.values()) or B < 256
     for g1, g2 in zip(*grads):
         assert torch.equal(g1, g2)
-    Y2, _ = ref(bt, graphs, K, inits=inits)
-    U.compute_loss(Y2, label)[1].backward()
-    for (name, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
-        _close(p1.grad, p2.grad, rel=5e-3, name=name)
+    Y3, _ = per_iter(bt, graphs, K, inits=inits)
+    assert torch.equal(Y1, Y3)
+    U.compute_loss(Y3, label)[1].backward()
+    for (name, p1), (_, p3) in zip(model.named_parameters(), per_iter.named_parameters()):
+        _close(p1.grad, p3.grad, rel=2e-5, name=name)
+    if B == 256:
+        Y2, _ = ref(bt, graphs, K, inits=inits)
+        U.compute_loss(Y2, label)[1].backward()
+        for (name, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
+            _close(p1.grad, p2.grad, rel=5e-3, name=name)
 
 
 def test_whole_forward_node_accumulates_and_respects_frozen(cuda):
