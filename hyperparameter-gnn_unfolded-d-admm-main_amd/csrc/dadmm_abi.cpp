@@ -392,6 +392,20 @@ int dadmm_gnn_gram(const dadmm_dims* d, const void* op, int32_t k, float* const*
     return hip_rc(dadmm::gnn_launch_gram(a, k, x, out, 0, (hipStream_t)stream), "gram launch");
 }
 
+int dadmm_gnn_gram_acc(const dadmm_dims* d, const void* op, const float* x, float* out, void* stream) {
+    dadmm::GnnArgs a;
+    int rc = gnn_common(d, &a);
+    if (rc) return rc;
+    if (d->B == 0) return ok();
+    if (!op || !out || !x) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(op) || !aligned16(out) || !aligned16(x))
+        return fail(DADMM_EINVAL, "op, x and out must be 16-byte aligned");
+    if (dadmm::gnn_gram_lds(a.m_pad) > 160 * 1024)
+        return fail(DADMM_EUNSUPPORTED, "m=%d too large for the gram tile", d->m);
+    set_op(&a, op);
+    return hip_rc(dadmm::gnn_launch_gram(a, 0, x, out, 2, (hipStream_t)stream), "gram launch");
+}
+
 int dadmm_gnn_step(const dadmm_dims* d, int32_t k, const int32_t* visit_ptr, const uint8_t* visit_q,
                    const float* deg, const float* hyp_k, float* const* yptr, const float* AtAy,
                    const float* Atb, const float* U, const float* D, float* U_next, float* D_next,

@@ -42,6 +42,32 @@ __device__ __forceinline__ float4 normal4(hiprandStatePhilox4_32_10_t* st) {
     return make_float4(a.x, a.y, b.x, b.y);
 }
 
+// DADMM_RNG_DIRECT: the Philox counter of draw `it` of virtual thread idx is formed directly
+// (rocrand's engine state after hiprand_init(seed, idx, offset) and `it` next4() calls: counter =
+// (offset / 4 + it, subsequence idx) as a 128-bit sum, key = seed) and its ten rounds evaluated
+// once. hiprand4 also evaluates the NEXT counter eagerly after each call, one Philox of four per
+// thread that no element uses; and the last draw's second Box-Muller pair is skipped when none of
+// its elements exists. Same words, same floats (offset % 4 == 0, so next4 never interleaves).
+#ifndef DADMM_RNG_DIRECT
+#define DADMM_RNG_DIRECT 1
+#endif
+
+__device__ __forceinline__ uint4 philox_round(uint4 c, uint2 k) {
+    const unsigned hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const unsigned hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    return make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+}
+
+__device__ __forceinline__ uint4 philox10(uint4 c, uint2 k) {
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+        c = philox_round(c, k);
+        k.x += 0x9E3779B9u;   // ROCRAND_PHILOX_W32_0
+        k.y += 0xBB67AE85u;   // ROCRAND_PHILOX_W32_1
+    }
+    return philox_round(c, k);
+}
+
 // 32-bit index arithmetic (numel < 2^31 is checked by the launcher): the 64-bit divisions of a
 // straightforward port cost more than the Philox rounds themselves.
 template <bool PADDED>
@@ -54,25 +80,48 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
     if (t >= 3) return;
     const uint32_t idx = gid - t * T;
     float* out = t == 0 ? a.y0 : (t == 1 ? a.U0 : a.d0);
-    hiprandStatePhilox4_32_10_t st;
-    hiprand_init(a.seed, (unsigned long long)idx, a.offset + (uint64_t)t * a.offset_step, &st);
     const uint32_t numel = (uint32_t)a.numel, n = (uint32_t)a.n, ns = (uint32_t)a.n_store;
     const uint32_t iters = (numel - 1) / (T * 4) + 1;
+    auto put = [&](uint32_t li, float v) {
+        uint32_t o = li;
+        if (PADDED) {
+            const uint32_t row = li / n;
+            o = row * ns + (li - row * n);
+        }
+        // transformation::normal (val * std + mean), contracted as torch's build does
+        out[o] = __builtin_fmaf(v, a.stddev, a.mean);
+    };
+    if (DADMM_RNG_DIRECT) {
+        // counter after discard_subsequence(idx) then discard(offset): (x, y) = offset / 4,
+        // (z, w) = idx plus the carry out of y
+        const uint64_t c0 = (a.offset + (uint64_t)t * a.offset_step) / 4;
+        const uint2 key = make_uint2((unsigned)a.seed, (unsigned)(a.seed >> 32));
+        uint32_t li = idx;
+        for (uint32_t it = 0; it < iters; ++it, li += 4 * T) {
+            const uint64_t cx = c0 + it;                      // the counter's low 64 bits
+            const unsigned carry = cx < c0 ? 1u : 0u;         // into the subsequence words
+            const uint4 r = philox10(make_uint4((unsigned)cx, (unsigned)(cx >> 32), idx + carry,
+                                                (idx + carry < idx) ? 1u : 0u), key);
+            const float2 p0 = box_muller(r.x, r.y);
+            if (li < numel) put(li, p0.x);
+            if (li + T < numel) put(li + T, p0.y);
+            if (li + 2 * T < numel) {
+                const float2 p1 = box_muller(r.z, r.w);
+                put(li + 2 * T, p1.x);
+                if (li + 3 * T < numel) put(li + 3 * T, p1.y);
+            }
+        }
+        return;
+    }
+    hiprandStatePhilox4_32_10_t st;
+    hiprand_init(a.seed, (unsigned long long)idx, a.offset + (uint64_t)t * a.offset_step, &st);
     uint32_t li = idx;
     for (uint32_t it = 0; it < iters; ++it) {
         const float4 r = normal4(&st);
         const float v[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii, li += T) {
-            if (li < numel) {
-                uint32_t o = li;
-                if (PADDED) {
-                    const uint32_t row = li / n;
-                    o = row * ns + (li - row * n);
-                }
-                // transformation::normal (val * std + mean), contracted as torch's build does
-                out[o] = __builtin_fmaf(v[ii], a.stddev, a.mean);
-            }
+            if (li < numel) put(li, v[ii]);
         }
     }
 }

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -62,6 +62,7 @@ EXPORTED_SYMBOLS = (
     "dadmm_gnn_flag_bytes",
     "dadmm_gnn_begin",
     "dadmm_gnn_gram",
+    "dadmm_gnn_gram_acc",
     "dadmm_gnn_step",
     "dadmm_gnn_finish",
     "dadmm_gnn_step_backward",
@@ -191,6 +192,7 @@ def load() -> ctypes.CDLL:
     L.dadmm_gnn_flag_bytes.argtypes = [i32]
     for name, args in (("dadmm_gnn_begin", [D] + [vp] * 7),
                        ("dadmm_gnn_gram", [D, vp, i32] + [vp] * 5),
+                       ("dadmm_gnn_gram_acc", [D] + [vp] * 4),
                        ("dadmm_gnn_step", [D, i32] + [vp] * 14),
                        ("dadmm_gnn_finish", [D] + [vp] * 4),
                        ("dadmm_gnn_step_backward", [D, i32] + [vp] * 18)):

@@ -70,6 +70,14 @@ class GnnRun:
                 _ptr(x), _ptr(out), _stream(self.dev)))
         return out
 
+    def gram_acc(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """out += A^T A x in one launch (== out.add_(self.gram(0, x=x)), bit for bit)."""
+        x = _pad_n(x.float(), self.op.n_store).contiguous()
+        with torch.cuda.device(self.dev):
+            _lib.check("dadmm_gnn_gram_acc", self.L.dadmm_gnn_gram_acc(
+                ctypes.byref(self.d), _ptr(self.op.workspace), _ptr(x), _ptr(out), _stream(self.dev)))
+        return out
+
     def step(self, k: int, AtAy, hyp_k, U, D):
         """One iteration; returns (y_{k+1}, U_{k+1}, delta_{k+1})."""
         g = self.graphs
@@ -232,7 +240,7 @@ class GnnTrainFn(torch.autograd.Function):
                 if k == 0:   # y_0, U_0, delta_0 are the random inits: no gradient
                     break
                 gA.add_(dA)
-                gy.add_(run.gram(0, x=gA))
+                run.gram_acc(gA, gy)
                 if gY is not None:
                     gy.add_(gY[k - 1])
                 gy1, gU1, gd1 = gy, gU, gd

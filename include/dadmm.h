@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 14
+#define DADMM_ABI_VERSION 15
 
 enum {
     DADMM_OK = 0,
@@ -299,6 +299,9 @@ int dadmm_gnn_begin(const dadmm_dims* d, const void* op, const float* b, const f
  * explicit x [B][P][n] (the adjoint of AtAy; flags / yptr unused then). */
 int dadmm_gnn_gram(const dadmm_dims* d, const void* op, int32_t k, float* const* yptr,
                    const int32_t* flags, const float* x, float* out, void* stream);
+/* out += A^T (A x) (ABI 15): the GNN adjoint's y gradient picks up the gram of the AtAy gradient
+ * in one launch instead of a gram and an add (bit-identical: out + the gram's value, one rounding). */
+int dadmm_gnn_gram_acc(const dadmm_dims* d, const void* op, const float* x, float* out, void* stream);
 /* One iteration: reads y_k (resolved), U_k (U, reset by the guard), delta_k (D), AtAy_k, Atb and
  * hyp_k [B][4][H]; writes y_{k+1} to yptr[k+1], U_{k+1} to U_next, delta_{k+1} to D_next.
  * G: [B][P][n] scratch. */

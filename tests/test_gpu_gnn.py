@@ -239,6 +239,28 @@ def test_features_are_the_reference_gram_and_atb(cuda):
     np.testing.assert_allclose(Atb.cpu().numpy(), want_b, rtol=1e-4, atol=1e-4 * np.abs(want_b).max())
 
 
+@pytest.mark.parametrize("P,m,n,B", [(4, 24, 48, 10), (16, 32, 256, 96), (50, 32, 1024, 40)])
+def test_gram_acc_equals_gram_plus_add(cuda, P, m, n, B):
+    """dadmm_gnn_gram_acc (out += A^T A x, the adjoint's one-launch accumulation) == out + the
+    gram of x, bit for bit, on the item kernel and the LDS-resident gram."""
+    from dadmm_hip import _lib
+    from dadmm_hip.gnn_ops import GnnRun
+    from dadmm_hip.graph import ingest
+    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, 1, "diff", False)
+    bb = _t(b, cuda)
+    run = GnnRun(model.operator(), bb, ingest(graphs, P, B, cuda), 1, P, _lib.VARIANT_GNN,
+                 *(_t(v, cuda) for v in inits), False)
+    ns = run.op.n_store
+    g = torch.Generator(device=cuda).manual_seed(P + n)
+    xin = torch.zeros(B, P, ns, device=cuda)
+    xin[..., :n] = torch.randn(B, P, n, device=cuda, generator=g)
+    out0 = torch.zeros(B, P, ns, device=cuda)
+    out0[..., :n] = torch.randn(B, P, n, device=cuda, generator=g)
+    want = out0 + run.gram(0, x=xin)
+    got = run.gram_acc(xin, out0.clone())
+    assert torch.equal(got[..., :n], want[..., :n])
+
+
 @pytest.mark.parametrize("mode", ["diff", "same"])
 def test_backward_matches_cpu_autograd(cuda, mode):
     import gnn_dlasso_models_progressive as G
