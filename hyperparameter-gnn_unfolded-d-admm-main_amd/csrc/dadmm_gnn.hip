@@ -579,6 +579,9 @@ constexpr int UCB = 128;
 // DADMM_STEP_KEEPU=1: the step keeps phase 1's U rows in registers for phase 2 (one fewer HBM
 // stream) — 97 instead of 82 VGPRs, four instead of five waves per SIMD: 86.1-86.4 vs 84.7-85.0 ms
 // at the configs[4] shard forward (profiles/r04/variants_r04o_step_keepu.txt), so off
+#ifndef DADMM_STEP_UPCH
+#define DADMM_STEP_UPCH 2       // row pairs in flight per wave in the fused step pass
+#endif
 #ifndef DADMM_STEP_KEEPU
 #define DADMM_STEP_KEEPU 0
 #endif
@@ -594,7 +597,7 @@ template <bool FUSED, bool KEEPU = false>
 __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, float* lds) {
     // row pairs in flight per wave: the fused pass streams 5 state tensors, so fewer pairs keep
     // its registers at 4+ waves per SIMD
-    constexpr int UP_CH = FUSED ? 2 : gnn::UP_CH;
+    constexpr int UP_CH = FUSED ? DADMM_STEP_UPCH : gnn::UP_CH;
     const int P = a.P, n = a.n;
     const int ncb = (n + UCB - 1) / UCB;
     const int s = item / ncb;
