@@ -748,6 +748,24 @@ int dadmm_hyper_linear(int32_t rows, int32_t K, int32_t N, const float* x1, int3
     return ok();
 }
 
+int dadmm_hyper_linear_ex(int32_t rows, int32_t K, int32_t N, const float* x1, int32_t ld1, int32_t K1,
+                          const float* x2, int32_t ld2, const float* W, const float* bias, const float* addend,
+                          int32_t ld_add, float* y, int32_t ldy, void* stream) {
+    dadmm::HyperArgs a;
+    int rc = hyper_input(rows, K, N, x1, ld1, K1, x2, ld2, W, y, ldy, &a);
+    if (rc) return rc;
+    if (addend && ld_add < N) return fail(DADMM_EINVAL, "ld_add=%d < N=%d", ld_add, N);
+    a.bias = bias;
+    a.addend = addend;
+    a.ld_add = ld_add;
+    a.P = 1;
+    a.B = rows;
+    a.splits = 1;
+    hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_BIAS, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "linear launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 int dadmm_hyper_gcn(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1, int32_t ld1,
                     int32_t K1, const float* x2, int32_t ld2, const float* W, const float* bias,
                     const float* ahat, int32_t ahat_per_sample, const float* bn_mean,

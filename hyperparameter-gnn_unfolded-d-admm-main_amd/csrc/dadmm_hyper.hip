@@ -366,6 +366,9 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
                     const int rr = 16 * (wr * WR + i) + 4 * h + r;
                     if (rr >= rows_t) continue;
                     float v = acc[i][c][r] + bv;
+                    // y = addend + x W^T in place (the adjoint's gradient accumulation; unsplit only)
+                    if (EPI == HYPER_EPI_BIAS && a.addend != nullptr)
+                        v = a.addend[(size_t)(row0 + rr) * a.ld_add + col] + v;
                     if (EPI == HYPER_EPI_HEAD) {
                         v = 1.0f / (1.0f + expf(-v));                  // torch.sigmoid  (:170)
                         v = fminf(fmaxf(v, 1e-4f), 0.9999f);          // clamp          (:171)

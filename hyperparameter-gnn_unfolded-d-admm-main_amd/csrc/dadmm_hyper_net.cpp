@@ -195,7 +195,7 @@ int dadmm_hyper_train_forward(const dadmm_hyper_net* net, int32_t B, const float
 static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
                           const float* ahat, int32_t ahat_per_sample, uint64_t seed, const dadmm_hyper_saved* sv,
                           const float* dhyp, const dadmm_hyper_grads* g, float* dAtAy, void* work, float* dsave,
-                          void* stream) {
+                          bool acc_dA, void* stream) {
     if (check_net(net, B) != DADMM_OK || !sv || !dhyp || !g || !dAtAy || !work) return DADMM_EINVAL;
     if (B == 0) return DADMM_OK;
     Work w;
@@ -271,8 +271,9 @@ static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* At
             if (!defer)
                 TRY(dadmm_hyper_wgrad(rows, N, 2 * n, dZ, N, AtAy, net->ld, n, Atb, net->ld, g->conv_w[0], nullptr,
                                       1, w.wscr, stream));
-            TRY(dadmm_hyper_linear(rows, N, n, dZ, N, N, nullptr, 0, g->conv_wt[0], nullptr, dAtAy, net->ld,
-                                   stream));
+            // (acc_dA: dAtAy += ..., in the linear's epilogue instead of a separate add)
+            TRY(dadmm_hyper_linear_ex(rows, N, n, dZ, N, N, nullptr, 0, g->conv_wt[0], nullptr,
+                                      acc_dA ? dAtAy : nullptr, net->ld, dAtAy, net->ld, stream));
         }
     }
     return DADMM_OK;
@@ -283,7 +284,7 @@ int dadmm_hyper_train_backward(const dadmm_hyper_net* net, int32_t B, const floa
                                const dadmm_hyper_saved* sv, const float* dhyp, const dadmm_hyper_grads* g,
                                float* dAtAy, void* work, void* stream) {
     return train_backward(net, B, AtAy, Atb, ahat, ahat_per_sample, seed, sv, dhyp, g, dAtAy, work, nullptr,
-                          stream);
+                          false, stream);
 }
 
 size_t dadmm_hyper_train_dsave_floats(const dadmm_hyper_net* net, int32_t B) {
@@ -295,10 +296,11 @@ size_t dadmm_hyper_train_dsave_floats(const dadmm_hyper_net* net, int32_t B) {
 int dadmm_hyper_train_backward_deferred(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
                                         const float* ahat, int32_t ahat_per_sample, uint64_t seed,
                                         const dadmm_hyper_saved* sv, const float* dhyp, const dadmm_hyper_grads* g,
-                                        float* dAtAy, void* work, float* dsave, void* stream) {
+                                        float* dAtAy, void* work, float* dsave, int32_t accumulate,
+                                        void* stream) {
     if (!dsave || ((uintptr_t)dsave & 15)) return DADMM_EINVAL;
     return train_backward(net, B, AtAy, Atb, ahat, ahat_per_sample, seed, sv, dhyp, g, dAtAy, work, dsave,
-                          stream);
+                          accumulate != 0, stream);
 }
 
 // the (R, N, K) of every batched weight gradient of one deferred pass, in launch order

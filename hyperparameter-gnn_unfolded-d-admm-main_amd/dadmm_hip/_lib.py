@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "dadmm_hyper_gcn",
     "dadmm_hyper_gcn_ex",
     "dadmm_hyper_linear",
+    "dadmm_hyper_linear_ex",
     "dadmm_hyper_rownorm",
     "dadmm_hyper_head",
     "dadmm_hyper_linear_ln_scratch_bytes",
@@ -204,6 +205,8 @@ def load() -> ctypes.CDLL:
                        ("dadmm_hyper_gcn_ex", [i32] * 4 + [vp, i32, vp, i32, vp, i32, vp, vp, i32]
                         + [vp] * 4 + [f32, f32, i32, vp, i32, vp]),
                        ("dadmm_hyper_linear", [i32] * 3 + [vp, i32, i32, vp, i32, vp, vp, vp, i32, vp]),
+                       ("dadmm_hyper_linear_ex", [i32] * 3 + [vp, i32, i32, vp, i32, vp, vp, vp, i32, vp, i32,
+                                                             vp]),
                        ("dadmm_hyper_rownorm", [i32, i32, vp, vp, vp, f32, i32, f32, vp, vp]),
                        ("dadmm_hyper_head", [i32, i32, i32, vp, i32, vp, vp] + [f32] * 4 + [vp, vp]),
                        ("dadmm_hyper_linear_ln", [i32, i32, i32, vp, i32, vp, vp, vp, vp, f32, i32,
@@ -243,7 +246,7 @@ def load() -> ctypes.CDLL:
     L.dadmm_hyper_train_backward_deferred.restype = ctypes.c_int
     L.dadmm_hyper_train_backward_deferred.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, vp, i32, u64,
                                                       ctypes.POINTER(HyperSaved), vp, ctypes.POINTER(HyperGrads),
-                                                      vp, vp, vp, vp]
+                                                      vp, vp, vp, i32, vp]
     L.dadmm_hyper_train_wgrad.restype = ctypes.c_int
     L.dadmm_hyper_train_wgrad.argtypes = [ctypes.POINTER(HyperNet), i32, i32, vp, ctypes.c_int64, vp,
                                           ctypes.POINTER(HyperSaved), ctypes.c_int64, vp, ctypes.c_int64,

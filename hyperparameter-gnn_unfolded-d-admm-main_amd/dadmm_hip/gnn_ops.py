@@ -235,11 +235,12 @@ class GnnTrainFn(torch.autograd.Function):
                                                          gy1, gU1, gd1)
                 if k == K - 1 and ghyp_last is not None:
                     ghyp.add_(ghyp_last)
-                dA = plan.backward_deferred(ctx.As[k], run.Atb, ctx.a_hat, ctx.per_sample, ctx.seeds[k],
-                                            ctx.svs[k], ghyp, g, dsave, k, stream)
-                if k == 0:   # y_0, U_0, delta_0 are the random inits: no gradient
+                # gA += d AtAy from the hypernetwork (in its last linear's epilogue); at k = 0 the
+                # sum is not used (y_0, U_0, delta_0 are the random inits: no gradient)
+                plan.backward_deferred(ctx.As[k], run.Atb, ctx.a_hat, ctx.per_sample, ctx.seeds[k],
+                                       ctx.svs[k], ghyp, g, dsave, k, stream, acc=gA)
+                if k == 0:
                     break
-                gA.add_(dA)
                 run.gram_acc(gA, gy)
                 if gY is not None:
                     gy.add_(gY[k - 1])

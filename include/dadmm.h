@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 15
+#define DADMM_ABI_VERSION 16
 
 enum {
     DADMM_OK = 0,
@@ -382,6 +382,11 @@ int dadmm_hyper_gcn_ex(int32_t B, int32_t P, int32_t K, int32_t N, const float* 
 int dadmm_hyper_linear(int32_t rows, int32_t K, int32_t N, const float* x1, int32_t ld1,
                        int32_t K1, const float* x2, int32_t ld2, const float* W, const float* bias,
                        float* y, int32_t ldy, void* stream);
+/* dadmm_hyper_linear with y = addend + (x W^T + bias) in the epilogue (ABI 16; addend [rows][ld_add],
+ * nullable, may alias y: each element is read before it is written by the same lane). */
+int dadmm_hyper_linear_ex(int32_t rows, int32_t K, int32_t N, const float* x1, int32_t ld1, int32_t K1,
+                          const float* x2, int32_t ld2, const float* W, const float* bias, const float* addend,
+                          int32_t ld_add, float* y, int32_t ldy, void* stream);
 int dadmm_hyper_rownorm(int32_t rows, int32_t C, const float* x, const float* weight,
                         const float* bias, float eps, int32_t act, float slope, float* y,
                         void* stream);
@@ -545,12 +550,14 @@ int dadmm_hyper_train_backward(const dadmm_hyper_net* net, int32_t B, const floa
  * dsave + k dsave_stride and its AtAy at AtAy + k atay_stride (Atb shared). Replaces ~19
  * launches per iteration by ~19 in all (gnn_dlasso_progressive.py:207-214's backward at small
  * batches is bound by launches, not by work). */
+/* accumulate != 0 (ABI 16): dAtAy += the input gradient (the adjoint's running AtAy gradient, added
+ * in the last linear's epilogue: the same bits as writing it and adding after); 0: dAtAy = it. */
 size_t dadmm_hyper_train_dsave_floats(const dadmm_hyper_net* net, int32_t B);
 int dadmm_hyper_train_backward_deferred(const dadmm_hyper_net* net, int32_t B, const float* AtAy,
                                         const float* Atb, const float* ahat, int32_t ahat_per_sample,
                                         uint64_t seed, const dadmm_hyper_saved* sv, const float* dhyp,
                                         const dadmm_hyper_grads* g, float* dAtAy, void* work, float* dsave,
-                                        void* stream);
+                                        int32_t accumulate, void* stream);
 int dadmm_hyper_train_wgrad(const dadmm_hyper_net* net, int32_t B, int32_t iters, const float* AtAy,
                             int64_t atay_stride, const float* Atb, const dadmm_hyper_saved* sv0,
                             int64_t sv_stride, const float* dsave, int64_t dsave_stride,

@@ -109,6 +109,25 @@ def test_gcn_layer_matches_torch(cuda, L, B, P, K, N, per_sample):
     _close(y, want, K)
 
 
+@pytest.mark.parametrize("rows,K,N,ldy", [(1280, 400, 256, 256), (37, 100, 48, 52), (20480, 400, 256, 256)])
+def test_linear_ex_addend_in_place_is_linear_plus_add(cuda, L, rows, K, N, ldy):
+    """dadmm_hyper_linear_ex with addend == y (the GNN adjoint's dAtAy accumulation) equals
+    dadmm_hyper_linear followed by an add, bit for bit; columns past N are left alone."""
+    gen = torch.Generator(device=cuda).manual_seed(rows + K)
+    x = torch.randn(rows, K, device=cuda, generator=gen)
+    W = torch.randn(N, K, device=cuda, generator=gen) / K ** 0.5
+    y0 = torch.randn(rows, ldy, device=cuda, generator=gen)
+    lin = torch.zeros(rows, ldy, device=cuda)
+    assert L.dadmm_hyper_linear(rows, K, N, _p(x), K, K, None, 0, _p(W), None, _p(lin), ldy, _s()) == 0
+    want = y0.clone()
+    want[:, :N] += lin[:, :N]
+    got = y0.clone()
+    rc = L.dadmm_hyper_linear_ex(rows, K, N, _p(x), K, K, None, 0, _p(W), None, _p(got), ldy, _p(got), ldy,
+                                 _s())
+    assert rc == 0, L.dadmm_last_error()
+    assert torch.equal(got, want)
+
+
 @pytest.mark.parametrize("B,P,n,N,per_sample", [(7, 5, 256, 100, True), (40, 50, 512, 100, True),
                                                 (9, 16, 64, 20, False), (3, 2, 16, 8, True),
                                                 (1024, 50, 1024, 100, True)])   # gcn32_kernel
