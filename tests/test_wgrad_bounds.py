@@ -101,3 +101,48 @@ def test_bounds_check_catches_segment_past_k():
     ns = {"np": np, "W2_T": W2_T, "WAVES": WAVES, "RING": RING, "_splits": _splits, "UNIFORM_FORM": True}
     exec(code, ns)
     assert ns["_bad_loads"](256, 32, 160, 160, 32, 160, 160, nb=4, zs=256 * 32 + 96, s1=256 * 160, s2=256 * 160) > 0
+
+
+def _fast_cursor_ok(R, nb, splits, W=WAVES, ring=RING):
+    """The fast form's cursor (csrc/dadmm_hyper_grad.hip, DADMM_W2_FAST): per-step deltas chosen
+    by masks, the first (nsteps - 9) / 8 rings without the range test. Its load sequence must equal
+    the reference cursor's: step min(first + 4 j, last step of the wave) for load j."""
+    spb = R // 2
+    steps = spb * nb
+    per = (steps + splits - 1) // splits
+    big = 1 << 40
+    for split in range(splits):
+        sb, se = split * per, min(split * per + per, steps)
+        for w in range(W):
+            first = sb + w
+            if first >= se or spb < W:
+                continue
+            st = {"lst": first, "lloc": first % spb, "pos": (first // spb) * big + 2 * (first % spb)}
+            seq = []
+
+            def load(check):
+                seq.append(st["pos"])
+                wr = st["lloc"] + W >= spb
+                if (st["lst"] + W < se) if check else True:
+                    st["pos"] += 2 * W + ((big - 2 * spb) if wr else 0)
+                    st["lst"] += W
+                    st["lloc"] += W - (spb if wr else 0)
+            nsteps = (se - first + W - 1) // W
+            nfull = nsteps // ring
+            nunc = min((nsteps - 9) // ring if nsteps >= 9 else 0, nfull)
+            for _ in range(ring):
+                load(True)
+            for g in range(nfull):
+                for _ in range(ring):
+                    load(g >= nunc)
+            for j, v in enumerate(seq):
+                s_ = min(first + W * j, first + W * (nsteps - 1))
+                if v != (s_ // spb) * big + 2 * (s_ % spb):
+                    return False
+    return True
+
+
+@pytest.mark.parametrize("R,nb,splits", [(20480, 25, 16), (4096, 25, 64), (1280, 25, 16), (510, 4, 1),
+                                         (1280, 1, 2), (20480, 25, 8), (300, 3, 4), (16, 3, 1), (74, 2, 3)])
+def test_wgrad2_fast_cursor_sequence(R, nb, splits):
+    assert _fast_cursor_ok(R, nb, splits)
