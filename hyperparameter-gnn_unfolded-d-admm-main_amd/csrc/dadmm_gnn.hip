@@ -579,6 +579,9 @@ constexpr int UCB = 128;
 // DADMM_STEP_KEEPU=1: the step keeps phase 1's U rows in registers for phase 2 (one fewer HBM
 // stream) — 97 instead of 82 VGPRs, four instead of five waves per SIMD: 86.1-86.4 vs 84.7-85.0 ms
 // at the configs[4] shard forward (profiles/r04/variants_r04o_step_keepu.txt), so off
+#ifndef DADMM_STEP_NOBR
+#define DADMM_STEP_NOBR 1       // fused step pass: unconditional loads, results selected after
+#endif
 #ifndef DADMM_STEP_UPCH
 #define DADMM_STEP_UPCH 2       // row pairs in flight per wave in the fused step pass
 #endif
@@ -631,7 +634,56 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     f32x4 ukeep[UMAX][UP_CH];
     auto phase1 = [&](int q0, int it) {
         f32x4 gv[UP_CH], yv[UP_CH];
-        if constexpr (FUSED) {
+        float alv[UP_CH];
+        if constexpr (FUSED && DADMM_STEP_NOBR) {
+            // every load unconditional (rows past P read agent P - 1, columns past n column 0 —
+            // both valid addresses), the results selected afterwards: no load sits under a branch,
+            // so the pass's loads stay in flight together instead of draining at each merge
+            f32x4 tv[UP_CH], bv[UP_CH], uv[UP_CH], dv[UP_CH];
+            float tav[UP_CH], rhv[UP_CH], dgv[UP_CH];
+            bool okv[UP_CH];
+#pragma unroll
+            for (int u = 0; u < UP_CH; ++u) {
+                const int p = 2 * (q0 + WAVES * u) + half;
+                const int pc = p < P ? p : P - 1;
+                okv[u] = p < P && cv;
+                const size_t off = base + (size_t)pc * n;
+                tv[u] = *(const f32x4*)(a.AtAy + off);
+                bv[u] = *(const f32x4*)(a.Atb + off);
+                yv[u] = *(const f32x4*)(ys + off);
+                uv[u] = *(const f32x4*)(U + off);
+                dv[u] = *(const f32x4*)(a.D + off);
+                tav[u] = hyp_at(a, s, 1, pc);
+                rhv[u] = hyp_at(a, s, 2, pc);
+                alv[u] = hyp_at(a, s, 0, pc);
+                dgv[u] = a.deg[(a.graph_shared ? 0 : (size_t)s * P) + pc];
+            }
+#pragma unroll
+            for (int u = 0; u < UP_CH; ++u) {
+                const bool ok = okv[u];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    tv[u][r] = ok ? tv[u][r] : 0.0f;
+                    bv[u][r] = ok ? bv[u][r] : 0.0f;
+                    yv[u][r] = (ok && !yzero) ? yv[u][r] : 0.0f;
+                    uv[u][r] = (ok && !uzero) ? uv[u][r] : 0.0f;
+                    dv[u][r] = ok ? dv[u][r] : 0.0f;
+                }
+                if constexpr (KEEPU) ukeep[it][u] = uv[u];
+                const int p = 2 * (q0 + WAVES * u) + half;
+                if (ok && fix != nullptr) *(f32x4*)(fix + base + (size_t)p * n) = yv[u];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float g = tv[u][r] - bv[u][r];
+                    g = g + sign_times(yv[u][r], tav[u]);   // sign(y) * tau
+                    g = g + uv[u][r] * dgv[u];
+                    g = g + dv[u][r] * rhv[u];
+                    g = clamp_t(g, -gclip, gclip);
+                    bad_g |= ok && g != g;                  // after the clamp only NaN (:216)
+                    gv[u][r] = ok ? g : 0.0f;
+                }
+            }
+        } else if constexpr (FUSED) {
             f32x4 tv[UP_CH], bv[UP_CH], uv[UP_CH], dv[UP_CH];
 #pragma unroll
             for (int u = 0; u < UP_CH; ++u) {
@@ -681,7 +733,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
             if (p < P) {
                 f32x4 v = z4;
                 if (cv) {
-                    const float al = hyp_at(a, s, 0, p);
+                    const float al = (FUSED && DADMM_STEP_NOBR) ? alv[u] : hyp_at(a, s, 0, p);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         v[r] = clamp_t(yv[u][r] - al * gv[u][r], -vclip, vclip);   // :221-225
