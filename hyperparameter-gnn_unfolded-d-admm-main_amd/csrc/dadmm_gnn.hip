@@ -756,11 +756,20 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     bool bad_u = false;
     auto phase2 = [&](int q0, int it) {
         f32x4 uv[UP_CH];
+        float etv[UP_CH];
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
             const int p = 2 * (q0 + WAVES * u) + half;
             if constexpr (KEEPU) {
                 uv[u] = ukeep[it][u];
+            } else if constexpr (FUSED && DADMM_STEP_NOBR) {
+                // unconditional (agent clamped), selected after, as in phase 1
+                const int pc = p < P ? p : P - 1;
+                const f32x4 t = *(const f32x4*)(U + base + (size_t)pc * n);
+                etv[u] = hyp_at(a, s, 3, pc);
+                const bool ok = p < P && cv && !uzero;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) uv[u][r] = ok ? t[r] : 0.0f;
             } else {
                 uv[u] = (p < P && cv && !uzero) ? *(const f32x4*)(U + base + (size_t)p * n) : z4;
             }
@@ -778,7 +787,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
                 const f32x4 yq = *(const f32x4*)(yl + (int)vl[t] * UCB + cl);
                 acc = acc + (yp - yq);
             }
-            const float et = hyp_at(a, s, 3, p);
+            const float et = (FUSED && DADMM_STEP_NOBR && !KEEPU) ? etv[u] : hyp_at(a, s, 3, p);
             f32x4 un;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
