@@ -900,26 +900,32 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
         for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0) red[c * H + (H == 1 ? 0 : p)] += v;
     };
+    // (round 4) no-alias views of the streams, so that the unrolled agent loops below can put
+    // several agents' loads in flight together; the loads read column min(c, n - 1) (always a
+    // valid address) and the lanes past n select zeros, as before
+    const float* __restrict__ AtAy_r = a.AtAy;
+    const float* __restrict__ Atb_r = a.Atb;
+    const float* __restrict__ U_r = a.U;
+    const float* __restrict__ D_r = a.D;
+    const float* __restrict__ ys_r = ys;
     for (int c0 = 64 * wv; c0 < n; c0 += 64 * WAVES) {
         const int c = c0 + lane;
         const bool cv = c < n;
-        const size_t base = (size_t)s * P * n + c;
+        const size_t base = (size_t)s * P * n + (cv ? c : n - 1);
         // recompute y_{k+1} for every agent of this column
+#pragma unroll 4
         for (int p = 0; p < P; ++p) {
-            float y1 = 0.0f;
-            if (cv) {
-                const size_t off = base + (size_t)p * n;
-                const float y = ys[off];
-                const float ta = hyp_at(a, s, 1, p);
-                const float st = sign_times(y, ta);
-                float gr = a.AtAy[off] - a.Atb[off];
-                gr = gr + st;
-                gr = gr + a.U[off] * a.deg[g0 + p];
-                gr = gr + a.D[off] * hyp_at(a, s, 2, p);
-                const float g = clamp_t(gr, -gclip, gclip);
-                y1 = clamp_t(y - hyp_at(a, s, 0, p) * g, -vclip, vclip);
-            }
-            y1l[p * 64 + lane] = y1;
+            const size_t off = base + (size_t)p * n;
+            const float y = ys_r[off];
+            const float ta = hyp_at(a, s, 1, p);
+            const float st = sign_times(y, ta);
+            float gr = AtAy_r[off] - Atb_r[off];
+            gr = gr + st;
+            gr = gr + U_r[off] * a.deg[g0 + p];
+            gr = gr + D_r[off] * hyp_at(a, s, 2, p);
+            const float g = clamp_t(gr, -gclip, gclip);
+            const float y1 = clamp_t(y - hyp_at(a, s, 0, p) * g, -vclip, vclip);
+            y1l[p * 64 + lane] = cv ? y1 : 0.0f;
         }
         // dual update adjoint; d_bar_raw (w.r.t. 2 L y_{k+1} before the GNN clamp)
         for (int p = 0; p < P; ++p) {
