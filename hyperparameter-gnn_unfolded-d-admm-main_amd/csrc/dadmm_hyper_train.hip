@@ -96,29 +96,57 @@ __global__ __launch_bounds__(THREADS) void gcn_bwd_kernel(GcnBwdArgs a) {
 
 // One wave per row, ROWNORM_BWD_ROWS rows per workgroup (2 per wave); per-lane column partials
 // of dweight / dbias are combined across the 4 waves in LDS in wave order (deterministic).
-constexpr int CH = 8;   // C <= 64 * 4 * CH
+// CH: 256-column chunks per lane (C <= 256 CH; the launcher picks the smallest). Round 4: the
+// wave's rows, dy rows and the affine parameters are loaded up front and unconditionally (columns
+// past C read column C - 1, a row past the last reads the last row; their terms are selected
+// away), so the wave waits for memory once instead of twice per row — the per-row load / reduce /
+// load chain at small batches was latency-bound (7.9 us per call at B = 256). Same operations in
+// the same order as before: bit-identical.
+template <int CH>
 __global__ __launch_bounds__(THREADS) void rownorm_bwd_kernel(RowNormBwdArgs a) {
     __shared__ __attribute__((aligned(16))) float red[4][2][2048];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int C = a.C, C4 = C / 4;
+    constexpr int RPW = ROWNORM_BWD_ROWS / 4;
+    const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
     f32x4 pw[CH], pb[CH];
 #pragma unroll
-    for (int u = 0; u < CH; ++u) pw[u] = pb[u] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    for (int u = 0; u < CH; ++u) pw[u] = pb[u] = z4;
     const uint32_t thr = drop_threshold(a.drop_p);
     const float scale = a.drop_p > 0.0f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
     const float invC = 1.0f / (float)C;
-    constexpr int RPW = ROWNORM_BWD_ROWS / 4;
+    bool cok[CH];
+    int cc[CH];
+    f32x4 wv[CH], bv[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        const int c4 = lane + 64 * u;
+        cok[u] = c4 < C4;
+        cc[u] = cok[u] ? c4 : C4 - 1;
+        wv[u] = *(const f32x4*)(a.weight + 4 * cc[u]);
+        bv[u] = *(const f32x4*)(a.bias + 4 * cc[u]);
+    }
+    f32x4 xr[RPW][CH], dr[RPW][CH];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        const int row = blockIdx.x * ROWNORM_BWD_ROWS + w * RPW + i;
+        const int rc = row < a.rows ? row : a.rows - 1;
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            xr[i][u] = *(const f32x4*)(a.xd + (size_t)rc * C + 4 * cc[u]);
+            dr[i][u] = *(const f32x4*)(a.dy + (size_t)rc * C + 4 * cc[u]);
+        }
+    }
+#pragma unroll
     for (int i = 0; i < RPW; ++i) {
         const int row = blockIdx.x * ROWNORM_BWD_ROWS + w * RPW + i;
         if (row >= a.rows) break;
-        const float* x = a.xd + (size_t)row * C;
-        const float* dy = a.dy + (size_t)row * C;
         f32x4 v[CH], g[CH];
         float s = 0.0f;
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
-            const int c4 = lane + 64 * u;
-            v[u] = c4 < C4 ? *(const f32x4*)(x + 4 * c4) : (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[u][e] = cok[u] ? xr[i][u][e] : 0.0f;
             s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
         }
 #pragma unroll
@@ -127,13 +155,11 @@ __global__ __launch_bounds__(THREADS) void rownorm_bwd_kernel(RowNormBwdArgs a) 
         float q = 0.0f;
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
-            const int c4 = lane + 64 * u;
-            if (c4 < C4) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float d = v[u][e] - mean;
-                    q += d * d;
-                }
+            for (int e = 0; e < 4; ++e) {
+                const float d = v[u][e] - mean;
+                const float dd = d * d;
+                q = cok[u] ? q + dd : q;
             }
         }
 #pragma unroll
@@ -143,24 +169,21 @@ __global__ __launch_bounds__(THREADS) void rownorm_bwd_kernel(RowNormBwdArgs a) 
         float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
-            const int c4 = lane + 64 * u;
-            if (c4 >= C4) continue;
-            const f32x4 wv = *(const f32x4*)(a.weight + 4 * c4);
-            const f32x4 bv = *(const f32x4*)(a.bias + 4 * c4);
-            const f32x4 dv = *(const f32x4*)(dy + 4 * c4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const float xh = (v[u][e] - mean) * rstd;
-                float dt = dv[e];
+                float dt = dr[i][u][e];
                 if (a.act) {
-                    const float t = xh * wv[e] + bv[e];
+                    const float t = xh * wv[u][e] + bv[u][e];
                     dt = t > 0.0f ? dt : dt * a.slope;
                 }
-                pw[u][e] += dt * xh;
-                pb[u][e] += dt;
-                const float dxh = dt * wv[e];
-                s1 += dxh;
-                s2 += dxh * xh;
+                const float dxh = dt * wv[u][e];
+                if (cok[u]) {
+                    pw[u][e] += dt * xh;
+                    pb[u][e] += dt;
+                    s1 += dxh;
+                    s2 += dxh * xh;
+                }
                 v[u][e] = xh;
                 g[u][e] = dxh;
             }
@@ -175,7 +198,7 @@ __global__ __launch_bounds__(THREADS) void rownorm_bwd_kernel(RowNormBwdArgs a) 
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
             const int c4 = lane + 64 * u;
-            if (c4 >= C4) continue;
+            if (!cok[u]) continue;
             f32x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -245,7 +268,12 @@ hipError_t launch_gcn_bwd(const GcnBwdArgs& a, hipStream_t st) {
 hipError_t launch_rownorm_bwd(const RowNormBwdArgs& a, hipStream_t st) {
     if (a.rows <= 0) return hipSuccess;
     const int nblk = (a.rows + ROWNORM_BWD_ROWS - 1) / ROWNORM_BWD_ROWS;
-    hipLaunchKernelGGL(hyper_train::rownorm_bwd_kernel, dim3(nblk), dim3(hyper_train::THREADS), 0, st, a);
+    if (a.C > 2048) return hipErrorInvalidValue;
+    const dim3 g(nblk), b(hyper_train::THREADS);
+    if (a.C <= 256) hipLaunchKernelGGL(hyper_train::rownorm_bwd_kernel<1>, g, b, 0, st, a);
+    else if (a.C <= 512) hipLaunchKernelGGL(hyper_train::rownorm_bwd_kernel<2>, g, b, 0, st, a);
+    else if (a.C <= 1024) hipLaunchKernelGGL(hyper_train::rownorm_bwd_kernel<4>, g, b, 0, st, a);
+    else hipLaunchKernelGGL(hyper_train::rownorm_bwd_kernel<8>, g, b, 0, st, a);
     return hipGetLastError();
 }
 
