@@ -31,9 +31,17 @@ namespace hyper_train {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int THREADS = 256;
 constexpr int CB = 64;   // columns per gcn_bwd workgroup
+// gcn_bwd workgroup size NT: its passes 1-2 use one lane per column (64), so at 256 threads three
+// waves idle until the mix. When the grid fills the chip (>= DADMM_GCNBWD_WIDE_MIN workgroups) the
+// one-wave form wins on throughput (B = 4096 train step 61.2 -> 56.6 ms); on small grids the
+// 4-wave mix's shorter per-lane chain wins (B = 256: 10.3 vs 10.8-11.6 ms). Same sums either way.
+#ifndef DADMM_GCNBWD_WIDE_MIN
+#define DADMM_GCNBWD_WIDE_MIN 2048
+#endif
 
 // One workgroup per (sample, 64 columns). LDS: M, then dM [P][CB]; A_hat block [P][P].
-__global__ __launch_bounds__(THREADS) void gcn_bwd_kernel(GcnBwdArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void gcn_bwd_kernel(GcnBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int P = a.P, N = a.N;
     const int ncb = (N + CB - 1) / CB;
@@ -41,7 +49,7 @@ __global__ __launch_bounds__(THREADS) void gcn_bwd_kernel(GcnBwdArgs a) {
     float* dm = lds;                 // [P][CB]
     float* ah = dm + P * CB;         // [P][P]
     const float* ahg = a.ahat + (a.ahat_per_sample ? (size_t)s * P * P : 0);
-    for (int i = threadIdx.x; i < P * P; i += THREADS) ah[i] = ahg[i];
+    for (int i = threadIdx.x; i < P * P; i += NT) ah[i] = ahg[i];
     const size_t row0 = (size_t)s * P;
     const uint32_t thr = drop_threshold(a.drop_p);
     const float scale = a.drop_p > 0.0f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
@@ -85,7 +93,7 @@ __global__ __launch_bounds__(THREADS) void gcn_bwd_kernel(GcnBwdArgs a) {
     __syncthreads();
     // dZ[q] = sum_p A_hat[p][q] dM[p]  (the mix M = A_hat Z, transposed)
     const int cols = N - c0 < CB ? N - c0 : CB;
-    for (int task = threadIdx.x; task < P * CB; task += THREADS) {
+    for (int task = threadIdx.x; task < P * CB; task += NT) {
         const int q = task / CB, c = task - q * CB;
         if (c >= cols) continue;
         float acc = 0.0f;
@@ -252,17 +260,24 @@ __global__ __launch_bounds__(THREADS) void head_act_kernel(int mode, int B, int 
 
 }  // namespace hyper_train
 
-hipError_t launch_gcn_bwd(const GcnBwdArgs& a, hipStream_t st) {
-    if (a.B <= 0 || a.N <= 0) return hipSuccess;
-    const size_t lds = 4 * ((size_t)a.P * hyper_train::CB + (size_t)a.P * a.P);
+template <int NT>
+static hipError_t launch_gcn_bwd_nt(const GcnBwdArgs& a, int grid, size_t lds, hipStream_t st) {
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)hyper_train::gcn_bwd_kernel,
+        hipError_t e = hipFuncSetAttribute((const void*)hyper_train::gcn_bwd_kernel<NT>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    const int ncb = (a.N + hyper_train::CB - 1) / hyper_train::CB;
-    hipLaunchKernelGGL(hyper_train::gcn_bwd_kernel, dim3(a.B * ncb), dim3(hyper_train::THREADS), lds, st, a);
+    hipLaunchKernelGGL(hyper_train::gcn_bwd_kernel<NT>, dim3(grid), dim3(NT), lds, st, a);
     return hipGetLastError();
+}
+
+hipError_t launch_gcn_bwd(const GcnBwdArgs& a, hipStream_t st) {
+    if (a.B <= 0 || a.N <= 0) return hipSuccess;
+    const size_t lds = 4 * ((size_t)a.P * hyper_train::CB + (size_t)a.P * a.P);
+    const int ncb = (a.N + hyper_train::CB - 1) / hyper_train::CB;
+    const int grid = a.B * ncb;
+    return grid >= DADMM_GCNBWD_WIDE_MIN ? launch_gcn_bwd_nt<64>(a, grid, lds, st)
+                                         : launch_gcn_bwd_nt<hyper_train::THREADS>(a, grid, lds, st);
 }
 
 hipError_t launch_rownorm_bwd(const RowNormBwdArgs& a, hipStream_t st) {
