@@ -38,9 +38,13 @@ constexpr int CB = 64;   // columns per gcn_bwd workgroup
 #ifndef DADMM_GCNBWD_WIDE_MIN
 #define DADMM_GCNBWD_WIDE_MIN 2048
 #endif
+// PR: at P <= PR agents a lane's rows are loaded at once into registers (0: the per-row loop)
+#ifndef DADMM_GCNBWD_PR
+#define DADMM_GCNBWD_PR 8
+#endif
 
 // One workgroup per (sample, 64 columns). LDS: M, then dM [P][CB]; A_hat block [P][P].
-template <int NT>
+template <int NT, int PR>
 __global__ __launch_bounds__(NT) void gcn_bwd_kernel(GcnBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int P = a.P, N = a.N;
@@ -58,33 +62,66 @@ __global__ __launch_bounds__(NT) void gcn_bwd_kernel(GcnBwdArgs a) {
         const float mean = a.mean[(size_t)s * N + c];
         const float rstd = 1.0f / sqrtf(a.var[(size_t)s * N + c] + a.eps);
         const float gam = a.gamma[c];
-        // pass 1: dxn = dropout'(dy), the two BatchNorm sums
-        float sb = 0.0f, sg = 0.0f;
-        for (int p = 0; p < P; ++p) {
-            const size_t o = (row0 + p) * N + c;
-            const float mv = a.m[o];
-            const float t = mv > 0.0f ? mv : mv * a.slope;
-            const float xh = (t - mean) * rstd;
-            float g = a.dy[o];
-            if (a.drop_p > 0.0f)
-                g = drop_hash(a.seed, a.site, (uint32_t)(row0 + p), (uint32_t)c) >= thr ? g * scale : 0.0f;
-            sb += g;
-            sg += g * xh;
-            dm[p * CB + threadIdx.x] = g;
-        }
-        // pass 2: BatchNorm and leaky_relu backward -> dM
-        const float inv = 1.0f / (float)P;
-        float sbias = 0.0f;
-        for (int p = 0; p < P; ++p) {
-            const size_t o = (row0 + p) * N + c;
-            const float mv = a.m[o];
-            const float t = mv > 0.0f ? mv : mv * a.slope;
-            const float xh = (t - mean) * rstd;
-            const float g = dm[p * CB + threadIdx.x];
-            const float dt = gam * rstd * (g - sb * inv - xh * (sg * inv));
-            const float d = mv > 0.0f ? dt : dt * a.slope;
-            sbias += d;
-            dm[p * CB + threadIdx.x] = d;
+        float sb = 0.0f, sg = 0.0f, sbias = 0.0f;
+        if constexpr (PR > 0) {
+            // P <= PR: every row's M and dY loaded at once (rows past P re-read row P - 1, unused),
+            // so the lane waits for memory once instead of once per row; same sums, same order
+            float mr[PR], gr[PR], xr[PR];
+#pragma unroll
+            for (int p = 0; p < PR; ++p) {
+                const size_t o = (row0 + (p < P ? p : P - 1)) * N + c;
+                mr[p] = a.m[o];
+                gr[p] = a.dy[o];
+            }
+#pragma unroll
+            for (int p = 0; p < PR; ++p) {
+                if (p >= P) break;
+                const float mv = mr[p];
+                const float t = mv > 0.0f ? mv : mv * a.slope;
+                xr[p] = (t - mean) * rstd;
+                float g = gr[p];
+                if (a.drop_p > 0.0f)
+                    g = drop_hash(a.seed, a.site, (uint32_t)(row0 + p), (uint32_t)c) >= thr ? g * scale : 0.0f;
+                sb += g;
+                sg += g * xr[p];
+                gr[p] = g;
+            }
+            const float inv = 1.0f / (float)P;
+#pragma unroll
+            for (int p = 0; p < PR; ++p) {
+                if (p >= P) break;
+                const float dt = gam * rstd * (gr[p] - sb * inv - xr[p] * (sg * inv));
+                const float d = mr[p] > 0.0f ? dt : dt * a.slope;
+                sbias += d;
+                dm[p * CB + threadIdx.x] = d;
+            }
+        } else {
+            // pass 1: dxn = dropout'(dy), the two BatchNorm sums
+            for (int p = 0; p < P; ++p) {
+                const size_t o = (row0 + p) * N + c;
+                const float mv = a.m[o];
+                const float t = mv > 0.0f ? mv : mv * a.slope;
+                const float xh = (t - mean) * rstd;
+                float g = a.dy[o];
+                if (a.drop_p > 0.0f)
+                    g = drop_hash(a.seed, a.site, (uint32_t)(row0 + p), (uint32_t)c) >= thr ? g * scale : 0.0f;
+                sb += g;
+                sg += g * xh;
+                dm[p * CB + threadIdx.x] = g;
+            }
+            // pass 2: BatchNorm and leaky_relu backward -> dM
+            const float inv = 1.0f / (float)P;
+            for (int p = 0; p < P; ++p) {
+                const size_t o = (row0 + p) * N + c;
+                const float mv = a.m[o];
+                const float t = mv > 0.0f ? mv : mv * a.slope;
+                const float xh = (t - mean) * rstd;
+                const float g = dm[p * CB + threadIdx.x];
+                const float dt = gam * rstd * (g - sb * inv - xh * (sg * inv));
+                const float d = mv > 0.0f ? dt : dt * a.slope;
+                sbias += d;
+                dm[p * CB + threadIdx.x] = d;
+            }
         }
         a.part[(size_t)s * N + c] = sg;                          // dgamma
         a.part[((size_t)a.B + s) * N + c] = sb;                  // dbeta
@@ -260,14 +297,14 @@ __global__ __launch_bounds__(THREADS) void head_act_kernel(int mode, int B, int 
 
 }  // namespace hyper_train
 
-template <int NT>
+template <int NT, int PR>
 static hipError_t launch_gcn_bwd_nt(const GcnBwdArgs& a, int grid, size_t lds, hipStream_t st) {
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)hyper_train::gcn_bwd_kernel<NT>,
+        hipError_t e = hipFuncSetAttribute((const void*)hyper_train::gcn_bwd_kernel<NT, PR>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(hyper_train::gcn_bwd_kernel<NT>, dim3(grid), dim3(NT), lds, st, a);
+    hipLaunchKernelGGL((hyper_train::gcn_bwd_kernel<NT, PR>), dim3(grid), dim3(NT), lds, st, a);
     return hipGetLastError();
 }
 
@@ -276,8 +313,12 @@ hipError_t launch_gcn_bwd(const GcnBwdArgs& a, hipStream_t st) {
     const size_t lds = 4 * ((size_t)a.P * hyper_train::CB + (size_t)a.P * a.P);
     const int ncb = (a.N + hyper_train::CB - 1) / hyper_train::CB;
     const int grid = a.B * ncb;
-    return grid >= DADMM_GCNBWD_WIDE_MIN ? launch_gcn_bwd_nt<64>(a, grid, lds, st)
-                                         : launch_gcn_bwd_nt<hyper_train::THREADS>(a, grid, lds, st);
+    constexpr int T4 = hyper_train::THREADS;
+    if (a.P <= DADMM_GCNBWD_PR)
+        return grid >= DADMM_GCNBWD_WIDE_MIN ? launch_gcn_bwd_nt<64, DADMM_GCNBWD_PR>(a, grid, lds, st)
+                                             : launch_gcn_bwd_nt<T4, DADMM_GCNBWD_PR>(a, grid, lds, st);
+    return grid >= DADMM_GCNBWD_WIDE_MIN ? launch_gcn_bwd_nt<64, 0>(a, grid, lds, st)
+                                         : launch_gcn_bwd_nt<T4, 0>(a, grid, lds, st);
 }
 
 hipError_t launch_rownorm_bwd(const RowNormBwdArgs& a, hipStream_t st) {
