@@ -498,17 +498,24 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(const float* __restrict
 // hundred rows), so the sum is latency-bound: each workgroup takes CS_C = 16 columns of one g and
 // splits the rows over CS_S = 16 slices (slice s: rows s, s + 16, ..., 8 loads in flight), then
 // adds the 16 slice sums in slice order through LDS — a fixed order, deterministic run to run.
+#ifndef DADMM_COLSUM_2STAGE
+#define DADMM_COLSUM_2STAGE 1
+#endif
 constexpr int CS_C = 16, CS_S = THREADS / CS_C;
+// bout (round 4, two-stage form for many batch blocks): workgroup (x, y) sums batch block y alone
+// and writes it to bout [G][nb][C]; a second colsum over bout (R = nb) adds the blocks in order.
+// The one-stage form left G x C / 16 workgroups (21 for a 100-wide BatchNorm) walking nb x R rows.
 __global__ __launch_bounds__(THREADS) void colsum_kernel(const float* __restrict__ part, int G, int R, int C,
                                                          float* __restrict__ out, int beta, int nb,
-                                                         size_t pstride) {
+                                                         size_t pstride, float* __restrict__ bout) {
     __shared__ float red[CS_S][CS_C + 1];
     const int cb = (C + CS_C - 1) / CS_C;
     const int g = blockIdx.x / cb, c0 = (blockIdx.x % cb) * CS_C;
     const int cl = threadIdx.x % CS_C, sl = threadIdx.x / CS_C;
     const int c = c0 + cl < C ? c0 + cl : C - 1;
     float s = 0.0f;
-    for (int bb = 0; bb < nb; ++bb) {   // batch blocks (deferred training gradients), in order
+    const int b0 = bout ? (int)blockIdx.y : 0, b1 = bout ? b0 + 1 : nb;
+    for (int bb = b0; bb < b1; ++bb) {   // batch blocks (deferred training gradients), in order
         const float* p = part + (size_t)bb * pstride + (size_t)g * R * C + c;
         int r = sl;
         for (; r + 7 * CS_S < R; r += 8 * CS_S) {
@@ -526,6 +533,10 @@ __global__ __launch_bounds__(THREADS) void colsum_kernel(const float* __restrict
         float t = 0.0f;
 #pragma unroll
         for (int k = 0; k < CS_S; ++k) t += red[k][cl];
+        if (bout) {
+            bout[((size_t)g * nb + b0) * C + c0 + cl] = t;
+            return;
+        }
         float* o = out + (size_t)g * C + c0 + cl;
         *o = beta ? *o + t : t;
     }
@@ -607,10 +618,19 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_colsum(const float* part, int G, int R, int C, float* out, int beta, hipStream_t st, int nb,
-                         size_t pstride) {
+                         size_t pstride, float* bscratch) {
     const int blocks = G * ((C + hgrad::CS_C - 1) / hgrad::CS_C);
+    if (bscratch && nb > 1 && DADMM_COLSUM_2STAGE) {
+        hipLaunchKernelGGL(hgrad::colsum_kernel, dim3(blocks, nb), dim3(hgrad::THREADS), 0, st, part, G, R, C,
+                           out, beta, nb, pstride, bscratch);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(hgrad::colsum_kernel, dim3(blocks), dim3(hgrad::THREADS), 0, st, (const float*)bscratch,
+                           G, nb, C, out, beta, 1, (size_t)0, (float*)nullptr);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(hgrad::colsum_kernel, dim3(blocks), dim3(hgrad::THREADS), 0, st, part, G, R, C, out, beta,
-                       nb, pstride);
+                       nb, pstride, (float*)nullptr);
     return hipGetLastError();
 }
 

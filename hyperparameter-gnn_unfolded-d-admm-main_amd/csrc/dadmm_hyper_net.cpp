@@ -322,6 +322,12 @@ size_t dadmm_hyper_train_wgrad_scratch_bytes(const dadmm_hyper_net* net, int32_t
         best = b > best ? b : best;
         return DADMM_OK;
     });
+    // the colsums' per-iteration block sums [G][iters][C] (G <= 3: BatchNorm dgamma / dbeta / dbias)
+    int cmax = 1;
+    for (int i = 0; i < 5; ++i) cmax = net->width[i] > cmax ? net->width[i] : cmax;
+    for (int j = 0; j < 3; ++j) cmax = net->dec_width[j] > cmax ? net->dec_width[j] : cmax;
+    const size_t cs = 4 * (size_t)3 * iters * cmax;
+    best = cs > best ? cs : best;
     return best;
 }
 
@@ -352,7 +358,7 @@ int dadmm_hyper_train_wgrad(const dadmm_hyper_net* net, int32_t B, int32_t iters
         return dadmm::launch_wgrad(a, st) == hipSuccess ? DADMM_OK : DADMM_EHIP;
     };
     auto cs = [&](const float* part, int G, int R, int C, float* out) -> int {
-        return dadmm::launch_colsum(part, G, R, C, out, 1, st, iters, (size_t)dsave_stride) == hipSuccess
+        return dadmm::launch_colsum(part, G, R, C, out, 1, st, iters, (size_t)dsave_stride, (float*)scratch) == hipSuccess
                    ? DADMM_OK : DADMM_EHIP;
     };
     const size_t ss = (size_t)sv_stride;

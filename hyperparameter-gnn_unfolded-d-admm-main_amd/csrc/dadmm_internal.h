@@ -330,9 +330,10 @@ struct WgradArgs {
 };
 int wgrad_splits(int R, int N, int K);
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st);
-// out [G][C] (+)= sum over r of part [G][R][C] (fixed order)
+// out [G][C] (+)= sum over r of part [G][R][C] (fixed order); bscratch [G][nb][C] floats: the
+// two-stage form for nb > 1 batch blocks
 hipError_t launch_colsum(const float* part, int G, int R, int C, float* out, int beta, hipStream_t st,
-                         int nb = 1, size_t pstride = 0);
+                         int nb = 1, size_t pstride = 0, float* bscratch = nullptr);
 // out [cols][rows] = in [rows][cols]
 hipError_t launch_transpose(const float* in, int rows, int cols, float* out, hipStream_t st);
 

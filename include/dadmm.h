@@ -565,7 +565,9 @@ int dadmm_hyper_train_wgrad(const dadmm_hyper_net* net, int32_t B, int32_t iters
 /* Row-split scratch of dadmm_hyper_train_wgrad (ABI 14): with `scratch` of at least this many bytes
  * (16-byte aligned) each weight gradient's rows spread over several workgroups per output tile and
  * the partials are added in a fixed order (deterministic); with scratch == NULL one workgroup walks
- * every row of its tile. 0 when no gradient splits. */
+ * every row of its tile. The scratch also holds the normalisation-parameter sums' per-iteration
+ * block sums (iters > 1), which are then added in iteration order: deterministic, but rounded in a
+ * different order than with scratch == NULL (f32 rounding). */
 size_t dadmm_hyper_train_wgrad_scratch_bytes(const dadmm_hyper_net* net, int32_t B, int32_t iters);
 
 #ifdef __cplusplus
