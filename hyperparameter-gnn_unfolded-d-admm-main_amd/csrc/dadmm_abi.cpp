@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/dadmm.h"
@@ -112,6 +113,11 @@ int check_fused_shape(const dadmm_dims* d, const uint32_t* nbr_order, int* graph
     return DADMM_OK;
 }
 
+bool agent_division() {
+    const char* e = getenv("DADMM_FUSED_DIVISION");
+    return !(e != nullptr && strcmp(e, "rows") == 0);
+}
+
 int forward_impl(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
                  const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
                  const float* U0, const float* d0, float* Y, float* Grec, float* Urec,
@@ -129,8 +135,12 @@ int forward_impl(const dadmm_dims* d, const void* op, const float* b, const uint
         return fail(DADMM_EINVAL, "Y, y0, U0, d0 and U_out must be 16-byte aligned");
     int graph = 0, nt = 0;
     if ((rc = check_fused_shape(d, nbr_order, &graph, &nt)) != DADMM_OK) return rc;
-    dadmm::fused_fn_ptr fn = rec ? dadmm::find_fused_rec(d->P, nt, graph)
-                                 : dadmm::find_fused(d->P, nt, graph);
+    // inference: the agent-resident kernel where it holds the shape (DADMM_FUSED_DIVISION=rows
+    // selects the row-divided kernel, e.g. for A/B timing; both are bit-identical)
+    dadmm::fused_fn_ptr fn = nullptr;
+    if (!rec && agent_division()) fn = dadmm::find_resident(d->P, nt, graph);
+    if (fn == nullptr)
+        fn = rec ? dadmm::find_fused_rec(d->P, nt, graph) : dadmm::find_fused(d->P, nt, graph);
     if (fn == nullptr)
         return fail(DADMM_EUNSUPPORTED, "no fused kernel for P=%d n=%d (n_pad=%d)", d->P, d->n,
                     64 * nt);

@@ -1024,13 +1024,12 @@ hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* o
     if (DADMM_GRAM_LDS && mode != 1 && mbk >= 1 && mbk <= 4 && gnn::gram_lds_bytes(mq, a.n_pad) <= 160 * 1024) {
         // workgroups = P x S splits of the tiles; S minimises (rounds of workgroups over the CUs) x
         // (tiles each wave runs), preferring fewer workgroups on a tie
-        static int cus = 0;
-        if (cus == 0) {
-            int dev = 0;
-            hipDeviceProp_t prop;
-            cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-                      ? prop.multiProcessorCount : 256;
-        }
+        // the current device's CU count, queried per call (the runtime caches the attribute; a
+        // function-static cache would size the splits for the first device a process used)
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
         const int tiles = (a.B + BT - 1) / BT;
         // a workgroup per (agent, run of tiles) at >= one tile per wave: too few workgroups to
         // spread over the CUs at small P x B (P = 5, B = 1024: 20) -> gram_kernel's items instead

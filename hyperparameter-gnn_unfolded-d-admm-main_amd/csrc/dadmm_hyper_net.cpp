@@ -336,6 +336,14 @@ int dadmm_hyper_train_wgrad(const dadmm_hyper_net* net, int32_t B, int32_t iters
                             const float* dsave, int64_t dsave_stride, const dadmm_hyper_grads* g, void* scratch,
                             void* stream) {
     if (check_net(net, B) != DADMM_OK || iters < 0 || !AtAy || !Atb || !sv0 || !dsave || !g) return DADMM_EINVAL;
+    // the iteration blocks are read at k * stride: a stride shorter than one block (or negative)
+    // would make the batched kernels read past (or before) the caller's buffers
+    if (atay_stride < 0 || sv_stride < 0 || dsave_stride < 0) return DADMM_EINVAL;
+    if (iters > 1 && B > 0) {
+        if (atay_stride < (int64_t)B * net->P * net->ld || sv_stride == 0 ||
+            (size_t)dsave_stride < dadmm_hyper_train_dsave_floats(net, B))
+            return DADMM_EINVAL;
+    }
     if (B == 0 || iters == 0) return DADMM_OK;
     if (net->n & 15) return DADMM_EUNSUPPORTED;
     if (scratch && ((uintptr_t)scratch & 15)) return DADMM_EINVAL;

@@ -52,6 +52,10 @@ enum { GRAPH_SHARED = 0, GRAPH_LANE = 1, GRAPH_ORDERED = 2 };
 fused_fn_ptr find_fused(int P, int nt, int graph);
 // Same shapes, recording the adjoint's trajectory (a.Grec / a.Urec must be set).
 fused_fn_ptr find_fused_rec(int P, int nt, int graph);
+// The agent-resident form of the same forward (dadmm_resident.hip: 4 waves, one per SIMD, each
+// owning whole agents; bit-identical to find_fused's kernels), or nullptr for shapes it does not
+// hold (it serves n_pad = 256 with P = 4 or 5, shared or per-sample ascending graphs).
+fused_fn_ptr find_resident(int P, int nt, int graph);
 
 // ---- adjoint (dadmm_backward.hip) ---------------------------------------------------------------
 struct BackwardArgs {

@@ -1,0 +1,516 @@
+// dadmm_resident.hip — the agent-resident fused K-iteration forward for gfx950 (MI355X): one
+// wave per SIMD, each wave owning whole agents of a 16-sample tile.
+//
+// Reference semantics: unfolded_DLASSO.py:34-140 (DLASSO_unfolded.forward / compute_delta), the
+// GNN variant's fixed clamps of gnn_dlasso_models_progressive.py:205-232 — exactly what
+// dadmm_fused.hip computes, with the same fma-chain orders, so the two kernels are bit-identical
+// (and both bit-exact against oracle_forward_f32).
+//
+// Division of the work. The workgroup is 16 samples x all P agents x all K
+// iterations, like fused_forward_kernel, but with 4 waves (one per SIMD, 512 registers each)
+// instead of 8, and the state divided by AGENT instead of by rows:
+//   * wave w owns the F = P / 4 "full" agents w, w + 4, ...: their y, U and delta for all n rows
+//     of the 16 samples live in the wave's registers. GEMM1 (R_p = A_p y_p - b_p, 4 m-block
+//     chains) takes y_p straight from registers — the GEMM2 accumulator layout (row 4h + r of
+//     sample j in lane 16h + j, element r) IS the 16x16x4 B-operand layout of the 0,4,8,12 chain
+//     order — and GEMM2 (G_p = A_p^T R_p) takes R_p straight from the GEMM1 accumulators, for the
+//     same reason. No LDS round trip of y or R for these agents;
+//   * the S = P % 4 remaining "split" agents are divided across the 4 waves as the 8-wave kernel
+//     divides every agent: GEMM1 m-block w (y from the LDS tile), GEMM2 n-tiles 4w..4w+3 (R from
+//     LDS), state for those rows in registers;
+//   * every wave has the same MFMA count (P = 5: 512 + 128 per iteration), and the only exchange
+//     is y_{k+1} of every agent through the LDS tile Ylds for the consensus delta = 2 L y (and
+//     the split agents' R through Rlds): two workgroup barriers per iteration.
+// Per iteration: GEMM1_k with delta_k = compute_delta(y_k) of the wave's rows (from Ylds) under
+// its MFMAs; barrier; GEMM2_k with U_k = clamp(U_{k-1} + delta_k eta_{k-1}), the gradient
+// assembly, the clamps and the primal update of each finished (agent, n-tile) chain under the
+// next chain's MFMAs, y_{k+1} to registers, Ylds and Y[k]; barrier.
+//
+// Consensus of one agent p (compute_delta restricted to delta[p], in the reference's order): the
+// updates delta[p] receives are, in order, the visits (q, p) of the agents q < p, then p's own
+// visits (p, q), then the visits (q, p) of q > p; each adds fl(y_p - y_q) == -fl(y_q - y_p)
+// (round-to-nearest is symmetric). With the agent p a wave-uniform RUNTIME value, the three runs
+// are three fma chains over all q with 0/1 multipliers (m1: q < p and p in N(q); m2: q != p and q
+// in N(p); m3: q > p and p in N(q)): fma(-d, 1, acc) = fl(acc - d), fma(-d, 0, acc) = acc (acc
+// starts at +0 and never becomes -0). Directed adjacencies and self-loops need no special case.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "dadmm_internal.h"
+
+namespace dadmm {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef const __attribute__((address_space(4))) float cfloat;
+
+constexpr int RW = 4;                 // waves per workgroup: one per SIMD
+
+// GEMM1 A-operand ring depth (steps of 16 columns; RA1 - 1 steps in flight under the MFMAs)
+#ifndef DADMM_RS_A1
+#define DADMM_RS_A1 2
+#endif
+// GEMM2 A^T-operand ring depth (chains of 16 n-rows x 64 m; the chains run in pairs, so even:
+// RA2 - 2 chains in flight under a pair's MFMAs)
+#ifndef DADMM_RS_A2
+#define DADMM_RS_A2 4
+#endif
+static_assert(DADMM_RS_A2 % 2 == 0 && DADMM_RS_A2 >= 4, "GEMM2 ring: whole pairs, one in flight");
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+// the iterate stream (written once, never re-read here): sc1, as dadmm_fused.hip's DADMM_Y_AUX
+__device__ __forceinline__ void bstore4_stream(f32x4 v, rsrc_t r, uint32_t voff) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, voff, 0, 16);
+}
+__device__ __forceinline__ void bstore4(f32x4 v, rsrc_t r, uint32_t voff) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, voff, 0, 0);
+}
+__device__ __forceinline__ float mclamp(float x, float lo, float hi) {
+    return __builtin_amdgcn_fmed3f(x, lo, hi);   // == min(max(x, lo), hi) for non-NaN x
+}
+__device__ __forceinline__ bool finitef(float x) { return __builtin_isfinite(x); }
+// keeps `base + constant` inside the loop (the constant folds into the instruction's offset)
+__device__ __forceinline__ uint32_t fresh(uint32_t x) {
+    asm volatile("" : "=v"(x) : "0"(x));
+    return x;
+}
+
+template <int P, int NT, int GRAPH>
+__global__ __launch_bounds__(RW * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void resident_forward_kernel(FusedArgs a) {
+    constexpr bool SHARED = GRAPH == GRAPH_SHARED;
+    constexpr int NP = NT * 64;          // padded n
+    constexpr int NB = NP / 16;          // 16-row n-tiles
+    constexpr int NBS = NB / RW;         // n-tiles of a split agent per wave
+    constexpr int F = P / RW;            // full agents per wave
+    constexpr int S = P % RW;            // split agents
+    constexpr int SA = S > 0 ? S : 1;    // array extents
+    constexpr int FA = F > 0 ? F : 1;
+    constexpr int MP = M_PAD;
+    constexpr int YS = NP + 8;           // Ylds row stride (floats): conflict-free b128 (dadmm_fused.hip)
+    constexpr int RS = MP + 8;           // Rlds row stride
+    constexpr int NA1 = F * 4 + S;       // GEMM1 chains per wave (A fragments per step)
+    constexpr int NC = F * NB + S * NBS; // GEMM2 chains per wave
+    constexpr int RA1 = DADMM_RS_A1, RA2 = DADMM_RS_A2;
+    __shared__ __attribute__((aligned(16))) float lds[P * BT * YS + SA * BT * RS + RW * NA1 * 256];
+    float* __restrict__ Ylds = lds;                    // [P][BT][YS]   y_k, n contiguous
+    float* __restrict__ Rlds = lds + P * BT * YS;      // [S][BT][RS]   split agents' R
+    float* __restrict__ Blds = Rlds + SA * BT * RS;    // [RW][NA1][64 lanes][4]  -b seeds
+
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15;             // sample within the tile (MFMA column)
+    const int h = lane >> 4;             // 4-row group within a 16-row tile
+    const int s = blockIdx.x * BT + j;
+    const bool sv = s < a.B;
+    const int n = a.n, m = a.m, B = a.B;
+    const uint32_t state_bytes = (uint32_t)((size_t)B * P * n * 4);
+    const rsrc_t rA = make_rsrc(a.A, (uint32_t)(P * MP * NP * 4));
+    const rsrc_t rAt = make_rsrc(a.At, (uint32_t)(P * MP * NP * 4));
+
+    // agent of GEMM2 chain c / state slot: own agents first (w + 4 i, all NB tiles), then the
+    // split agents (4 F + i, this wave's NBS tiles)
+    auto own_agent = [&](int i) { return w + RW * i; };                  // wave-uniform
+    auto split_agent = [](int i) { return RW * F + i; };
+
+    // ---- graph: consensus multipliers of the wave's agents (m1 / m2 / m3, see the header) and
+    //      degrees; uniform (SGPRs) for a shared graph, per lane for per-sample graphs ----------
+    uint32_t msk[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+        msk[q] = SHARED ? __builtin_amdgcn_readfirstlane((uint32_t)a.nbr[q])
+                        : (sv ? (uint32_t)a.nbr[(size_t)s * P + q] : 0u);
+    float mo[FA][3][P], ms[SA][3][P], dgo[FA], dgs[SA];
+    auto mults = [&](int p, float (&mm)[3][P]) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const bool into = (msk[q] >> p) & 1u;     // p in N(q): q's visit (q, p)
+            const bool from = (msk[p] >> q) & 1u;     // q in N(p): p's visit (p, q)
+            mm[0][q] = (q < p && into) ? 1.0f : 0.0f;
+            mm[1][q] = (q != p && from) ? 1.0f : 0.0f;
+            mm[2][q] = (q > p && into) ? 1.0f : 0.0f;
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < F; ++i) {
+        const int p = own_agent(i);
+        // a runtime-uniform agent index into the mask array: select it out once
+        uint32_t mp = msk[0];
+#pragma unroll
+        for (int q = 1; q < P; ++q) mp = p == q ? msk[q] : mp;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const bool into = (msk[q] >> p) & 1u;
+            const bool from = (mp >> q) & 1u;
+            mo[i][0][q] = (q < p && into) ? 1.0f : 0.0f;
+            mo[i][1][q] = (q != p && from) ? 1.0f : 0.0f;
+            mo[i][2][q] = (q > p && into) ? 1.0f : 0.0f;
+        }
+        dgo[i] = SHARED ? a.deg[p] : (sv ? a.deg[(size_t)s * P + p] : 0.0f);
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        mults(split_agent(i), ms[i]);
+        dgs[i] = SHARED ? a.deg[split_agent(i)] : (sv ? a.deg[(size_t)s * P + split_agent(i)] : 0.0f);
+    }
+
+    // ---- state: own agents [F][NB] tiles, split agents [S][NBS] tiles (tile tt of split agent
+    //      i is n-tile NBS * w + tt); element r of tile t is row 16 t + 4 h + r of sample j ------
+    // y_k itself lives only in the LDS tile Ylds (every agent's rows are needed there for the
+    // consensus anyway): GEMM1 reads its B operand and the update its own rows from there
+    f32x4 Uo[FA][NB], Do[FA][NB];
+    f32x4 Us[SA][NBS], Ds[SA][NBS];
+    uint32_t status = 0;
+    {
+        const rsrc_t ry = make_rsrc(a.y0, state_bytes);
+        const rsrc_t ru = make_rsrc(a.U0, state_bytes);
+        const rsrc_t rd = make_rsrc(a.d0, state_bytes);
+        bool bad_y = false, bad_u = false;
+        auto load3 = [&](int p, int nb, f32x4& vu, f32x4& vd) {
+            const int n0 = nb * 16 + 4 * h;
+            const uint32_t off = n0 < n ? (uint32_t)(((s * P + p) * n + n0) * 4) : 0x80000000u;
+            const f32x4 vy = bload4(ry, off, 0);
+            vu = bload4(ru, off, 0);
+            vd = bload4(rd, off, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                bad_y |= !finitef(vy[r]);
+                bad_u |= !finitef(vu[r]);
+            }
+            *(f32x4*)(Ylds + (p * BT + j) * YS + n0) = vy;
+        };
+#pragma unroll
+        for (int i = 0; i < F; ++i)
+#pragma unroll
+            for (int t = 0; t < NB; ++t) load3(own_agent(i), t, Uo[i][t], Do[i][t]);
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+#pragma unroll
+            for (int tt = 0; tt < NBS; ++tt) load3(split_agent(i), NBS * w + tt, Us[i][tt], Ds[i][tt]);
+        status |= (bad_y ? 1u : 0u) | (bad_u ? 2u : 0u);
+    }
+    // -b seeds of the GEMM1 chains (own agents' 4 m-blocks, split agents' m-block w), parked in
+    // LDS lane-linear (conflict-free b128) and re-read each iteration: registers are the budget
+    auto bslot = [&](int c) { return (f32x4*)(Blds + ((w * NA1 + c) * 64 + lane) * 4); };
+    auto bseed = [&](int p, int mb) {
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int mi = 16 * mb + 4 * h + r;
+            v[r] = (sv && mi < m) ? -a.b[((size_t)s * P + p) * m + mi] : 0.0f;
+        }
+        return v;
+    };
+#pragma unroll
+    for (int i = 0; i < F; ++i)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) *bslot(i * 4 + mb) = bseed(own_agent(i), mb);
+#pragma unroll
+    for (int i = 0; i < S; ++i) *bslot(F * 4 + i) = bseed(split_agent(i), w);
+    {
+        bool bad_h = false;
+        const int nh = a.K * a.hyp_rows * 4;
+        for (int i = threadIdx.x; i < nh; i += RW * 64) bad_h |= !finitef(a.hyp[i]);
+        status |= bad_h ? 8u : 0u;
+    }
+
+    // per-lane byte offsets: GEMM1 A fragment (row 16 mb + j, columns 16 t + 4 h ..), GEMM2 A^T
+    // fragment (row 16 nt + j, columns 16 mb + 4 h ..), the lane's sample in an iterate
+    const uint32_t voffA = (uint32_t)((j * NP + 4 * h) * 4);
+    const uint32_t voffAt = (uint32_t)((j * MP + 4 * h) * 4);
+    const uint32_t voffY = (uint32_t)((s * P * n + 4 * h) * 4);
+    const float dlim = a.variant != 0 ? 20.0f : __builtin_inff();
+
+    // delta_k rows (4) of agent p at n-tile nb, from the y_k tile of every agent in Ylds
+    auto yrow = [&](int p, int nb) -> f32x4 { return *(const f32x4*)(Ylds + (p * BT + j) * YS + nb * 16 + 4 * h); };
+    auto delta4 = [&](int p, int nb, const float (&mm)[3][P]) {
+        const f32x4 yp = yrow(p, nb);
+        f32x4 dq[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const f32x4 yq = *(const f32x4*)(Ylds + (q * BT + j) * YS + nb * 16 + 4 * h);
+            dq[q] = yq - yp;
+        }
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ph = 0; ph < 3; ++ph)
+#pragma unroll
+            for (int q = 0; q < P; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(-dq[q][r], mm[ph][q], acc[r]);
+        f32x4 d;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d[r] = mclamp(acc[r], -dlim, dlim);
+        return d;
+    };
+
+    // GEMM1 A ring
+    f32x4 ar[RA1][NA1];
+    uint32_t vA = voffA;
+    auto load_a = [&](f32x4 (&slot)[NA1], int t) {
+#pragma unroll
+        for (int i = 0; i < F; ++i)
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+                slot[i * 4 + mb] = bload4(rA, vA + 64 * t, (uint32_t)((own_agent(i) * MP + 16 * mb) * NP * 4));
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+            slot[F * 4 + i] = bload4(rA, vA + 64 * t, (uint32_t)((split_agent(i) * MP + 16 * w) * NP * 4));
+    };
+    // GEMM2 A^T ring: chain c = own (i, nt) for c < F NB, else split (i, tt)
+    f32x4 at[RA2][4];
+    uint32_t vAt = voffAt;
+    auto chain_agent = [&](int c) { return c < F * NB ? own_agent(c / NB) : split_agent((c - F * NB) / NBS); };
+    auto chain_tile = [&](int c) { return c < F * NB ? c % NB : NBS * w + (c - F * NB) % NBS; };
+    auto load_at = [&](f32x4 (&slot)[4], int c) {
+        const uint32_t so = (uint32_t)((chain_agent(c) * NP + 16 * chain_tile(c)) * MP * 4);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) slot[mb] = bload4(rAt, vAt + 64 * mb, so);
+    };
+
+    float et_prev[P], vclip_prev = 0.0f;
+#pragma unroll
+    for (int p = 0; p < P; ++p) et_prev[p] = 0.0f;
+
+#pragma unroll
+    for (int t = 0; t + 1 < RA1; ++t) load_a(ar[t], t);
+    __syncthreads();
+
+    for (int k = 0; k < a.K; ++k) {
+        vA = fresh(voffA);
+        vAt = fresh(voffAt);
+        const bool live = k > 0;
+        // seq_hyp(k): (alpha, tau, rho, eta) of every agent, kernel-uniform scalars
+        float al[P], ta[P], rh[P], et[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const cfloat* hp = (const cfloat*)a.hyp + ((size_t)k * a.hyp_rows + (a.hyp_rows == 1 ? 0 : p)) * 4;
+            al[p] = hp[0]; ta[p] = hp[1]; rh[p] = hp[2]; et[p] = hp[3];
+        }
+        auto hsel = [&](const float (&v)[P], int p) {   // v[p] for a runtime-uniform p
+            float x = v[0];
+#pragma unroll
+            for (int q = 1; q < P; ++q) x = p == q ? v[q] : x;
+            return x;
+        };
+        float gclip, vclip;
+        if (a.variant == 0) {
+            gclip = fmaxf(1.0f, 30.0f - (float)k);          // unfolded_DLASSO.py:80
+            vclip = fmaxf(10.0f, 200.0f - (float)(k * 3));  // unfolded_DLASSO.py:92
+        } else {
+            gclip = 10.0f;                                   // gnn_dlasso_models_progressive.py:212
+            vclip = 100.0f;                                  // :224, :232
+        }
+
+        // ---- GEMM1: R_p = A_p y_p - b_p; delta_k of the wave's rows under the MFMAs (k >= 1;
+        //      iteration 0 keeps the caller's delta0: a separate copy of the loop, no branch) -----
+        f32x4 ro[FA][4], rsp[SA];
+        auto gemm1 = [&](auto dual_tag) {
+            constexpr bool DUAL = decltype(dual_tag)::value;
+#pragma unroll
+        for (int i = 0; i < F; ++i)
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) ro[i][mb] = *bslot(i * 4 + mb);
+#pragma unroll
+        for (int i = 0; i < S; ++i) rsp[i] = *bslot(F * 4 + i);
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+            if (t + RA1 - 1 < NB) load_a(ar[(t + RA1 - 1) % RA1], t + RA1 - 1);
+            f32x4 yo[FA], yb[SA];
+#pragma unroll
+            for (int i = 0; i < F; ++i) yo[i] = yrow(own_agent(i), t);
+#pragma unroll
+            for (int i = 0; i < S; ++i) yb[i] = yrow(split_agent(i), t);
+            const f32x4(&av)[NA1] = ar[t % RA1];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int i = 0; i < F; ++i)
+#pragma unroll
+                    for (int mb = 0; mb < 4; ++mb) ro[i][mb] = mfma4(av[i * 4 + mb][r], yo[i][r], ro[i][mb]);
+#pragma unroll
+                for (int i = 0; i < S; ++i) rsp[i] = mfma4(av[F * 4 + i][r], yb[i][r], rsp[i]);
+            }
+            if constexpr (DUAL) {
+                // delta_k of own tile t, and of split tile tt at steps t = tt * NB / NBS
+#pragma unroll
+                for (int i = 0; i < F; ++i) Do[i][t] = delta4(own_agent(i), t, mo[i]);
+#pragma unroll
+                for (int tt = 0; tt < NBS; ++tt)
+                    if (tt * (NB / NBS) == t) {
+#pragma unroll
+                        for (int i = 0; i < S; ++i) Ds[i][tt] = delta4(split_agent(i), NBS * w + tt, ms[i]);
+                    }
+            }
+        }
+        };
+        if (live) gemm1(std::true_type{});
+        else gemm1(std::false_type{});
+#pragma unroll
+        for (int i = 0; i < S; ++i) *(f32x4*)(Rlds + (i * BT + j) * RS + 16 * w + 4 * h) = rsp[i];
+        // GEMM2's first A^T chains, in flight across the barrier
+#pragma unroll
+        for (int c = 0; c + 2 < RA2 && c < NC; ++c) load_at(at[c], c);
+        __syncthreads();
+
+        // ---- GEMM2 + gradient assembly + primal update -----------------------------------------
+        f32x4 rsb[SA][4];
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) rsb[i][mb] = *(const f32x4*)(Rlds + (i * BT + j) * RS + 16 * mb + 4 * h);
+        bool bad_g = false;
+        const rsrc_t rY = make_rsrc(a.Y + (size_t)k * B * P * n, state_bytes);
+        // the primal update of chain c from its G (:73-93): y_{k+1} to registers, Ylds, Y[k]
+        auto update = [&](int c, const f32x4& gp) {
+            const bool own = c < F * NB;
+            const int ii = own ? c / NB : (c - F * NB) / NBS;
+            const int tl = own ? c % NB : (c - F * NB) % NBS;
+            const int p = chain_agent(c), nb = chain_tile(c);
+            f32x4& U = own ? Uo[ii][tl] : Us[ii][tl];
+            const f32x4& D = own ? Do[ii][tl] : Ds[ii][tl];
+            const float alp = own ? hsel(al, p) : al[p];
+            const float tap = own ? hsel(ta, p) : ta[p];
+            const float rhp = own ? hsel(rh, p) : rh[p];
+            const float etp = own ? hsel(et_prev, p) : et_prev[p];
+            const float dgp = own ? dgo[ii] : dgs[ii];
+            const f32x4 Y = yrow(p, nb);   // y_k (this wave's rows: no other wave writes them)
+            f32x4 yn;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                // the deferred dual update U_k = clamp(U_{k-1} + delta_k eta_{k-1}) (:95-99);
+                // k = 0 keeps the caller's U0
+                const float un = mclamp(U[r] + D[r] * etp, -vclip_prev, vclip_prev);
+                const float uk = live ? un : U[r];
+                U[r] = uk;
+                const float yv = Y[r];
+                // grad = (AtAy - Atb) + sign(y)*tau + U*deg + delta*rho, left to right
+                float gr = gp[r];
+                gr = gr + sign_times(yv, tap);
+                gr = gr + uk * dgp;
+                gr = gr + D[r] * rhp;
+                bad_g |= (gr != gr);                            // :84 guard (flag only)
+                gr = mclamp(gr, -gclip, gclip);                 // :80-81
+                float v = yv - alp * gr;                        // :89
+                yn[r] = mclamp(v, -vclip, vclip);               // :92-93
+            }
+            const int n0 = nb * 16 + 4 * h;
+            *(f32x4*)(Ylds + (p * BT + j) * YS + n0) = yn;
+            bstore4_stream(yn, rY, n0 < n ? voffY + (uint32_t)((p * n + nb * 16) * 4) : 0x80000000u);
+        };
+        auto bop = [&](int c, int mb) -> const f32x4& {
+            return c < F * NB ? ro[c / NB][mb] : rsb[(c - F * NB) / NBS][mb];
+        };
+        f32x4 gprev[2];
+#pragma unroll
+        for (int c0 = 0; c0 < NC; c0 += 2) {
+            const int nc = c0 + 1 < NC ? 2 : 1;
+            f32x4 gc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+            for (int u = 0; u < nc; ++u) {
+                const int c = c0 + u;
+                if (c + RA2 - 2 < NC) load_at(at[(c + RA2 - 2) % RA2], c + RA2 - 2);
+            }
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int u = 0; u < nc; ++u)
+                        gc[u] = mfma4(at[(c0 + u) % RA2][mb][r], bop(c0 + u, mb)[r], gc[u]);
+            if (c0 == NC - nc || c0 + 2 >= NC) {
+                // next iteration's first GEMM1 steps, before the last Y stores
+                if (k + 1 < a.K) {
+#pragma unroll
+                    for (int t = 0; t + 1 < RA1; ++t) load_a(ar[t], t);
+                }
+            }
+            if (c0 > 0) {
+                update(c0 - 2, gprev[0]);
+                update(c0 - 1, gprev[1]);
+            }
+            gprev[0] = gc[0];
+            gprev[1] = gc[1];
+            if (c0 + 2 >= NC) {
+#pragma unroll
+                for (int u = 0; u < nc; ++u) update(c0 + u, gc[u]);
+            }
+        }
+        status |= bad_g ? 4u : 0u;
+#pragma unroll
+        for (int p = 0; p < P; ++p) et_prev[p] = et[p];
+        vclip_prev = vclip;
+        __syncthreads();
+    }
+
+    if (a.U_out != nullptr) {
+        // the dual update of the last iteration (deferred like the others)
+        const rsrc_t rU = make_rsrc(a.U_out, state_bytes);
+        auto fin = [&](int p, int nb, const f32x4& U, const float (&mm)[3][P], float etp) {
+            f32x4 v = U;
+            if (a.K > 0) {
+                const f32x4 d = delta4(p, nb, mm);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = mclamp(U[r] + d[r] * etp, -vclip_prev, vclip_prev);
+            }
+            const int n0 = nb * 16 + 4 * h;
+            bstore4(v, rU, n0 < n ? (uint32_t)(((s * P + p) * n + n0) * 4) : 0x80000000u);
+        };
+        float etq[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) etq[p] = et_prev[p];
+#pragma unroll
+        for (int i = 0; i < F; ++i) {
+            float ep = etq[0];
+#pragma unroll
+            for (int q = 1; q < P; ++q) ep = own_agent(i) == q ? etq[q] : ep;
+#pragma unroll
+            for (int t = 0; t < NB; ++t) fin(own_agent(i), t, Uo[i][t], mo[i], ep);
+        }
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+#pragma unroll
+            for (int tt = 0; tt < NBS; ++tt)
+                fin(split_agent(i), NBS * w + tt, Us[i][tt], ms[i], etq[split_agent(i)]);
+    }
+    if (a.status != nullptr) {
+        uint32_t wst = status;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) wst |= __shfl_xor(wst, off);
+        if (lane == 0 && wst) atomicOr((unsigned int*)a.status, wst);
+    }
+}
+
+template <int P, int NT, int GRAPH>
+hipError_t launch_resident(const FusedArgs& a, hipStream_t stream) {
+    const int grid = (a.B + BT - 1) / BT;
+    hipLaunchKernelGGL((resident_forward_kernel<P, NT, GRAPH>), dim3(grid), dim3(RW * 64), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// The agent-resident kernel's shapes: n_pad = 256 (NT = 4), P = 4 or 5 (one full agent per
+// wave, at most one split agent: the state of 16 samples fits the 512 registers of a wave),
+// shared or per-sample ascending graphs. Everything else: find_fused.
+fused_fn_ptr find_resident(int P, int nt, int graph) {
+    if (nt != 4 || (graph != GRAPH_SHARED && graph != GRAPH_LANE)) return nullptr;
+    if (P == 5) return graph == GRAPH_SHARED ? &launch_resident<5, 4, GRAPH_SHARED> : &launch_resident<5, 4, GRAPH_LANE>;
+    if (P == 4) return graph == GRAPH_SHARED ? &launch_resident<4, 4, GRAPH_SHARED> : &launch_resident<4, 4, GRAPH_LANE>;
+    return nullptr;
+}
+
+}  // namespace dadmm

@@ -52,10 +52,28 @@ __device__ __forceinline__ float4 normal4(hiprandStatePhilox4_32_10_t* st) {
 #define DADMM_RNG_DIRECT 1
 #endif
 
+// The launch is bound by these rounds (~60 % of its time at the headline shape), so each round
+// is 2 v_mad_u64_u32 (both halves of a product in one instruction; __umulhi plus a separate low
+// multiply compiled to v_mul_hi_u32 + v_mul_lo_u32) and 2 gfx950 v_bitop3_b32 (LUT 0x96 =
+// a ^ b ^ c; LLVM leaves the 3-way xors as pairs of v_xor_b32). The key word is wave-uniform.
+// Same integer results.
+#ifndef DADMM_RNG_MAD
+#define DADMM_RNG_MAD 1
+#endif
+__device__ __forceinline__ unsigned xor3(unsigned a, unsigned b, unsigned c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 __device__ __forceinline__ uint4 philox_round(uint4 c, uint2 k) {
+#if DADMM_RNG_MAD
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    return make_uint4(xor3((unsigned)(p1 >> 32), c.y, k.x), (unsigned)p1,
+                      xor3((unsigned)(p0 >> 32), c.w, k.y), (unsigned)p0);
+#else
     const unsigned hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
     const unsigned hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
     return make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+#endif
 }
 
 __device__ __forceinline__ uint4 philox10(uint4 c, uint2 k) {

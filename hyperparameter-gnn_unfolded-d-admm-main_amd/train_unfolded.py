@@ -39,6 +39,7 @@ import configurations  # noqa: E402
 import gnn_dlasso_utils  # noqa: E402
 import unfolded_DLASSO  # noqa: E402
 from dadmm_hip import dist as D  # noqa: E402
+from dadmm_hip.autograd import raise_if_timed_out  # noqa: E402
 
 
 def _dataset(A, size, args, gen):
@@ -62,6 +63,25 @@ def _inits(args, bs, lo, hi, device):
         return None
     shape = (bs, args.P, args.n, 1)
     return tuple(torch.empty(shape, device=device).normal_(0.0, 1e-2)[lo:hi] for _ in range(3))
+
+
+def validate(model, b_va, x_va, graph, args, bs, gen, rank, world, device):
+    """The epoch's validation loss (global over ranks) and the last batch's hyp. A timed-out
+    guard recomputation (NaN losses, compute_loss) raises GuardTimeoutError here instead of
+    reaching the scheduler and the checkpoint test as NaN (the float() syncs anyway)."""
+    model.eval()
+    hyp = None
+    with torch.no_grad():
+        tot, nb = 0.0, 0
+        for idx in _batches(args.test_size, bs, gen, shuffle=True):
+            lo, hi = D.shard_range(bs, rank, world)
+            sel = idx[lo:hi].to(device)
+            Y, hyp = model(b_va[sel], [graph] * (hi - lo), inits=_inits(args, bs, lo, hi, device))
+            loss_mean, loss_final = gnn_dlasso_utils.compute_loss(Y, x_va[sel])
+            raise_if_timed_out(loss_final)
+            tot += float(D.global_losses(loss_mean, loss_final, hi - lo)[1])
+            nb += 1
+    return tot / max(nb, 1), hyp
 
 
 def main(argv=None):
@@ -119,18 +139,7 @@ def main(argv=None):
             nb += 1
         train_losses.append(tot / max(nb, 1))
 
-        model.eval()
-        with torch.no_grad():
-            tot, nb = 0.0, 0
-            for idx in _batches(args.test_size, bs, gen, shuffle=True):
-                lo, hi = D.shard_range(bs, rank, world)
-                sel = idx[lo:hi].to(device)
-                Y, hyp = model(b_va[sel], [graph] * (hi - lo),
-                               inits=_inits(args, bs, lo, hi, device))
-                loss_mean, loss_final = gnn_dlasso_utils.compute_loss(Y, x_va[sel])
-                tot += float(D.global_losses(loss_mean, loss_final, hi - lo)[1])
-                nb += 1
-            valid = tot / max(nb, 1)
+        valid, hyp = validate(model, b_va, x_va, graph, args, bs, gen, rank, world, device)
         valid_losses.append(valid)
         scheduler.step(valid)
         if rank == 0:

@@ -219,3 +219,33 @@ def test_hyper_linear_ln_validation(L):
     assert L.dadmm_hyper_linear_ln(*args(4, None)) == -1            # no scratch
     # a split input whose split point is not a multiple of 16
     assert L.dadmm_hyper_linear(8, 16, 4, _fk(0), 8, 8, _fk(1), 8, _fk(2), None, _fk(4), 4, None) == -2
+
+
+def test_hyper_train_wgrad_rejects_bad_strides(L):
+    """dadmm_hyper_train_wgrad validates its iteration strides before launching (a
+    short or negative stride would make the batched kernels read outside the caller's buffers)."""
+    from dadmm_hip import _lib
+    net = _lib.HyperNet()
+    net.P, net.n, net.ld, net.H = 5, 16, 16, 5
+    for i in range(5):
+        net.width[i] = 8
+        net.conv_w[i] = net.conv_b[i] = net.bn_w[i] = net.bn_b[i] = 0x10000
+    for jj in range(3):
+        net.dec_width[jj] = 8
+        net.dec_w[jj] = net.dec_b[jj] = net.ln_w[jj] = net.ln_b[jj] = 0x10000
+    net.norm_w = net.norm_b = net.fc_w = net.fc_b = 0x10000
+    B, iters = 4, 3
+    dfl = L.dadmm_hyper_train_dsave_floats(ctypes.byref(net), B)
+    assert dfl > 0
+    sv, g = _lib.HyperSaved(), _lib.HyperGrads()
+    atay = B * net.P * net.ld
+
+    def call(a_s, s_s, d_s):
+        return L.dadmm_hyper_train_wgrad(ctypes.byref(net), B, iters, _fk(0), a_s, _fk(1),
+                                         ctypes.byref(sv), s_s, _fk(2), d_s, ctypes.byref(g), None, None)
+    assert call(-1, 100, dfl) == -1                  # negative
+    assert call(atay, -5, dfl) == -1
+    assert call(atay, 100, -16) == -1
+    assert call(atay - 1, 100, dfl) == -1            # shorter than one AtAy block
+    assert call(atay, 0, dfl) == -1                  # every iteration on the same saved block
+    assert call(atay, 100, dfl - 4) == -1            # shorter than one dsave block

@@ -242,6 +242,36 @@ def test_compute_loss_flags_timed_out_forward():
     assert mean.item() == 1.0 and final.item() == 1.0
 
 
+def test_driver_validation_raises_on_timed_out_forward():
+    """the drivers' no_grad validation loop must not feed the NaN losses of
+    a timed-out guard recomputation into the LR scheduler / checkpoint test: train_unfolded.
+    validate raises GuardTimeoutError (fake model on the CPU returning tagged iterates)."""
+    import train_unfolded
+    from dadmm_hip import _lib
+    from dadmm_hip.autograd import GuardTimeoutError, tag_status
+    P, n, m, bs, K = 3, 6, 4, 4, 2
+    args = argparse.Namespace(test_size=8, init_draw="local", P=P, n=n)
+
+    class Fake(torch.nn.Module):
+        def __init__(self, bits):
+            super().__init__()
+            self.bits = bits
+
+        def forward(self, b, graphs, inits=None):
+            Y = torch.zeros(K, len(b), P, n, 1)
+            if self.bits & _lib.STATUS_BARRIER_TIMEOUT:
+                Y = Y + float("nan")
+            return tag_status(Y, torch.tensor([self.bits], dtype=torch.int32)), torch.zeros(P, 4, 1)
+
+    b_va, x_va = torch.zeros(8, P, m, 1), torch.zeros(8, n, 1)
+    gen = torch.Generator().manual_seed(0)
+    v, _ = train_unfolded.validate(Fake(0), b_va, x_va, None, args, bs, gen, 0, 1, torch.device("cpu"))
+    assert np.isfinite(v)
+    with pytest.raises(GuardTimeoutError):
+        train_unfolded.validate(Fake(_lib.STATUS_BARRIER_TIMEOUT), b_va, x_va, None, args, bs, gen,
+                                0, 1, torch.device("cpu"))
+
+
 @pytest.mark.parametrize("P,B,prob,loops", [(5, 200, 0.5, False), (16, 150, 0.3, False),
                                            (9, 120, 0.4, True), (50, 80, 0.5, False)])
 def test_vectorized_ingestion_equals_per_graph_path(P, B, prob, loops):
