@@ -596,9 +596,47 @@ def check_parity(O, model, A, b, G, dev, P, n, m, K, Bs=32):
     Y = Y[..., 0].cpu().numpy()
     Y32, _, _ = O.forward_f32(A, bs, [G] * Bs, table, y0, U0, d0)
     Y64, _, _ = O.forward_f64(A, bs, [G] * Bs, table, y0, U0, d0)
+    # north_star's "final-iterate MSE <= 1e-5 vs the CPU reference": the reference's own op
+    # sequence replayed in fp32 on the CPU (oracle.ref_torch: Gram form, per-agent GEMVs, the
+    # Python compute_delta loop), also at BASELINE configs[0]
+    from oracle import ref_torch
+    Yr = ref_torch.forward(A, bs, [G] * Bs, table, y0, U0, d0)
+    mse = lambda a, c: float(((a[-1] - c[-1]) ** 2).mean())   # noqa: E731
     return {"samples": Bs, "bit_exact_vs_fp32_oracle": bool(np.array_equal(Y, Y32)),
             "max_abs_diff_vs_fp32_oracle": float(np.abs(Y - Y32).max()),
-            "final_iter_mse_vs_fp64": float(((Y[-1] - Y64[-1]) ** 2).mean())}
+            "final_iter_mse_vs_fp64": mse(Y, Y64),
+            "final_iter_mse_vs_reference_form_fp32": mse(Y, Yr),
+            "reference_form_fp32_mse_vs_fp64": mse(Yr, Y64),
+            "tolerance": 1e-5,
+            "configs0": parity_configs0(O, dev)}
+
+
+def parity_configs0(O, dev):
+    """BASELINE configs[0] (P=5, n=200, m=50, B=32, K=15, shared ER(0.5) graph, the reference's
+    default hyper-parameter init param = 0): the drop-in module on the GPU vs the reference-form
+    fp32 CPU replay (oracle.ref_torch) and the fp64 restatement, final-iterate MSE."""
+    import argparse as _ap
+
+    import unfolded_DLASSO
+    from oracle import ref_torch
+    P, n, m, B, K = 5, 200, 50, 32, 15
+    A, b, _ = O.make_problem(P, m, n, B, seed=1200)
+    G = O.er_graph(P, 0.5, seed=7)
+    rng = np.random.default_rng(99)
+    y0, U0, d0 = (1e-2 * rng.standard_normal((3, B, P, n))).astype(np.float32)
+    mod = unfolded_DLASSO.DLASSO_unfolded(torch.from_numpy(A)[None].to(dev), _ap.Namespace(
+        GHN_iter_num=K, DADMM_mode="diff", alpha_max=0.1, tau_max=0.99, rho_max=0.99,
+        eta_max=0.99, max_penalty_threshold=0.8, penalty_reduction_factor=0.95)).to(dev).eval()
+    with torch.no_grad():
+        Y, _ = mod(torch.from_numpy(b).to(dev)[..., None], [G] * B,
+                   inits=tuple(torch.from_numpy(v).to(dev) for v in (y0, U0, d0)))
+        table = mod.hyp_table(K).cpu().numpy()
+    Y = Y[..., 0].cpu().numpy()
+    Yr = ref_torch.forward(A, b, [G] * B, table, y0, U0, d0)
+    Y64, _, _ = O.forward_f64(A, b, [G] * B, table, y0, U0, d0)
+    mse = lambda a, c: float(((a[-1] - c[-1]) ** 2).mean())   # noqa: E731
+    return {"P": P, "n": n, "m": m, "B": B, "K": K,
+            "final_iter_mse_vs_reference_form_fp32": mse(Y, Yr), "final_iter_mse_vs_fp64": mse(Y, Y64)}
 
 
 def _host_cpus():

@@ -104,6 +104,7 @@ void resident_forward_kernel(FusedArgs a) {
     constexpr int RS = MP + 8;           // Rlds row stride
     constexpr int NA1 = F * 4 + S;       // GEMM1 chains per wave (A fragments per step)
     constexpr int NC = F * NB + S * NBS; // GEMM2 chains per wave
+    constexpr int NSC = S * NBS;         // the split agents' chains run first (their LDS B operands die early)
     constexpr int RA1 = DADMM_RS_A1, RA2 = DADMM_RS_A2;
     __shared__ __attribute__((aligned(16))) float lds[P * BT * YS + SA * BT * RS + RW * NA1 * 256];
     float* __restrict__ Ylds = lds;                    // [P][BT][YS]   y_k, n contiguous
@@ -270,11 +271,11 @@ void resident_forward_kernel(FusedArgs a) {
         for (int i = 0; i < S; ++i)
             slot[F * 4 + i] = bload4(rA, vA + 64 * t, (uint32_t)((split_agent(i) * MP + 16 * w) * NP * 4));
     };
-    // GEMM2 A^T ring: chain c = own (i, nt) for c < F NB, else split (i, tt)
+    // GEMM2 A^T ring: chain c = split (i, tt) for c < NSC, else own (i, nt)
     f32x4 at[RA2][4];
     uint32_t vAt = voffAt;
-    auto chain_agent = [&](int c) { return c < F * NB ? own_agent(c / NB) : split_agent((c - F * NB) / NBS); };
-    auto chain_tile = [&](int c) { return c < F * NB ? c % NB : NBS * w + (c - F * NB) % NBS; };
+    auto chain_agent = [&](int c) { return c >= NSC ? own_agent((c - NSC) / NB) : split_agent(c / NBS); };
+    auto chain_tile = [&](int c) { return c >= NSC ? (c - NSC) % NB : NBS * w + c % NBS; };
     auto load_at = [&](f32x4 (&slot)[4], int c) {
         const uint32_t so = (uint32_t)((chain_agent(c) * NP + 16 * chain_tile(c)) * MP * 4);
 #pragma unroll
@@ -376,9 +377,9 @@ void resident_forward_kernel(FusedArgs a) {
         const rsrc_t rY = make_rsrc(a.Y + (size_t)k * B * P * n, state_bytes);
         // the primal update of chain c from its G (:73-93): y_{k+1} to registers, Ylds, Y[k]
         auto update = [&](int c, const f32x4& gp) {
-            const bool own = c < F * NB;
-            const int ii = own ? c / NB : (c - F * NB) / NBS;
-            const int tl = own ? c % NB : (c - F * NB) % NBS;
+            const bool own = c >= NSC;
+            const int ii = own ? (c - NSC) / NB : c / NBS;
+            const int tl = own ? (c - NSC) % NB : c % NBS;
             const int p = chain_agent(c), nb = chain_tile(c);
             f32x4& U = own ? Uo[ii][tl] : Us[ii][tl];
             const f32x4& D = own ? Do[ii][tl] : Ds[ii][tl];
@@ -412,7 +413,7 @@ void resident_forward_kernel(FusedArgs a) {
             bstore4_stream(yn, rY, n0 < n ? voffY + (uint32_t)((p * n + nb * 16) * 4) : 0x80000000u);
         };
         auto bop = [&](int c, int mb) -> const f32x4& {
-            return c < F * NB ? ro[c / NB][mb] : rsb[(c - F * NB) / NBS][mb];
+            return c >= NSC ? ro[(c - NSC) / NB][mb] : rsb[c / NBS][mb];
         };
         f32x4 gprev[2];
 #pragma unroll

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 GPU session: GPU suite (no -x: a failing parity test must not hide the bench), then the
+# Round GPU session (TAG, TESTS, BENCH, BENCH2 env): GPU suite (no -x: a failing parity test must not hide the bench), then the
 # 1-GPU bench, then a 2-rank rehearsal of the self-launching multi-rank bench (gloo on one GPU).
 # Stops at the first step that times out, aborts or faults (exit >= 124).
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
-OUT=gpurun_out/${TAG:-r04}
+OUT=gpurun_out/${TAG:-round}
 mkdir -p "$OUT"
 run() {  # name seconds cmd...
     local name=$1 secs=$2; shift 2
