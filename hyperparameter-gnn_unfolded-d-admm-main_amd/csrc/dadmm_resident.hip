@@ -62,6 +62,40 @@ constexpr int RW = 4;                 // waves per workgroup: one per SIMD
 #endif
 static_assert(DADMM_RS_A2 % 2 == 0 && DADMM_RS_A2 >= 4, "GEMM2 ring: whole pairs, one in flight");
 
+// Ablation knobs (timing builds only, never shipped): operand loads replaced by register values,
+// the consensus skipped, the iterate stores skipped.
+#ifdef DADMM_RES_ABL_ACONST
+#define RABL_A(x, v) ((f32x4){__builtin_bit_cast(float, (v)), 0.001f, 0.002f, 0.003f})
+#else
+#define RABL_A(x, v) (x)
+#endif
+
+// DADMM_RES_SGB: the schedule of each GEMM step / GEMM2 pair pinned with sched_group_barrier —
+// the step's LDS and global reads first, then one MFMA followed by up to V1 (GEMM1) / V2
+// (GEMM2) VALU instructions, repeated: with one wave per SIMD nothing else fills the matrix
+// pipe's shadow, so the VALU work has to be spread between the wave's own MFMAs.
+#ifndef DADMM_RES_SGB
+#define DADMM_RES_SGB 0
+#endif
+#ifndef DADMM_RES_V1
+#define DADMM_RES_V1 5
+#endif
+#ifndef DADMM_RES_V2
+#define DADMM_RES_V2 5
+#endif
+template <int NM, int V, int NDS, int NVM>
+__device__ __forceinline__ void sgb_pattern() {
+#if DADMM_RES_SGB
+    if constexpr (NDS > 0) __builtin_amdgcn_sched_group_barrier(0x100, NDS, 0);
+    if constexpr (NVM > 0) __builtin_amdgcn_sched_group_barrier(0x020, NVM, 0);
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+    }
+#endif
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -266,10 +300,10 @@ void resident_forward_kernel(FusedArgs a) {
         for (int i = 0; i < F; ++i)
 #pragma unroll
             for (int mb = 0; mb < 4; ++mb)
-                slot[i * 4 + mb] = bload4(rA, vA + 64 * t, (uint32_t)((own_agent(i) * MP + 16 * mb) * NP * 4));
+                slot[i * 4 + mb] = RABL_A(bload4(rA, vA + 64 * t, (uint32_t)((own_agent(i) * MP + 16 * mb) * NP * 4)), vA + 64 * t + mb);
 #pragma unroll
         for (int i = 0; i < S; ++i)
-            slot[F * 4 + i] = bload4(rA, vA + 64 * t, (uint32_t)((split_agent(i) * MP + 16 * w) * NP * 4));
+            slot[F * 4 + i] = RABL_A(bload4(rA, vA + 64 * t, (uint32_t)((split_agent(i) * MP + 16 * w) * NP * 4)), vA + 64 * t);
     };
     // GEMM2 A^T ring: chain c = split (i, tt) for c < NSC, else own (i, nt)
     f32x4 at[RA2][4];
@@ -279,7 +313,7 @@ void resident_forward_kernel(FusedArgs a) {
     auto load_at = [&](f32x4 (&slot)[4], int c) {
         const uint32_t so = (uint32_t)((chain_agent(c) * NP + 16 * chain_tile(c)) * MP * 4);
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb) slot[mb] = bload4(rAt, vAt + 64 * mb, so);
+        for (int mb = 0; mb < 4; ++mb) slot[mb] = RABL_A(bload4(rAt, vAt + 64 * mb, so), vAt + 64 * mb + so);
     };
 
     float et_prev[P], vclip_prev = 0.0f;
@@ -345,7 +379,11 @@ void resident_forward_kernel(FusedArgs a) {
 #pragma unroll
                 for (int i = 0; i < S; ++i) rsp[i] = mfma4(av[F * 4 + i][r], yb[i][r], rsp[i]);
             }
+#ifdef DADMM_RES_ABL_NODELTA
+            if constexpr (false) {
+#else
             if constexpr (DUAL) {
+#endif
                 // delta_k of own tile t, and of split tile tt at steps t = tt * NB / NBS
 #pragma unroll
                 for (int i = 0; i < F; ++i) Do[i][t] = delta4(own_agent(i), t, mo[i]);
@@ -356,6 +394,7 @@ void resident_forward_kernel(FusedArgs a) {
                         for (int i = 0; i < S; ++i) Ds[i][tt] = delta4(split_agent(i), NBS * w + tt, ms[i]);
                     }
             }
+            sgb_pattern<4 * NA1, DUAL ? DADMM_RES_V1 : 1, DUAL ? 2 + 6 : 2, NA1>();
         }
         };
         if (live) gemm1(std::true_type{});
@@ -410,7 +449,9 @@ void resident_forward_kernel(FusedArgs a) {
             }
             const int n0 = nb * 16 + 4 * h;
             *(f32x4*)(Ylds + (p * BT + j) * YS + n0) = yn;
+#ifndef DADMM_RES_ABL_NOSTORE
             bstore4_stream(yn, rY, n0 < n ? voffY + (uint32_t)((p * n + nb * 16) * 4) : 0x80000000u);
+#endif
         };
         auto bop = [&](int c, int mb) -> const f32x4& {
             return c >= NSC ? ro[(c - NSC) / NB][mb] : rsb[c / NBS][mb];
@@ -443,6 +484,7 @@ void resident_forward_kernel(FusedArgs a) {
                 update(c0 - 2, gprev[0]);
                 update(c0 - 1, gprev[1]);
             }
+            sgb_pattern<16 * 2, DADMM_RES_V2, 4, 8>();
             gprev[0] = gc[0];
             gprev[1] = gc[1];
             if (c0 + 2 >= NC) {

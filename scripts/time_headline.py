@@ -62,13 +62,14 @@ def timed(fn, reps):
 
 
 for rnd in range(rounds):
-    for div in ("agents", "rows"):
+    for div in os.environ.get("DIVISIONS", "agents,rows").split(","):
         os.environ["DADMM_FUSED_DIVISION"] = div
         ms_k, out = timed(lambda: forward_raw(op, bt, g, hyp, y0, U0, d0, path="fused"), reps)
         Y, _, st = out
         with torch.no_grad():
             ms_f, (Ym, _) = timed(lambda: model(bt[..., None], graph_list), reps)
-        print(json.dumps({"round": rnd, "division": div, "cfg": [B, P, n, m, K],
+        print(json.dumps({"lib": os.path.basename(os.environ.get("DADMM_LIB_VARIANT", "libdadmm.so")),
+                          "round": rnd, "division": div, "cfg": [B, P, n, m, K],
                           "kernel_ms": ms_k, "module_forward_ms": ms_f,
                           "M_iters_per_s": B * K / ms_f / 1e3, "status": int(st.item()),
                           "Ysum": float(Y.double().sum())}),

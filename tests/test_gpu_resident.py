@@ -2,7 +2,7 @@
 and against the row-divided fused kernel (csrc/dadmm_fused.hip).
 
 Both kernels serve ``dadmm_forward`` for n_pad = 256, P in {4, 5}; the environment variable
-DADMM_FUSED_DIVISION selects one ("agents", the default, or "rows"). Bar: bit-exact
+DADMM_FUSED_DIVISION selects one ("rows", the default, or "agents"). Bar: bit-exact
 (np.array_equal) on every iterate and on U_K against oracle.forward_f32 and against each other,
 and the same guard status words (path "fused": the kernels only flag; path "auto": the gated
 stepwise recomputation makes the result exact).
