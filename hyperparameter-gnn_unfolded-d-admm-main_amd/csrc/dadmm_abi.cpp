@@ -914,7 +914,10 @@ int dadmm_hyper_gcn_train(int32_t B, int32_t P, int32_t K, int32_t N, const floa
                           const float* ahat, int32_t ahat_per_sample, const float* bn_weight,
                           const float* bn_bias, float bn_eps, float slope, float drop_p, uint64_t seed,
                           int32_t site, float* y, int32_t ldy, float* m_out, float* mean_out,
-                          float* var_out, void* stream) {
+                          float* var_out, const float* bn_running_mean, const float* bn_running_var,
+                          void* stream) {
+    if ((bn_running_mean == nullptr) != (bn_running_var == nullptr))
+        return fail(DADMM_EINVAL, "running mean and variance: both or neither");
     if (B < 0 || P < 2 || P > 160)
         return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d (training BatchNorm needs P >= 2; P <= 160)", B, P);
     if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(DADMM_EINVAL, "dropout p=%g not in [0, 1)", drop_p);
@@ -937,6 +940,9 @@ int dadmm_hyper_gcn_train(int32_t B, int32_t P, int32_t K, int32_t N, const floa
     a.save_m = m_out;
     a.save_mean = mean_out;
     a.save_var = var_out;
+    // eval-mode BatchNorm (running statistics) inside the training epilogue, else batch statistics
+    a.bn_mean = bn_running_mean;
+    a.bn_var = bn_running_var;
     a.drop_p = drop_p;
     a.seed = seed;
     a.site = site;
@@ -949,13 +955,13 @@ int dadmm_hyper_gcn_train_bwd(int32_t B, int32_t P, int32_t N, const float* dy, 
                               const float* mean, const float* var, const float* bn_weight,
                               float bn_eps, const float* ahat, int32_t ahat_per_sample, float slope,
                               float drop_p, uint64_t seed, int32_t site, float* dz, float* part,
-                              void* stream) {
+                              int32_t bn_eval, void* stream) {
     if (B < 0 || P < 2 || P > 64 || N < 1) return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d N=%d", B, P, N);
     if (!dy || !m || !mean || !var || !bn_weight || !ahat || !dz || !part)
         return fail(DADMM_EINVAL, "a required pointer is NULL");
     if ((int64_t)B * P * N >= ((int64_t)1 << 31)) return fail(DADMM_EUNSUPPORTED, "operand larger than 2^31 floats");
     dadmm::GcnBwdArgs a{dy, m, mean, var, bn_weight, ahat, ahat_per_sample ? 1 : 0, dz, part, B, P, N,
-                        bn_eps, slope, drop_p, seed, site};
+                        bn_eps, slope, drop_p, seed, site, bn_eval ? 1 : 0};
     hipError_t e = dadmm::launch_gcn_bwd(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(DADMM_EHIP, "gcn backward launch: %s", hipGetErrorString(e));
     return ok();

@@ -457,6 +457,16 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             for (int task = threadIdx.x; task < ns * TN; task += THREADS) {
                 const int sl = task / TN, c = task - sl * TN;
                 if (c >= cols) continue;
+                if (a.bn_mean != nullptr) {
+                    // eval-mode BatchNorm (model.eval() with autograd): the running statistics,
+                    // saved per sample like batch statistics for the backward
+                    const float mean = a.bn_mean[col0 + c], var = a.bn_var[col0 + c];
+                    smean[sl * TN + c] = mean;
+                    srstd[sl * TN + c] = 1.0f / sqrtf(var + a.bn_eps);
+                    a.save_mean[(size_t)(s0 + sl) * a.N + col0 + c] = mean;
+                    a.save_var[(size_t)(s0 + sl) * a.N + col0 + c] = var;
+                    continue;
+                }
                 const float* mc = mt + sl * P * ZS + c;
                 float sum = 0.0f;
                 for (int q = 0; q < P; ++q) {

@@ -95,6 +95,9 @@ int check_net(const dadmm_hyper_net* net, int B) {
         if (net->dec_width[j] < 4 || (net->dec_width[j] & 3) || !net->dec_w[j] || !net->dec_b[j] ||
             !net->ln_w[j] || !net->ln_b[j])
             return DADMM_EINVAL;
+    if (net->bn_eval)
+        for (int i = 0; i < 5; ++i)
+            if (!net->bn_rm[i] || !net->bn_rv[i]) return DADMM_EINVAL;
     if (!net->norm_w || !net->norm_b || !net->fc_w || !net->fc_b) return DADMM_EINVAL;
     return DADMM_OK;
 }
@@ -164,7 +167,8 @@ int dadmm_hyper_train_forward(const dadmm_hyper_net* net, int32_t B, const float
         TRY(dadmm_hyper_gcn_train(B, P, K, N, x1, ld1, K1, x2, ld2, net->conv_w[i], net->conv_b[i], ahat,
                                   ahat_per_sample, net->bn_w[i], net->bn_b[i], net->bn_eps[i], LEAKY,
                                   i < 4 ? net->drop_enc : 0.0f, seed, i, sv->y[i], N, sv->m[i], sv->mean[i],
-                                  sv->var[i], stream));
+                                  sv->var[i], net->bn_eval ? net->bn_rm[i] : nullptr,
+                                  net->bn_eval ? net->bn_rv[i] : nullptr, stream));
         x1 = sv->y[i];
         ld1 = N;
         K1 = N;
@@ -257,7 +261,7 @@ static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* At
         float* part = defer ? d.pgcn[i] : w.part;
         TRY(dadmm_hyper_gcn_train_bwd(B, P, N, dx, sv->m[i], sv->mean[i], sv->var[i], net->bn_w[i],
                                       net->bn_eps[i], ahat, ahat_per_sample, LEAKY, i < 4 ? net->drop_enc : 0.0f,
-                                      seed, i, dZ, part, stream));
+                                      seed, i, dZ, part, net->bn_eval, stream));
         if (!defer) TRY(dadmm_hyper_colsum(part, 3, B, N, g->bn_wbc[i], 1, stream));
         if (i > 0) {
             const int Kin = net->width[i - 1];

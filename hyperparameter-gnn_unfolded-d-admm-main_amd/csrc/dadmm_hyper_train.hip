@@ -16,6 +16,7 @@
 //   Dropout: dx = dy * keep / (1 - p);   leaky_relu: dx = dy * (x > 0 ? 1 : slope);
 //   BatchNorm (batch statistics of the P nodes of a sample, biased variance):
 //     dx = gamma rstd (dxn - mean(dxn) - xhat mean(dxn xhat)),  dgamma = sum dxn xhat, dbeta = sum dxn;
+//   BatchNorm in eval mode (running statistics: constants): dx = gamma rstd dxn, same dgamma / dbeta;
 //   LayerNorm over C columns: the same with the row's statistics and per-column affine;
 //   clamp(x, lo, hi): dx = dy * (lo <= x <= hi);  sigmoid: dx = dy * s (1 - s).
 // Sums run in fixed orders (deterministic); results agree with torch to f32 rounding.
@@ -86,11 +87,12 @@ __global__ __launch_bounds__(NT) void gcn_bwd_kernel(GcnBwdArgs a) {
                 sg += g * xr[p];
                 gr[p] = g;
             }
-            const float inv = 1.0f / (float)P;
+            // eval-mode BatchNorm (running statistics): the mean / var are constants, dt = gamma rstd dy
+            const float inv = a.bn_eval ? 0.0f : 1.0f / (float)P;
 #pragma unroll
             for (int p = 0; p < PR; ++p) {
                 if (p >= P) break;
-                const float dt = gam * rstd * (gr[p] - sb * inv - xr[p] * (sg * inv));
+                const float dt = a.bn_eval ? gam * rstd * gr[p] : gam * rstd * (gr[p] - sb * inv - xr[p] * (sg * inv));
                 const float d = mr[p] > 0.0f ? dt : dt * a.slope;
                 sbias += d;
                 dm[p * CB + threadIdx.x] = d;
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(NT) void gcn_bwd_kernel(GcnBwdArgs a) {
                 const float t = mv > 0.0f ? mv : mv * a.slope;
                 const float xh = (t - mean) * rstd;
                 const float g = dm[p * CB + threadIdx.x];
-                const float dt = gam * rstd * (g - sb * inv - xh * (sg * inv));
+                const float dt = a.bn_eval ? gam * rstd * g : gam * rstd * (g - sb * inv - xh * (sg * inv));
                 const float d = mv > 0.0f ? dt : dt * a.slope;
                 sbias += d;
                 dm[p * CB + threadIdx.x] = d;

@@ -308,6 +308,7 @@ struct GcnBwdArgs {
     float eps, slope, drop_p;
     uint64_t seed;
     int site;
+    int bn_eval;            // BatchNorm on constant (running) statistics: no batch-statistics terms
 };
 hipError_t launch_gcn_bwd(const GcnBwdArgs& a, hipStream_t st);
 // hyper-parameter head: mode 0: hyp = head(z); mode 1: dz = dhyp * head'(z); z, hyp, dhyp [B][4H]

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
@@ -115,7 +115,9 @@ class HyperNet(ctypes.Structure):
                 ("ln_w", ctypes.c_void_p * 3), ("ln_b", ctypes.c_void_p * 3),
                 ("ln_eps", _f3), ("dec_slope", _f3), ("dec_drop", _f3),
                 ("fc_w", ctypes.c_void_p), ("fc_b", ctypes.c_void_p),
-                ("drop_enc", ctypes.c_float), ("maxv", ctypes.c_float * 4)]
+                ("drop_enc", ctypes.c_float), ("maxv", ctypes.c_float * 4),
+                # ABI 17: eval-mode BatchNorm (running statistics) in the training kernels
+                ("bn_rm", ctypes.c_void_p * 5), ("bn_rv", ctypes.c_void_p * 5), ("bn_eval", ctypes.c_int32)]
 
 
 class HyperSaved(ctypes.Structure):
@@ -218,9 +220,9 @@ def load() -> ctypes.CDLL:
     L.dadmm_hyper_linear_ln_scratch_bytes.argtypes = [i32, i32, i32]
     # training mode (model.train()): forward with dropout / batch statistics, and the backward
     for name, args in (("dadmm_hyper_gcn_train", [i32] * 4 + [vp, i32, i32, vp, i32] + [vp] * 3 + [i32]
-                        + [vp, vp, f32, f32, f32, u64, i32, vp, i32, vp, vp, vp, vp]),
+                        + [vp, vp, f32, f32, f32, u64, i32, vp, i32, vp, vp, vp, vp, vp, vp]),
                        ("dadmm_hyper_gcn_train_bwd", [i32] * 3 + [vp] * 5 + [f32, vp, i32, f32, f32, u64,
-                                                                          i32, vp, vp, vp]),
+                                                                          i32, vp, vp, i32, vp]),
                        ("dadmm_hyper_linear_ln_train", [i32, i32, i32, vp, i32, vp, vp, vp, vp, f32, i32,
                                                         f32, f32, u64, i32, vp, vp, vp, vp]),
                        ("dadmm_hyper_rownorm_bwd", [i32, i32, vp, vp, vp, vp, f32, i32, f32, f32, u64,

@@ -202,7 +202,8 @@ class GnnTrainFn(torch.autograd.Function):
                 Us.append(U)
                 Ds.append(D)
         run.finish()
-        hyper_ops.queue_running_stats(model, plan.stats(arena, K), run.P, defer=False)
+        if plan.train:   # eval mode (a backward through model.eval()): running statistics are inputs
+            hyper_ops.queue_running_stats(model, plan.stats(arena, K), run.P, defer=False)
         ctx.run, ctx.model, ctx.plan, ctx.a_hat, ctx.per_sample, ctx.seeds = run, model, plan, a_hat, per_sample, seeds
         ctx.arena, ctx.svs, ctx.As, ctx.Us, ctx.Ds = arena, svs, As, Us, Ds
         ctx.params = params

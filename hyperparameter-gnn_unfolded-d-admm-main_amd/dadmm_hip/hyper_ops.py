@@ -31,46 +31,11 @@ from .ops import _ptr, _stream
 LEAKY_SLOPE = 0.01   # F.leaky_relu / nn.LeakyReLU default negative_slope (reference :52-68, :97)
 
 
-class HyperEvalFn(torch.autograd.Function):
-    """hyp_k [B, 4, H] of one iteration in eval mode WITH autograd (VERDICT r3 missing #4: the
-    reference runs its modules under any grad mode, gnn_dlasso_models_progressive.py:165-196).
-    Forward: the fused inference kernels (hypernetwork_eval: BatchNorm on running statistics, no
-    dropout). Backward: torch autograd through the model's batched torch composition
-    (model.hypernetwork, eval mode) recomputed from the saved inputs — the same function, so the
-    gradients are those of the forward's values to f32 rounding. Inputs: AtAy [B, P, n_store]
-    (differentiable), Atb, ahat, the model, n, per-sample flag, the HyperBuffers, then the
-    hypernetwork's parameters (param_list order) so that autograd delivers their gradients."""
-
-    @staticmethod
-    def forward(ctx, AtAy, Atb, ahat, model, n, per_sample, bufs, *params):
-        hypernetwork_eval(model, AtAy, Atb, n, ahat, per_sample, bufs)
-        ctx.save_for_backward(AtAy, Atb, ahat)
-        ctx.model, ctx.n, ctx.n_params = model, n, len(params)
-        ctx.params = params
-        return bufs.hyp.clone()
-
-    @staticmethod
-    def backward(ctx, g):
-        AtAy, Atb, ahat = ctx.saved_tensors
-        model, n, params = ctx.model, ctx.n, ctx.params
-        B = AtAy.shape[0]
-        with torch.enable_grad():
-            x = AtAy.detach().requires_grad_(True)
-            outs = model.hypernetwork(x[..., :n], Atb[..., :n].detach(), ahat)
-            hyp = torch.stack(outs, dim=1).reshape(B, 4, -1)
-            want = [x] + [p for p in params if p.requires_grad]
-            grads = torch.autograd.grad(hyp, want, g, allow_unused=True)
-        gx = grads[0]
-        it = iter(grads[1:])
-        gp = tuple(next(it) if p.requires_grad else None for p in params)
-        ctx.params = None
-        return (gx, None, None, None, None, None, None) + gp
-
-
 def supported(model, n: int) -> bool:
     """Whether ``model`` (a DLASSO_GNNHyp3_Progressive) can run its hypernetwork through the
-    fused kernels: eval mode, standard BatchNorm / LayerNorm modules, every feature width a
-    multiple of 4 (16-byte operand rows) and LayerNorm widths <= 2048."""
+    fused kernels: eval mode, standard BatchNorm / LayerNorm modules, every hidden feature width
+    a multiple of 4 (16-byte operand rows) and LayerNorm widths <= 2048. Any n: layer 1's input
+    cat(AtAy, Atb) of width 2n is zero-padded to a multiple of 4 (``layer1_input``)."""
     if model.training:
         return False
     enc = model.encoder
@@ -81,11 +46,34 @@ def supported(model, n: int) -> bool:
     if any(not isinstance(ln, nn.LayerNorm) or not ln.elementwise_affine or len(ln.normalized_shape) != 1
            for ln in lns):
         return False
-    widths = [n, enc.conv1.lin.out_features, enc.conv2.lin.out_features, enc.conv3.lin.out_features,
+    widths = [enc.conv1.lin.out_features, enc.conv2.lin.out_features, enc.conv3.lin.out_features,
               model.decoder[4].out_features, model.decoder[8].out_features]
     if any(w % 4 for w in widths):
         return False
     return all(ln.normalized_shape[0] <= 2048 for ln in lns)
+
+
+def layer1_input(model, AtAy, Atb, n):
+    """Layer 1's operands when cat(AtAy, Atb) (:165) cannot be read in place (n % 16 != 0):
+    (x [B*P, Kp], W1 [N, Kp], Kp) with Kp = 2n rounded up to a multiple of 4 (16-byte rows, what
+    the GEMM kernels read); the padding columns of x and of the weight copy are zero, so
+    x W1^T is the unpadded product (the extra terms are exact zeros). The weight copy is one
+    buffer per model, refreshed from conv1's weight on every call (captured HIP graphs included)."""
+    B, P, _ = AtAy.shape
+    K = 2 * n
+    Kp = (K + 3) & ~3
+    x = torch.cat([AtAy[..., :n], Atb[..., :n]], dim=2).reshape(B * P, K)
+    w = model.encoder.conv1.lin.weight
+    if Kp == K:
+        return x.contiguous(), w, K
+    x = torch.nn.functional.pad(x, (0, Kp - K))
+    ent = _cache(model)
+    wp = ent.get("w1_padded")
+    if wp is None or wp.shape != (w.shape[0], Kp) or wp.device != w.device:
+        wp = ent["w1_padded"] = torch.zeros((w.shape[0], Kp), device=w.device, dtype=w.dtype)
+    with torch.no_grad():
+        wp[:, :K].copy_(w)
+    return x, wp, Kp
 
 
 class HyperBuffers:
@@ -135,11 +123,12 @@ def hypernetwork_eval(model, AtAy, Atb, n, ahat, per_sample, bufs: HyperBuffers)
     enc = model.encoder
     convs = (enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5)
     bns = (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)
+    w1 = model.encoder.conv1.lin.weight
     if n % 16 == 0:   # cat(AtAy, Atb) (:165) read in place from the two buffers
         x1, ld1, K1, x2, ld2, K = AtAy, ns, n, Atb, ns, 2 * n
     else:
-        xc = torch.cat([AtAy[..., :n], Atb[..., :n]], dim=2).reshape(B * P, 2 * n).contiguous()
-        x1, ld1, K1, x2, ld2, K = xc, 2 * n, 2 * n, None, 0, 2 * n
+        xc, w1, Kp = layer1_input(model, AtAy, Atb, n)
+        x1, ld1, K1, x2, ld2, K = xc, Kp, Kp, None, 0, Kp
     with torch.cuda.device(dev):
         for i, (conv, bn) in enumerate(zip(convs, bns)):
             N = conv.lin.out_features
@@ -154,7 +143,7 @@ def hypernetwork_eval(model, AtAy, Atb, n, ahat, per_sample, bufs: HyperBuffers)
                 x1, ld1, K1, x2, ld2, K = y, y.shape[1], N, None, 0, N
                 continue
             _lib.check("dadmm_hyper_gcn", L.dadmm_hyper_gcn(
-                B, P, K, N, _ptr(x1), ld1, K1, _ptr(x2), ld2, _ptr(conv.lin.weight),
+                B, P, K, N, _ptr(x1), ld1, K1, _ptr(x2), ld2, _ptr(w1 if i == 0 else conv.lin.weight),
                 _ptr(conv.bias), _ptr(ahat), int(per_sample), _ptr(bn.running_mean),
                 _ptr(bn.running_var), _ptr(bn.weight), _ptr(bn.bias), float(bn.eps), LEAKY_SLOPE,
                 _ptr(y), y.shape[1], stream))
@@ -187,14 +176,18 @@ def hypernetwork_eval(model, AtAy, Atb, n, ahat, per_sample, bufs: HyperBuffers)
 # ---- training mode (model.train()) ------------------------------------------------------------
 
 def supported_train(model, n: int) -> bool:
-    """Whether the training-mode hypernetwork can run on the HIP kernels: train mode, the
-    standard modules of the reference (Dropout, BatchNorm1d with affine + running statistics,
-    LayerNorm), P >= 2 (batch statistics over the nodes) and 4-aligned feature widths."""
-    if not model.training or model.P < 2:
+    """Whether the differentiable hypernetwork can run on the HIP training kernels: the standard
+    modules of the reference (Dropout, BatchNorm1d with affine + running statistics, LayerNorm),
+    P >= 2 and 4-aligned feature widths. In train mode the BatchNorms use the samples' batch
+    statistics and the Dropouts their p; in eval mode (a backward through model.eval(), e.g.
+    torch.autograd.grad of a validation loss) the same kernels run with the running statistics
+    and no dropout (the network torch's eval mode computes)."""
+    if model.P < 2:
         return False
     enc = model.encoder
     bns = (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)
-    if any(not (bn.affine and bn.track_running_stats and bn.momentum is not None) for bn in bns):
+    if any(not (bn.affine and bn.track_running_stats and bn.momentum is not None
+                and bn.running_mean is not None) for bn in bns):
         return False
     drops = [enc.dropout] + [model.decoder[i] for i in (1, 5, 9)]
     if any(not isinstance(d, nn.Dropout) for d in drops):
@@ -203,7 +196,8 @@ def supported_train(model, n: int) -> bool:
     if any(not isinstance(ln, nn.LayerNorm) or not ln.elementwise_affine or len(ln.normalized_shape) != 1
            or ln.normalized_shape[0] > 2048 for ln in lns):
         return False
-    widths = [n, enc.conv1.lin.out_features, enc.conv2.lin.out_features, enc.conv3.lin.out_features,
+    # (any n: layer 1's 2n-wide input is zero-padded to a multiple of 4 by layer1_input)
+    widths = [enc.conv1.lin.out_features, enc.conv2.lin.out_features, enc.conv3.lin.out_features,
               enc.conv5.lin.out_features, model.decoder[0].out_features, model.decoder[4].out_features,
               model.decoder[8].out_features]
     return all(w % 4 == 0 for w in widths)
@@ -295,13 +289,17 @@ class HyperTrainFn(torch.autograd.Function):
         enc = model.encoder
         convs = (enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5)
         bns = (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)
-        p_enc = float(enc.dropout.p)
+        train = model.training
+        ctx.train = train
+        # eval mode: Dropout is the identity and BatchNorm normalises with its running statistics
+        p_enc = float(enc.dropout.p) if train else 0.0
         rows = B * P
+        w1 = enc.conv1.lin.weight
         if n % 16 == 0:   # cat(AtAy, Atb) (:165) read in place
             x1, ld1, K1, x2, ld2, K = AtAy, ns, n, Atb, ns, 2 * n
         else:
-            xc = torch.cat([AtAy[..., :n], Atb[..., :n]], dim=2).reshape(rows, 2 * n).contiguous()
-            x1, ld1, K1, x2, ld2, K = xc, 2 * n, 2 * n, None, 0, 2 * n
+            xc, w1, Kp = layer1_input(model, AtAy, Atb, n)
+            x1, ld1, K1, x2, ld2, K = xc, Kp, Kp, None, 0, Kp
         x1in = (x1, ld1, K1, x2, ld2)   # layer 1's input, for its weight gradient
         saved = []          # per GCN layer: (M, mean, var)
         stats = []          # per GCN layer: (bn, mean, var) for the running statistics
@@ -314,13 +312,14 @@ class HyperTrainFn(torch.autograd.Function):
                 mean = torch.empty((B, N), device=dev)
                 var = torch.empty((B, N), device=dev)
                 _lib.check("dadmm_hyper_gcn_train", L.dadmm_hyper_gcn_train(
-                    B, P, K, N, _ptr(x1), ld1, K1, _ptr(x2), ld2, _ptr(conv.lin.weight),
+                    B, P, K, N, _ptr(x1), ld1, K1, _ptr(x2), ld2, _ptr(w1 if i == 0 else conv.lin.weight),
                     _ptr(conv.bias), _ptr(ahat), int(per_sample), _ptr(bn.weight), _ptr(bn.bias),
                     float(bn.eps), LEAKY_SLOPE, p_enc if i < 4 else 0.0, seed, i, _ptr(y), N, _ptr(M),
-                    _ptr(mean), _ptr(var), stream))
-                if defer:
+                    _ptr(mean), _ptr(var), None if train else _ptr(bn.running_mean),
+                    None if train else _ptr(bn.running_var), stream))
+                if train and defer:   # (eval mode: the running statistics are inputs, not updated)
                     stats.append((bn, mean, var))
-                else:
+                elif train:
                     with torch.no_grad():
                         _update_running_stats(bn, mean, var, P)
                 saved.append((M, mean, var))
@@ -344,7 +343,7 @@ class HyperTrainFn(torch.autograd.Function):
                 _lib.check("dadmm_hyper_linear_ln_train", L.dadmm_hyper_linear_ln_train(
                     B, width, N, _ptr(x), width, _ptr(lin.weight), _ptr(lin.bias), _ptr(lnd.weight),
                     _ptr(lnd.bias), float(lnd.eps), 1, float(model.decoder[4 * blk + 3].negative_slope),
-                    float(model.decoder[4 * blk + 1].p), seed, 4 + blk, _ptr(out), _ptr(xd),
+                    float(model.decoder[4 * blk + 1].p) if train else 0.0, seed, 4 + blk, _ptr(out), _ptr(xd),
                     _ptr(scratch), stream))
                 dec_in.append(x)
                 dec_xd.append(xd)
@@ -358,7 +357,7 @@ class HyperTrainFn(torch.autograd.Function):
             mx = [float(model.alpha_max), float(model.tau_max), float(model.rho_max), float(model.eta_max)]
             _lib.check("dadmm_hyper_head_act", L.dadmm_hyper_head_act(
                 0, B, H, _ptr(z), None, *mx, _ptr(hyp), stream))
-        if defer:
+        if defer and train:
             if not hasattr(model, "_bn_pending"):
                 model._bn_pending = []
             model._bn_pending.append((stats, P))
@@ -389,7 +388,8 @@ class HyperTrainFn(torch.autograd.Function):
         enc = model.encoder
         convs = (enc.conv1, enc.conv2, enc.conv3, enc.conv4, enc.conv5)
         bns = (enc.bn1, enc.bn2, enc.bn3, enc.bn4, enc.bn5)
-        p_enc = float(enc.dropout.p)
+        train = ctx.train
+        p_enc = float(enc.dropout.p) if train else 0.0
         H = model.fc.out_features // 4
         acc = _GradAccumulator.current(model, dev)
         chk = _lib.check
@@ -411,7 +411,8 @@ class HyperTrainFn(torch.autograd.Function):
                 chk("dadmm_hyper_rownorm_bwd", L.dadmm_hyper_rownorm_bwd(
                     B, N, _ptr(dx), _ptr(ctx.dec_xd[blk]), _ptr(lnd.weight), _ptr(lnd.bias),
                     float(lnd.eps), 1, float(model.decoder[4 * blk + 3].negative_slope),
-                    float(model.decoder[4 * blk + 1].p), ctx.seed, 4 + blk, _ptr(dv), _ptr(part), stream))
+                    float(model.decoder[4 * blk + 1].p) if train else 0.0, ctx.seed, 4 + blk, _ptr(dv),
+                    _ptr(part), stream))
                 acc.colsum(part, 1, nbytes // (4 * 2 * N), 2 * N, lnd.weight)   # -> ln.weight, ln.bias
                 acc.wgrad(B, N, Kin, dv, N, ctx.dec_in[blk], Kin, Kin, None, 0, lin.weight, lin.bias)
                 dx = acc.input_grad(B, dv, N, lin.weight)           # [B, Kin]
@@ -436,13 +437,17 @@ class HyperTrainFn(torch.autograd.Function):
                 chk("dadmm_hyper_gcn_train_bwd", L.dadmm_hyper_gcn_train_bwd(
                     B, P, N, _ptr(dx), _ptr(M), _ptr(mean), _ptr(var), _ptr(bn.weight),
                     float(bn.eps), _ptr(ctx.ahat), int(ctx.per_sample), LEAKY_SLOPE,
-                    p_enc if i < 4 else 0.0, ctx.seed, i, _ptr(dZ), _ptr(part), stream))
+                    p_enc if i < 4 else 0.0, ctx.seed, i, _ptr(dZ), _ptr(part), int(not train), stream))
                 acc.colsum(part, 3, B, N, bn.weight)          # -> bn.weight, bn.bias, conv.bias
                 Kin = conv.lin.in_features
                 if i == 0:
-                    # layer 1's input cat(AtAy, Atb) read in place; only d AtAy is needed
+                    # layer 1's input cat(AtAy, Atb) (read in place, or zero-padded to Kp columns
+                    # by layer1_input); only d AtAy is needed
                     x1, ld1, K1, x2, ld2 = ctx.x1in
-                    acc.wgrad(rows, N, Kin, dZ, N, x1, ld1, K1, x2, ld2, conv.lin.weight, None)
+                    if x2 is None and K1 != Kin:   # padded: dW1 = the first 2n columns
+                        acc.wgrad_cols(rows, N, K1, dZ, N, x1, ld1, conv.lin.weight, Kin)
+                    else:
+                        acc.wgrad(rows, N, Kin, dZ, N, x1, ld1, K1, x2, ld2, conv.lin.weight, None)
                     acc.input_grad(rows, dZ, N, conv.lin.weight, cols=n, out=dAtAy, ldo=ns)
                 else:
                     acc.wgrad(rows, N, Kin, dZ, N, ctx.xs[i], Kin, Kin, None, 0, conv.lin.weight, None)
@@ -531,12 +536,17 @@ class NativeHyperPlan:
             net.dec_w[j], net.dec_b[j] = lins[j].weight.data_ptr(), lins[j].bias.data_ptr()
             net.ln_w[j], net.ln_b[j], net.ln_eps[j] = lns[j].weight.data_ptr(), lns[j].bias.data_ptr(), float(lns[j].eps)
             net.dec_slope[j] = float(acts[j].negative_slope)
-            net.dec_drop[j] = float(drops[j].p)
+            net.dec_drop[j] = float(drops[j].p) if model.training else 0.0
         net.H = model.fc.out_features // 4
         net.fc_w, net.fc_b = model.fc.weight.data_ptr(), model.fc.bias.data_ptr()
-        net.drop_enc = float(enc.dropout.p)
+        net.drop_enc = float(enc.dropout.p) if model.training else 0.0
         for c, v in enumerate((model.alpha_max, model.tau_max, model.rho_max, model.eta_max)):
             net.maxv[c] = float(v)
+        # eval mode (model.eval() under autograd): BatchNorm on the running statistics, no dropout
+        net.bn_eval = 0 if model.training else 1
+        for i, bn in enumerate(bns):
+            net.bn_rm[i], net.bn_rv[i] = bn.running_mean.data_ptr(), bn.running_var.data_ptr()
+        self.train = model.training
         self.net = net
         self.bns = bns
         self.H = H = net.H
@@ -567,15 +577,16 @@ class NativeHyperPlan:
         convs, bns, lins, lns, drops, _ = _modules(model)
         params = param_list(model)
         key = (B, P, n, ns, dev, tuple(p.data_ptr() for p in params), float(model.encoder.dropout.p),
-               tuple(float(d.p) for d in drops),
+               tuple(float(d.p) for d in drops), model.training,
+               tuple((bn.running_mean.data_ptr(), bn.running_var.data_ptr()) for bn in bns),
                (float(model.alpha_max), float(model.tau_max), float(model.rho_max), float(model.eta_max)))
         plans = _cache(model)["plans"]
-        plan = plans.get((B, dev))
+        plan = plans.get((B, dev, model.training))
         if plan is None or plan.key != key:
             if len(plans) > 8:
                 plans.clear()
             plan = NativeHyperPlan(model, B, P, n, ns, dev, key)
-            plans[(B, dev)] = plan
+            plans[(B, dev, model.training)] = plan
         return plan
 
     def saved(self, arena, k=0):
@@ -649,7 +660,8 @@ def _native_forward(ctx, L, AtAy, Atb, ahat, model, n, per_sample, seed, defer):
     sv = plan.saved(arena)
     with torch.cuda.device(dev):
         plan.forward(AtAy, Atb, ahat, per_sample, seed, sv, _stream(dev))
-    queue_running_stats(model, plan.stats(arena, 1), P, defer)
+    if plan.train:   # eval mode: the running statistics were inputs
+        queue_running_stats(model, plan.stats(arena, 1), P, defer)
     ctx.model, ctx.n, ctx.per_sample, ctx.seed = model, n, per_sample, seed
     ctx.arena, ctx.sv, ctx.plan = arena, sv, plan
     ctx.AtAy, ctx.Atb, ctx.ahat = AtAy, Atb, ahat
@@ -743,6 +755,18 @@ class _GradAccumulator:
         _lib.check("dadmm_hyper_wgrad", self.L.dadmm_hyper_wgrad(
             R, N, K, _ptr(dz), ldz, _ptr(x1), ld1, K1, _ptr(x2), ld2, ctypes.c_void_p(self.ptr(weight)),
             gb, 1, _ptr(self.scratch), self.stream))
+
+    def wgrad_cols(self, R, N, Kp, dz, ldz, x, ldx, weight, K):
+        """dW (+)= (dZ^T X)[:, :K] for an input zero-padded to Kp > K columns (layer1_input):
+        the padded product into a scratch tile, its first K columns added to weight's slot."""
+        nb = self.L.dadmm_hyper_wgrad_scratch_bytes(R, N, Kp)
+        if nb > 4 * self.scratch.numel():
+            self.scratch = torch.empty(nb // 4 + 4, device=self.dev)
+        tmp = torch.empty((N, Kp), device=self.dev)
+        _lib.check("dadmm_hyper_wgrad", self.L.dadmm_hyper_wgrad(
+            R, N, Kp, _ptr(dz), ldz, _ptr(x), ldx, Kp, None, 0, _ptr(tmp), None, 0,
+            _ptr(self.scratch), self.stream))
+        self.view(weight).add_(tmp[:, :K])
 
     def colsum(self, part, G, R, C, first):
         _lib.check("dadmm_hyper_colsum", self.L.dadmm_hyper_colsum(

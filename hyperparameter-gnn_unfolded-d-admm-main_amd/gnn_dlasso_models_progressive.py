@@ -17,7 +17,8 @@ in inference (model.eval() under no_grad) on the fused HIP kernels of ``dadmm_hi
 (model.train(): Dropout, per-sample BatchNorm batch statistics, autograd) on the training kernels
 (``hyper_ops.HyperTrainFn`` / ``gnn_ops.GnnTrainFn``: the same GEMMs with train epilogues, and
 HIP backward kernels for every term, the linears' weight / input GEMMs included
-(csrc/dadmm_hyper_grad.hip, csrc/dadmm_hyper.hip)).
+(csrc/dadmm_hyper_grad.hip, csrc/dadmm_hyper.hip)); model.eval() under autograd runs the same
+training kernels with BatchNorm on its running statistics and no dropout (round 5).
 ``hyper_backend = "torch"`` selects the batched torch composition below instead (tests).
 
 GCNConv (torch_geometric; absent here, unpinned version) is restated from its
@@ -184,8 +185,8 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         self._op = None
         self._op_key = None
         self.last_status = None
-        # "auto": the fused HIP hypernetwork in inference (eval + no_grad), torch otherwise;
-        # "torch": always the torch composition (tests compare the two)
+        # "auto": the HIP hypernetwork kernels (inference kernels for eval + no_grad, the training
+        # kernels and their backward otherwise); "torch": always the torch composition (tests)
         self.hyper_backend = "auto"
         # inference forwards replay a captured HIP graph of the K-iteration loop (one launch of
         # ~16 K kernels instead of as many host calls); False: issue them one by one
@@ -193,8 +194,9 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         self._graph_plans = {}
         # optional observer, called every iteration with (AtAy_k, Atb, (alpha, tau, rho, eta))
         self.on_hyp = None
-        # which hypernetwork implementation the last forward ran: "hip-eval-graph", "hip-eval",
-        # "hip-train" or "torch"
+        # which hypernetwork implementation the last forward ran: "hip-eval-graph", "hip-eval"
+        # (inference kernels), "hip-train" (training kernels), "hip-eval-grad" (training kernels in
+        # eval mode: model.eval() under autograd) or "torch"
         self.last_backend = None
 
     @property
@@ -257,14 +259,11 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         n = self.n
         # inference (model.eval() under no_grad): the hypernetwork runs on the fused HIP kernels
         fused = self.hyper_backend == "auto" and not grad and hyper_ops.supported(self, n)
-        # training (model.train()): the HIP training-mode hypernetwork (dropout, batch statistics,
-        # its backward) — HyperTrainFn
-        train_hip = self.hyper_backend == "auto" and hyper_ops.supported_train(self, n)
-        # eval mode with autograd enabled: the inference kernels forward, torch autograd through
-        # the recomputed composition backward (hyper_ops.HyperEvalFn)
-        eval_grad = (self.hyper_backend == "auto" and grad and not self.training
-                     and hyper_ops.supported(self, n))
-        self.last_backend = "hip-eval-autograd" if eval_grad else self._backend_name(fused, train_hip)
+        # differentiable (model.train(), or model.eval() under autograd): the HIP training kernels
+        # and their backward (HyperTrainFn / GnnTrainFn) — dropout and batch statistics in train
+        # mode, running statistics and no dropout in eval mode
+        train_hip = self.hyper_backend == "auto" and not fused and hyper_ops.supported_train(self, n)
+        self.last_backend = self._backend_name(fused, train_hip)
         if fused and self.use_hip_graph and self.on_hyp is None:
             # the plan owns its device state: no per-forward GnnRun (its Y, Atb, G) is built
             return self._forward_graphed(bb, graphs, a_hat.contiguous(), y0, U0, d0, K, H)
@@ -274,9 +273,9 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         Atb = run.Atb[..., :n]
         y, U, D = run.ys[0], run.U0, run.d0
         ys = []
-        if fused or train_hip or eval_grad:
+        if fused or train_hip:
             a_hat = a_hat.contiguous()
-        if fused or eval_grad:
+        if fused:
             enc = self.encoder
             bufs = hyper_ops.HyperBuffers(batch_size, self.P, enc.conv5.lin.out_features,
                                           [self.decoder[i].out_features for i in (0, 4, 8)], H,
@@ -290,13 +289,10 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
                 alpha_k, tau_k, rho_k, eta_k = hyper_ops.hypernetwork_eval(
                     self, AtAy, run.Atb, n, a_hat, not graphs.shared, bufs)
                 hyp_k = bufs.hyp
-            elif eval_grad:
-                hyp_k = hyper_ops.HyperEvalFn.apply(AtAy, run.Atb, a_hat, self, n, not graphs.shared, bufs,
-                                                    *hyper_ops.param_list(self))
-                alpha_k, tau_k, rho_k, eta_k = (hyp_k[:, c].view(batch_size, H, 1, 1) for c in range(4))
             elif train_hip:
+                # eval mode draws no dropout seed (the reference's eval forward consumes no RNG)
                 hyp_k = hyper_ops.hypernetwork_train(self, AtAy, run.Atb, n, a_hat, not graphs.shared,
-                                                     defer=True)
+                                                     seed=None if self.training else 0, defer=True)
                 alpha_k, tau_k, rho_k, eta_k = (hyp_k[:, c].view(batch_size, H, 1, 1) for c in range(4))
             else:
                 alpha_k, tau_k, rho_k, eta_k = self.hypernetwork(AtAy[..., :n], Atb, a_hat)
@@ -318,7 +314,7 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         B, n = bb.shape[0], self.n
         run = GnnRun(self.operator(), bb, graphs, K, H, _lib.VARIANT_GNN, y0, U0, d0, False)
         plan = hyper_ops.NativeHyperPlan.get(self, B, self.P, n, run.op.n_store, bb.device)
-        seeds = [hyper_ops.draw_dropout_seed() for _ in range(K)]
+        seeds = [hyper_ops.draw_dropout_seed() if self.training else 0 for _ in range(K)]
         Y, hyp = GnnTrainFn.apply(run, self, plan, a_hat, not graphs.shared, seeds,
                                   *hyper_ops.param_list(self))
         self.last_status = run.status
@@ -349,11 +345,10 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         if fused:
             return "hip-eval-graph" if self.use_hip_graph and self.on_hyp is None else "hip-eval"
         if train_hip:
-            return "hip-train"
+            return "hip-train" if self.training else "hip-eval-grad"
         if self.hyper_backend != "torch" and not DLASSO_GNNHyp3_Progressive._warned_torch:
             DLASSO_GNNHyp3_Progressive._warned_torch = True
-            why = ("eval mode with autograd enabled" if not self.training else
-                   "a module or width the HIP kernels do not cover")
+            why = "a module or width the HIP kernels do not cover"
             warnings.warn(f"DLASSO_GNNHyp3_Progressive: hypernetwork on the torch composition ({why}); "
                           f"the D-ADMM iterations still run on HIP", RuntimeWarning, stacklevel=3)
         return "torch"

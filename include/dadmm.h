@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 16
+#define DADMM_ABI_VERSION 17
 
 enum {
     DADMM_OK = 0,
@@ -416,8 +416,12 @@ int dadmm_hyper_linear_ln(int32_t rows, int32_t K, int32_t N, const float* x, in
  *   m_out [B*P][N] = A_hat (x W^T) + bias and the per-sample mean_out / var_out [B][N] (biased
  *   variance: the normalisation; the caller updates the running statistics). P >= 2, N % 4 == 0.
  *   Replaces: GCNConv + F.leaky_relu + bn_i (train) + self.dropout of graph_conv (:52-68).
+ *   ABI 17: with bn_running_mean / bn_running_var (both non-NULL, [N]) the BatchNorm is the eval-mode
+ *   one (running statistics; they are written to mean_out / var_out per sample for the backward):
+ *   the layer of model.eval() with autograd (gnn_dlasso_models_progressive.py:52-68, eval).
  * dadmm_hyper_gcn_train_bwd: from dy [B*P][N] (gradient of that y) to dz [B*P][N] (gradient of
- *   x W^T), and part [3][B][N]: per-sample sums of dgamma, dbeta and d(GCNConv.bias).
+ *   x W^T), and part [3][B][N]: per-sample sums of dgamma, dbeta and d(GCNConv.bias). bn_eval:
+ *   mean / var are constants (running statistics): dx = gamma rstd dy, no batch-statistics terms.
  * dadmm_hyper_linear_ln_train: one decoder block Linear -> Dropout_p -> LayerNorm -> LeakyReLU?
  *   (:94-105) in train mode; xd [rows][N] = the LayerNorm input (post-dropout), for the backward.
  * dadmm_hyper_rownorm_bwd: backward of LayerNorm (+ LeakyReLU when act) rows from their input xd:
@@ -431,12 +435,13 @@ int dadmm_hyper_gcn_train(int32_t B, int32_t P, int32_t K, int32_t N, const floa
                           const float* ahat, int32_t ahat_per_sample, const float* bn_weight,
                           const float* bn_bias, float bn_eps, float slope, float drop_p, uint64_t seed,
                           int32_t site, float* y, int32_t ldy, float* m_out, float* mean_out,
-                          float* var_out, void* stream);
+                          float* var_out, const float* bn_running_mean, const float* bn_running_var,
+                          void* stream);
 int dadmm_hyper_gcn_train_bwd(int32_t B, int32_t P, int32_t N, const float* dy, const float* m,
                               const float* mean, const float* var, const float* bn_weight,
                               float bn_eps, const float* ahat, int32_t ahat_per_sample, float slope,
                               float drop_p, uint64_t seed, int32_t site, float* dz, float* part,
-                              void* stream);
+                              int32_t bn_eval, void* stream);
 int dadmm_hyper_linear_ln_train(int32_t rows, int32_t K, int32_t N, const float* x, int32_t ldx,
                                 const float* W, const float* bias, const float* ln_weight,
                                 const float* ln_bias, float eps, int32_t act, float slope, float drop_p,
@@ -505,6 +510,13 @@ typedef struct dadmm_hyper_net {
     const float* fc_b;
     float drop_enc;             /* the encoder's Dropout p                                        */
     float maxv[4];              /* alpha_max, tau_max, rho_max, eta_max                           */
+    /* ABI 17: bn_eval != 0 runs the same kernels with the module in eval mode (a backward of
+     * model.eval() under autograd): every BatchNorm normalises with its running statistics
+     * bn_rm / bn_rv [width_i] instead of the sample's batch statistics (which the saved
+     * mean / var slices then hold, per sample), and the caller sets every dropout p to 0.     */
+    const float* bn_rm[5];
+    const float* bn_rv[5];
+    int32_t bn_eval;
 } dadmm_hyper_net;
 typedef struct dadmm_hyper_saved {
     float* y[5];                /* [B*P][width_i] block outputs                                   */
