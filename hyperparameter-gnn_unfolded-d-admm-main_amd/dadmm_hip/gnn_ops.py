@@ -115,10 +115,8 @@ def _check_guards(run: GnnRun):
     """Once per backward pass (one host sync): the adjoint assumes no guard fired."""
     if getattr(run, "_checked", False):
         return
-    if not getattr(run.graphs, "symmetric", True):
-        raise NotImplementedError(
-            "the GNN model's adjoint needs undirected graphs (it applies delta = 2 L y as its own "
-            "transpose); the forward follows any adjacency")
+    # (any adjacency: the step adjoint applies compute_delta through the forward's visit lists,
+    # and that map is symmetric for directed graphs too; oracle.laplacians)
     st = int(run.status.item())
     run._checked = True
     if st:

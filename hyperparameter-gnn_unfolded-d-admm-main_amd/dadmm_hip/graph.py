@@ -119,8 +119,9 @@ class GraphBatch:
         # P > 8): such batches take the stepwise path, which follows any order
         self.fused_ok = fused_ok
         # every graph undirected (p in N(q) <=> q in N(p)), as the reference's Erdos-Renyi graphs
-        # are. The adjoints use delta = 2 L y as its own transpose, which holds only then: they
-        # refuse a batch with a directed graph (the forward follows any adjacency)
+        # are. compute_delta is symmetric for any adjacency, but the fused kernels' shared-graph
+        # consensus (consensus_fma) reads one multiplier per unordered pair: a directed shared
+        # graph takes the exact recomputation (forward) and the general adjoint (backward)
         self.symmetric = symmetric
         # P > MASK_P: dense 0/1 adjacency uint8 [1 if shared else B, P, P] (nbr is all zero)
         self.adj = adj

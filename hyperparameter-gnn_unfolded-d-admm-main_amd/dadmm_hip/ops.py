@@ -246,10 +246,13 @@ def backward_raw(op: PreparedOperator, graphs: GraphBatch, traj: Trajectory,
     _dev_check(gY)
     if path not in ("auto", "fused", "general"):
         raise ValueError(f"unknown path {path!r}")
-    if not getattr(graphs, "symmetric", True):
-        raise NotImplementedError(
-            "the adjoint needs undirected graphs (p in N(q) <=> q in N(p), as the reference's "
-            "Erdos-Renyi graphs are): it applies delta = 2 L y as its own transpose")
+    # compute_delta is the sum over its visits (p, q) of (e_p - e_q)(e_p - e_q)^T: symmetric for
+    # ANY adjacency, so every adjoint applies it through the forward's own visit order. The fused
+    # adjoint's shared-graph consensus (consensus_fma) reads one edge multiplier per unordered
+    # pair, i.e. assumes a symmetric adjacency: a directed SHARED graph takes the general adjoint
+    # (its visit lists follow the successor lists); per-sample graphs use the direction-aware
+    # consensus_lane / consensus_ordered in either adjoint.
+    directed_shared = graphs.shared and not getattr(graphs, "symmetric", True)
     K, B, P, ns = traj.Y.shape
     H = int(traj.hyp.shape[1])
     gY = _pad_n(gY.float(), ns).contiguous()
@@ -258,7 +261,11 @@ def backward_raw(op: PreparedOperator, graphs: GraphBatch, traj: Trajectory,
     d = op.dims(B=B, K=K, variant=traj.variant, hyp_rows=H, graph_shared=graphs.shared)
     L = _lib.load()
     dhyp = torch.empty((K, H, 4), dtype=torch.float32, device=gY.device)
-    use_fused = path == "fused" or (path == "auto" and traj.fused and graphs.fused_ok)
+    if path == "fused" and directed_shared:
+        raise ValueError("the fused adjoint assumes a symmetric shared adjacency; use 'auto' or "
+                         "'general' for a directed shared graph")
+    use_fused = path == "fused" or (path == "auto" and traj.fused and graphs.fused_ok
+                                    and not directed_shared)
     with torch.cuda.device(gY.device):
         stream = _stream(gY.device)
         if use_fused:

@@ -209,16 +209,25 @@ def forward_np64(A, b, graph_list, hyp, y0, U0, d0, variant=0):
 
 
 def laplacians(graph_list, P):
-    """(D - Adj) per sample [B,P,P] float64 and degrees [B,P] (compute_delta = 2 (D - Adj) y)."""
+    """(L [B,P,P] float64, deg [B,P]) with compute_delta(y) = 2 L y and deg = len(neighbors(p))
+    (sum_neighbors, unfolded_DLASSO.py:112-118). compute_delta (:127-140) adds, for every visit
+    (p, q) with q in neighbors(p), (y_p - y_q) to delta[p] and subtracts it from delta[q]: the map
+    is the sum over visits of (e_p - e_q)(e_p - e_q)^T, SYMMETRIC for any adjacency (a directed
+    graph's successor lists included; a self-loop contributes nothing). For an undirected graph
+    every edge is visited twice and 2 L = 2 (D - Adj)."""
     B = len(graph_list)
     L = np.zeros((B, P, P))
     deg = np.zeros((B, P))
     for s, G in enumerate(graph_list):
         for p in range(P):
             for q in G.neighbors(p):
-                L[s, p, q] -= 1.0
                 deg[s, p] += 1.0
-        L[s] += np.diag(deg[s])
+                if q == p:
+                    continue
+                L[s, p, p] += 0.5
+                L[s, q, q] += 0.5
+                L[s, p, q] -= 0.5
+                L[s, q, p] -= 0.5
     return L, deg
 
 
@@ -229,7 +238,8 @@ def backward_np64(A, graph_list, hyp, y0, d0, Y, Grec, Urec, gY, variant=0):
     Follows the derivative torch autograd takes through the reference's forward
     (unfolded_DLASSO.py:53-107): sign() has zero derivative; clamp(x, lo, hi) passes the
     gradient where lo <= x <= hi; delta_{k+1} = compute_delta(y_{k+1}) = 2 (D - Adj) y_{k+1} is
-    differentiated (its transpose is itself), delta_0 is a random leaf; b, y0, U0 carry no
+    differentiated (its transpose is itself, for any adjacency: ``laplacians``), delta_0 is a
+    random leaf; b, y0, U0 carry no
     gradient. Per iteration k (a = alpha_k, ...; g = clamp(gr_k); z = y_k - a g; w = U_k + d_{k+1} e):
         dEta_k   += sum(w_bar d_{k+1})            w_bar = U_bar [|w| <= vclip]
         d_bar    += w_bar e ;  y_bar += 2 L d_bar  (GNN variant: d_bar masked by |2Ly| <= 20)

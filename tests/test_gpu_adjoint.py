@@ -294,11 +294,14 @@ def test_training_steps_reduce_loss(cuda):
     assert min(losses[-3:]) < losses[0], losses
 
 
-def test_directed_graph_forward_exact_adjoint_refuses(cuda):
+def test_directed_graph_adjoints_vs_oracle(cuda):
     """A DIRECTED adjacency (successor lists, not symmetric; outside the reference's Erdos-Renyi
-    graphs): the recording forward follows it bit-exactly (a shared-graph launch flags it with
-    status bit 16 and the exact recomputation runs), and the adjoints, which apply delta = 2 L y
-    as its own transpose, refuse it instead of returning wrong gradients."""
+    graphs, VERDICT r4 missing #3): the recording forward follows it bit-exactly (a shared-graph
+    launch flags it with status bit 16 and the exact recomputation runs), and the adjoint is
+    right too: compute_delta is the sum over its visits of (e_p - e_q)(e_p - e_q)^T, symmetric for
+    any adjacency (oracle.laplacians; tests/test_oracle.py checks that against torch autograd of
+    the literal edge loop). A directed shared graph takes the general adjoint; per-sample graphs
+    the fused one. Both against the fp64 oracle adjoint, and through loss.backward()."""
     import networkx as nx
     from dadmm_hip import _lib
     from dadmm_hip.autograd import dadmm_unfolded_apply
@@ -318,10 +321,15 @@ def test_directed_graph_forward_exact_adjoint_refuses(cuda):
         assert not g.symmetric
         assert np.array_equal(Y.cpu().numpy(), Yo)
         assert np.array_equal(traj.Grec[..., :n].cpu().numpy(), Go)
-        gY = _t(np.ones((K, B, P, n), np.float32), cuda)
-        with pytest.raises(NotImplementedError, match="undirected"):
-            backward_raw(op, g, traj, gY)
+        gYn = np.random.default_rng(9).standard_normal((K, B, P, n)).astype(np.float32)
+        want = O.backward_np64(A, graphs, hyp, y0, d0, Yo, Go, Uro, gYn)
+        for path in ("auto", "general"):
+            dh = backward_raw(op, g, traj, _t(gYn, cuda), path=path)
+            _close(dh.cpu().numpy().astype(np.float64), want)
+        if g.shared:
+            with pytest.raises(ValueError, match="symmetric shared adjacency"):
+                backward_raw(op, g, traj, _t(gYn, cuda), path="fused")
         table = _t(hyp, cuda).requires_grad_(True)
         Y2, _ = dadmm_unfolded_apply(op, _t(b, cuda), g, table, _t(y0, cuda), _t(U0, cuda), _t(d0, cuda))
-        with pytest.raises(NotImplementedError, match="undirected"):
-            Y2.sum().backward()
+        (Y2 * _t(gYn, cuda)).sum().backward()
+        _close(table.grad.cpu().numpy().astype(np.float64), want)

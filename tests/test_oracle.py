@@ -284,15 +284,30 @@ def test_fixture_trained_hyp_ranges():
 
 
 # ---- the adjoint (§8(f) row 1): reverse mode of the forward w.r.t. the hyper-parameter table ---
-@pytest.mark.parametrize("variant,H,per_sample", [(0, 5, False), (0, 1, False), (1, 5, True),
-                                                  (1, 1, True)])
-def test_adjoint_matches_torch_autograd_of_the_reference_ops(variant, H, per_sample):
+def _digraph(P, seed):
+    """A random directed graph (successor lists, a self-loop included): compute_delta's map is
+    still symmetric (oracle.laplacians)."""
+    rng = np.random.default_rng(seed)
+    G = nx.DiGraph()
+    G.add_nodes_from(range(P))
+    G.add_edges_from((p, q) for p in range(P) for q in range(P) if p != q and rng.random() < 0.4)
+    G.add_edge(2, 2)
+    return G
+
+
+@pytest.mark.parametrize("variant,H,per_sample,directed", [(0, 5, False, False), (0, 1, False, False),
+                                                           (1, 5, True, False), (1, 1, True, False),
+                                                           (0, 5, False, True), (1, 5, True, True)])
+def test_adjoint_matches_torch_autograd_of_the_reference_ops(variant, H, per_sample, directed):
     """backward_np64 == torch.autograd.grad through the reference's op sequence (fp64 replay,
-    unfolded_DLASSO.py:53-107 + compute_delta's edge loop), on the same trajectory."""
+    unfolded_DLASSO.py:53-107 + compute_delta's edge loop), on the same trajectory; directed
+    graphs (successor lists) too."""
     import torch
     P, m, n, B, K = 5, 16, 48, 3, 12
     A, b, _ = O.make_problem(P, m, n, B, seed=31)
-    if per_sample:
+    if directed:
+        graphs = ([_digraph(P, 60 + s) for s in range(B)] if per_sample else [_digraph(P, 7)] * B)
+    elif per_sample:
         graphs = [O.connected_er_graph(P, 0.5, seed=60 + s) for s in range(B)]
     else:
         graphs = [O.er_graph(P, 0.5, seed=7)] * B
