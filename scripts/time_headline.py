@@ -68,9 +68,18 @@ for rnd in range(rounds):
         Y, _, st = out
         with torch.no_grad():
             ms_f, (Ym, _) = timed(lambda: model(bt[..., None], graph_list), reps)
+            # host time to enqueue one module forward (no sync inside the loop): when it nears the
+            # GPU time, the step becomes host-bound
+            import time as _time
+            torch.cuda.synchronize()
+            t0 = _time.perf_counter()
+            for _ in range(reps):
+                model(bt[..., None], graph_list)
+            host_ms = (_time.perf_counter() - t0) * 1e3 / reps
+            torch.cuda.synchronize()
         print(json.dumps({"lib": os.path.basename(os.environ.get("DADMM_LIB_VARIANT", "libdadmm.so")),
                           "round": rnd, "division": div, "cfg": [B, P, n, m, K],
-                          "kernel_ms": ms_k, "module_forward_ms": ms_f,
+                          "kernel_ms": ms_k, "module_forward_ms": ms_f, "host_enqueue_ms": host_ms,
                           "M_iters_per_s": B * K / ms_f / 1e3, "status": int(st.item()),
                           "Ysum": float(Y.double().sum())}),
               flush=True)

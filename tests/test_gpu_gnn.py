@@ -277,10 +277,10 @@ def test_backward_matches_cpu_autograd(cuda, mode, n, directed):
         rng = np.random.default_rng(4)
         graphs = []
         for _ in range(B):
-            G = nx.DiGraph()
-            G.add_nodes_from(range(P))
-            G.add_edges_from((p, q) for p in range(P) for q in range(P) if p != q and rng.random() < 0.5)
-            graphs.append(G)
+            dg = nx.DiGraph()
+            dg.add_nodes_from(range(P))
+            dg.add_edges_from((p, q) for p in range(P) for q in range(P) if p != q and rng.random() < 0.5)
+            graphs.append(dg)
     gen = torch.Generator().manual_seed(11)
     enc = model.encoder
     with torch.no_grad():
