@@ -951,6 +951,61 @@ int dadmm_hyper_gcn_train(int32_t B, int32_t P, int32_t K, int32_t N, const floa
     return ok();
 }
 
+static int bn_running_splits(int32_t iters, int32_t B) {
+    // ~64 rows per split (16 per wave): enough blocks to spread the sums over the chip
+    const int64_t T = (int64_t)iters * B;
+    const int64_t s = T / 64;
+    return s < 1 ? 1 : (s > 256 ? 256 : (int)s);
+}
+
+size_t dadmm_hyper_bn_running_scratch_bytes(int32_t layers, const int32_t* widths, int32_t iters,
+                                            int32_t B) {
+    if (layers < 1 || layers > dadmm::BN_MAX_LAYERS || !widths || iters < 1 || B < 1) return 0;
+    size_t total = 0;
+    for (int i = 0; i < layers; ++i) total += widths[i] > 0 ? (size_t)widths[i] : 0;
+    return 8 * 2 * total * (size_t)bn_running_splits(iters, B);
+}
+
+int dadmm_hyper_bn_running_update(int32_t layers, const int32_t* widths, float* const* running_mean,
+                                  float* const* running_var, int64_t* const* tracked,
+                                  const float* const* mean, const float* const* var,
+                                  int64_t block_stride, int32_t iters, int32_t B, int32_t P,
+                                  const double* weights, double decay, void* scratch, void* stream) {
+    if (layers < 1 || layers > dadmm::BN_MAX_LAYERS || !widths || !running_mean || !running_var || !mean ||
+        !var || !weights || !scratch || P < 2 || B < 0 || iters < 0)
+        return fail(DADMM_EINVAL, "bad BatchNorm running-statistics arguments");
+    if ((uintptr_t)scratch & 7) return fail(DADMM_EINVAL, "scratch must be 8-byte aligned");
+    if (B == 0 || iters == 0) return ok();
+    if ((int64_t)iters * B >= ((int64_t)1 << 31)) return fail(DADMM_EUNSUPPORTED, "too many rows");
+    dadmm::BnRunArgs a{};
+    a.layers = layers;
+    a.iters = iters;
+    a.B = B;
+    a.P = P;
+    a.col0[0] = 0;
+    for (int i = 0; i < layers; ++i) {
+        if (widths[i] < 1 || !running_mean[i] || !running_var[i] || !mean[i] || !var[i])
+            return fail(DADMM_EINVAL, "layer %d: bad width or NULL pointer", i);
+        if (block_stride < (int64_t)B * widths[i] && iters > 1)
+            return fail(DADMM_EINVAL, "block_stride shorter than one iteration's [B][width] block");
+        a.width[i] = widths[i];
+        a.col0[i + 1] = a.col0[i] + widths[i];
+        a.rmean[i] = running_mean[i];
+        a.rvar[i] = running_var[i];
+        a.tracked[i] = tracked ? tracked[i] : nullptr;
+        a.mean[i] = mean[i];
+        a.var[i] = var[i];
+    }
+    a.block_stride = block_stride;
+    a.w = weights;
+    a.decay = decay;
+    a.part = (double*)scratch;
+    a.splits = bn_running_splits(iters, B);
+    hipError_t e = dadmm::launch_bn_running(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "BatchNorm running-statistics launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 int dadmm_hyper_gcn_train_bwd(int32_t B, int32_t P, int32_t N, const float* dy, const float* m,
                               const float* mean, const float* var, const float* bn_weight,
                               float bn_eps, const float* ahat, int32_t ahat_per_sample, float slope,

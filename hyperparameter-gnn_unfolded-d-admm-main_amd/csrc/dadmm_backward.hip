@@ -60,7 +60,14 @@ __device__ __forceinline__ uint32_t fresh_s(uint32_t x) {
     return x;
 }
 
-constexpr int WAVES = 8;
+// Waves per workgroup: 8 (two per SIMD, 256 registers each) or 4 (one per SIMD, 512 registers:
+// twice the rows per wave, room to keep more of the five trajectory streams in flight). 4 with
+// the pipelined prefetch (PF 2) is the default: 1.22 vs 1.27-1.28 ms at H (profiles/r05/adjoint_variants_r05j.txt)
+#ifndef DADMM_BWD_WAVES
+#define DADMM_BWD_WAVES 4
+#endif
+constexpr int WAVES = DADMM_BWD_WAVES;
+static_assert(WAVES == 8 || WAVES == 4, "adjoint workgroup: 4 or 8 waves");
 // GEMM2's A^T operand through a per-wave LDS ring filled by LDS-DMA, as in the forward
 // (dadmm_fused.hip): BWD_QD quarter-chains of 1 KB per wave, BWD_QD - 1 in flight
 #ifndef DADMM_BWD_AT_DMA
@@ -75,6 +82,14 @@ constexpr int BWD_QD = 5;
 // two tiles' temporaries: 256 VGPRs + 231 spilled at H; this form: 13 spilled.
 #ifndef DADMM_BWD_ROT
 #define DADMM_BWD_ROT 1
+#endif
+// DADMM_BWD_PF=1 (4-wave form): all five streams of a tile (Y[k], Urec, gY, Y[k-1] or d0,
+// Grec) are loaded at the top of the tile, one memory round trip instead of four dependent ones.
+// DADMM_BWD_PF=2: software-pipelined — the streams of the NEXT tile (after a wave's last tile:
+// the first tile of iteration k - 1) are issued at the top of the current one, so the last
+// tile's prefetch lands under the GEMM phases
+#ifndef DADMM_BWD_PF
+#define DADMM_BWD_PF (DADMM_BWD_WAVES == 4 ? 2 : 0)
 #endif
 #if DADMM_BWD_ROT
 #define BWD_ROW(e, r) (r)
@@ -208,6 +223,32 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rAt, (lds_void*)(Qlds + (w * BWD_QD + q % BWD_QD) * 256), 16,
                                                  vAt + 64 * t, (uint32_t)(p * NP * MP * 4), 0, 0);
     };
+#if DADMM_BWD_PF == 2
+    // the five streams of (iteration kk, tile tt_) into one set of registers; every load is
+    // unconditional (branch-free: a load under a branch makes the compiler drain the queue)
+    f32x4 cy1[P], cu[P], cg[P], cyk[P], cgr[P];
+    // stream c of (iteration kk, tile tt_): 0 Y[kk], 1 Urec[kk], 2 gY[kk], 3 Y[kk-1] (d0 at kk = 0),
+    // 4 Grec[kk]
+    auto issue1 = [&](int c, int kk, int tt_, f32x4 (&dst)[P]) {
+        const float* base = c == 0 ? a.Y + (size_t)kk * S
+                          : c == 1 ? a.Urec + (size_t)kk * S
+                          : c == 2 ? a.gY + (size_t)kk * S
+                          : c == 3 ? (kk > 0 ? a.Y + (size_t)(kk - 1) * S : a.d0)
+                                   : a.Grec + (size_t)kk * S;
+        const rsrc_t rs = make_rsrc(base, state_bytes);
+        const int n0_ = (w * T2 + tt_) * 16 + 4 * h;
+        const uint32_t vr = n0_ < n ? (uint32_t)((s * P * n + n0_) * 4) : 0x80000000u;
+#pragma unroll
+        for (int p = 0; p < P; ++p) dst[p] = bload4(rs, vr, (uint32_t)(p * n * 4));
+    };
+    if (has_tiles) {
+        issue1(0, K - 1, 0, cy1);
+        issue1(1, K - 1, 0, cu);
+        issue1(2, K - 1, 0, cg);
+        issue1(3, K - 1, 0, cyk);
+        issue1(4, K - 1, 0, cgr);
+    }
+#endif
     __syncthreads();
 
     for (int k = K - 1; k >= 0; --k) {
@@ -242,11 +283,11 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
         // ---- elementwise adjoint of iteration k on this lane's rows ---------------------------
         if (has_tiles) {
             const rsrc_t ryk = make_rsrc(k > 0 ? a.Y + (size_t)(k - 1) * S : a.y0, state_bytes);
-            const rsrc_t ry1 = make_rsrc(a.Y + (size_t)k * S, state_bytes);
-            const rsrc_t rgr = make_rsrc(a.Grec + (size_t)k * S, state_bytes);
-            const rsrc_t ruk = make_rsrc(a.Urec + (size_t)k * S, state_bytes);
-            const rsrc_t rgy = make_rsrc(a.gY + (size_t)k * S, state_bytes);
-            const rsrc_t rd0 = make_rsrc(a.d0, state_bytes);
+            [[maybe_unused]] const rsrc_t ry1 = make_rsrc(a.Y + (size_t)k * S, state_bytes);
+            [[maybe_unused]] const rsrc_t rgr = make_rsrc(a.Grec + (size_t)k * S, state_bytes);
+            [[maybe_unused]] const rsrc_t ruk = make_rsrc(a.Urec + (size_t)k * S, state_bytes);
+            [[maybe_unused]] const rsrc_t rgy = make_rsrc(a.gY + (size_t)k * S, state_bytes);
+            [[maybe_unused]] const rsrc_t rd0 = make_rsrc(a.d0, state_bytes);
 #if DADMM_BWD_ROT
 #pragma unroll 1
 #else
@@ -260,25 +301,56 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                 const uint32_t vrow = ok ? (uint32_t)((s * P * n + n0) * 4) : 0x80000000u;
                 // live ranges kept short (register budget): [P][4] temporaries t1, t2
                 float t1[P][4], t2[P][4];
+#if DADMM_BWD_PF == 2
+                // this tile's streams were issued a tile (or the GEMM phases) ago; each stream of
+                // the next tile (after the last tile: iteration k - 1's first) is issued into the
+                // same registers right after this tile's last read of it
+                const bool last_t = tt + 1 == T2;
+                const int nk = last_t ? (k > 0 ? k - 1 : 0) : k, ntt = last_t ? 0 : tt + 1;
+#define py1 cy1
+#define pu cu
+#define pg cg
+#define pyk cyk
+#define pgr cgr
+#define BWD_LD(pre, rs) (pre[p])
+#define BWD_NEXT(c, arr) issue1(c, nk, ntt, arr)
+#elif DADMM_BWD_PF
+                f32x4 py1[P], pu[P], pg[P], pyk[P], pgr[P];
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const uint32_t so = (uint32_t)(p * n * 4);
+                    py1[p] = bload4(ry1, vrow, so);
+                    pu[p] = bload4(ruk, vrow, so);
+                    pg[p] = bload4(rgy, vrow, so);
+                    pyk[p] = k > 0 ? bload4(ryk, vrow, so) : bload4(rd0, vrow, so);
+                    pgr[p] = bload4(rgr, vrow, so);
+                }
+#define BWD_LD(pre, rs) (pre[p])
+#else
+#define BWD_LD(pre, rs) bload4(rs, vrow, (uint32_t)(p * n * 4))
+#endif
                 // t2 = delta_{k+1} formed from y_{k+1} exactly as the forward did
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
-                    const f32x4 v = bload4(ry1, vrow, (uint32_t)(p * n * 4));
+                    const f32x4 v = BWD_LD(py1, ry1);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) t1[p][r] = v[r];
                 }
+#if DADMM_BWD_PF == 2
+                BWD_NEXT(0, cy1);
+#endif
                 cons(t1, t2, mk);
                 const uint32_t md1 = clamp_delta(t2, a.variant);
                 fence();
                 // dual update adjoint (:98-99); t1 = d_bar
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
-                    const f32x4 vu = bload4(ruk, vrow, (uint32_t)(p * n * 4));
-                    const f32x4 vg = bload4(rgy, vrow, (uint32_t)(p * n * 4));
+                    const f32x4 vu = BWD_LD(pu, ruk);
+                    const f32x4 vg = BWD_LD(pg, rgy);
                     const f32x4 gprev = *(const f32x4*)(Glds + (p * BT + j) * YS + n0);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int e = 4 * tt + r;
+                        [[maybe_unused]] const int e = 4 * tt + r;
                         yb[p][BWD_ROW(e, r)] = yb[p][BWD_ROW(e, r)] + vg[r];  // + gY[k]
                         const float wv = vu[r] + t2[p][r] * et[p];
                         const float wb = inside(wv, -vclip, vclip) ? Ub[p][BWD_ROW(e, r)] : 0.0f;
@@ -288,6 +360,10 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                         Ub[p][BWD_ROW(e, r)] = wb;
                     }
                 }
+#if DADMM_BWD_PF == 2
+                BWD_NEXT(1, cu);
+                BWD_NEXT(2, cg);
+#endif
                 cons(t1, t2, mk);   // t2 = 2 L d_bar
 #pragma unroll
                 for (int p = 0; p < P; ++p)
@@ -295,6 +371,29 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                     for (int r = 0; r < 4; ++r) yb[p][BWD_ROW(4 * tt + r, r)] += t2[p][r];
                 fence();
                 // t1 = y_k; t2 = delta_k (k > 0: formed from y_k as the forward did; k = 0: d0)
+#if DADMM_BWD_PF
+                if (k > 0) {
+#pragma unroll
+                    for (int p = 0; p < P; ++p)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) t1[p][r] = pyk[p][r];
+                    cons(t1, t2, mk);
+                    clamp_delta(t2, a.variant);
+                } else {   // y_0 (the prefetch slot held d0)
+#pragma unroll
+                    for (int p = 0; p < P; ++p) {
+                        const f32x4 v = bload4(ryk, vrow, (uint32_t)(p * n * 4));
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            t1[p][r] = v[r];
+                            t2[p][r] = pyk[p][r];
+                        }
+                    }
+                }
+#if DADMM_BWD_PF == 2
+                BWD_NEXT(3, cyk);
+#endif
+#else
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
                     const f32x4 v = bload4(ryk, vrow, (uint32_t)(p * n * 4));
@@ -312,15 +411,16 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                         for (int r = 0; r < 4; ++r) t2[p][r] = v[r];
                     }
                 }
+#endif
                 fence();
                 // primal update + gradient clamp adjoint (:73-93)
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
-                    const f32x4 vgr = bload4(rgr, vrow, (uint32_t)(p * n * 4));
+                    const f32x4 vgr = BWD_LD(pgr, rgr);
                     f32x4 gbv;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int e = 4 * tt + r;
+                        [[maybe_unused]] const int e = 4 * tt + r;
                         const float yk = t1[p][r];
                         const float gr = vgr[r];
                         const float g = tclamp(gr, -gclip, gclip);
@@ -337,6 +437,15 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                     }
                     *(f32x4*)(Glds + (p * BT + j) * YS + n0) = gbv;
                 }
+#if DADMM_BWD_PF == 2
+                BWD_NEXT(4, cgr);
+#undef py1
+#undef pu
+#undef pg
+#undef pyk
+#undef pgr
+#undef BWD_NEXT
+#endif
 #if DADMM_BWD_ROT
                 // rotate: the next tile's carried state moves to rows 0..3 (T2 rotations: identity)
 #pragma unroll
@@ -479,12 +588,13 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 }
 
 template <int P, int NT, int GRAPH>
-__global__ __launch_bounds__(WAVES * 64) void backward_kernel(BackwardArgs a) {
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVES == 4 ? 1 : 2, WAVES == 4 ? 1 : 2)))
+void backward_kernel(BackwardArgs a) {
     constexpr int NP = NT * 64;
     __shared__ __attribute__((aligned(16))) float lds[P * BT * ((NP + 4) + (M_PAD + 4)) + WAVES * P * 4 +
                                                       (DADMM_BWD_AT_DMA ? WAVES * BWD_QD * 256 : 0)];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (w < 4)
+    if (WAVES == 4 || w < 4)
         body<P, NT, GRAPH, 0>(a, lds, w);
     else
         body<P, NT, GRAPH, 1>(a, lds, w);

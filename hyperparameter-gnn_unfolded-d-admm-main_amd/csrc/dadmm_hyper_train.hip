@@ -297,7 +297,116 @@ __global__ __launch_bounds__(THREADS) void head_act_kernel(int mode, int B, int 
     out[idx] = g * ((1.0f - s) * s);                   // sigmoid
 }
 
+// BatchNorm running statistics in closed form (dadmm_hyper_bn_running_update). Pass 1: workgroup
+// (64-column block of the concatenated layers, split s) — lane = column, wave = a quarter of the
+// split's rows — sums w[t] mean[t][c] and w[t] var[t][c] P / (P - 1) over its rows in float64
+// (coalesced along the columns); the 4 waves add in wave order (LDS). Pass 2: per column, the
+// splits in order, plus decay * the old value. Deterministic.
+// the layer of column block cb (64 columns; blocks never straddle layers) and its pointers,
+// selected with uniform branches (no dynamic indexing of the kernel-argument arrays)
+__device__ inline int bn_layer_of_block(const BnRunArgs& a, int cb, int* c0) {
+    int L = 0, first = 0;
+#pragma unroll
+    for (int i = 0; i < BN_MAX_LAYERS; ++i) {
+        if (i >= a.layers) break;
+        const int nb = (a.width[i] + 63) / 64;
+        if (cb < first + nb) {
+            L = i;
+            break;
+        }
+        first += nb;
+    }
+    *c0 = (cb - first) * 64;
+    return L;
+}
+
+template <class T, int S>
+__device__ inline T bn_pick(const T (&arr)[S], int L) {
+    T r = arr[0];
+#pragma unroll
+    for (int i = 1; i < S; ++i)
+        if (L == i) r = arr[i];
+    return r;
+}
+
+// partial weighted sums: block (cb, sp) covers 64 columns of one layer and rows t of split sp;
+// the 4 waves take interleaved quarters of the split and reduce through LDS (fixed order)
+__global__ __launch_bounds__(256) void bn_running_part_kernel(BnRunArgs a) {
+    __shared__ double red[4][2][64];
+    const int total = a.col0[a.layers];
+    const int sp = blockIdx.y;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int c0;
+    const int L = bn_layer_of_block(a, blockIdx.x, &c0);
+    const int N = bn_pick(a.width, L);
+    const float* __restrict__ mean = bn_pick(a.mean, L);
+    const float* __restrict__ var = bn_pick(a.var, L);
+    const int cc = c0 + lane;
+    const int T = a.iters * a.B;
+    const int per = (T + a.splits - 1) / a.splits;
+    const int t0 = sp * per, t1 = t0 + per < T ? t0 + per : T;
+    const double uf = (double)a.P / (double)(a.P - 1);
+    double sm = 0.0, sv = 0.0;
+    if (cc < N) {
+        int k = t0 / a.B, b = t0 - k * a.B + wv;
+        while (b >= a.B) { b -= a.B; ++k; }
+        for (int t = t0 + wv; t < t1; t += 4) {
+            const size_t o = (size_t)k * a.block_stride + (size_t)b * N + cc;
+            const double wt = a.w[t];
+            sm += wt * (double)mean[o];
+            sv += wt * ((double)var[o] * uf);
+            b += 4;
+            while (b >= a.B) { b -= a.B; ++k; }
+        }
+    }
+    red[wv][0][lane] = sm;
+    red[wv][1][lane] = sv;
+    __syncthreads();
+    if (wv == 0 && cc < N) {
+        double m = red[0][0][lane], v = red[0][1][lane];
+        for (int q = 1; q < 4; ++q) {
+            m += red[q][0][lane];
+            v += red[q][1][lane];
+        }
+        const int c = bn_pick(a.col0, L) + cc;
+        a.part[((size_t)sp * 2) * total + c] = m;
+        a.part[((size_t)sp * 2 + 1) * total + c] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void bn_running_finish_kernel(BnRunArgs a) {
+    const int total = a.col0[a.layers];
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= total) return;
+    int L = 0;
+#pragma unroll
+    for (int i = 1; i < BN_MAX_LAYERS; ++i)
+        if (i < a.layers && c >= a.col0[i]) L = i;
+    const int cc = c - bn_pick(a.col0, L);
+    double m = 0.0, v = 0.0;
+    for (int sp = 0; sp < a.splits; ++sp) {
+        m += a.part[((size_t)sp * 2) * total + c];
+        v += a.part[((size_t)sp * 2 + 1) * total + c];
+    }
+    float* rm = bn_pick(a.rmean, L);
+    float* rv = bn_pick(a.rvar, L);
+    rm[cc] = (float)(a.decay * (double)rm[cc] + m);
+    rv[cc] = (float)(a.decay * (double)rv[cc] + v);
+    int64_t* tr = bn_pick(a.tracked, L);
+    if (cc == 0 && tr != nullptr) tr[0] += (int64_t)a.iters * a.B;
+}
+
 }  // namespace hyper_train
+
+hipError_t launch_bn_running(const BnRunArgs& a, hipStream_t st) {
+    const int total = a.col0[a.layers];
+    if (total == 0) return hipSuccess;
+    int blocks = 0;
+    for (int i = 0; i < a.layers; ++i) blocks += (a.width[i] + 63) / 64;
+    hipLaunchKernelGGL(hyper_train::bn_running_part_kernel, dim3(blocks, a.splits), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(hyper_train::bn_running_finish_kernel, dim3((total + 255) / 256), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
 
 template <int NT, int PR>
 static hipError_t launch_gcn_bwd_nt(const GcnBwdArgs& a, int grid, size_t lds, hipStream_t st) {

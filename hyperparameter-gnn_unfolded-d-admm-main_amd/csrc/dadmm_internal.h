@@ -311,6 +311,26 @@ struct GcnBwdArgs {
     int bn_eval;            // BatchNorm on constant (running) statistics: no batch-statistics terms
 };
 hipError_t launch_gcn_bwd(const GcnBwdArgs& a, hipStream_t st);
+
+// BatchNorm running statistics after T = iters * B sequential train-mode calls, closed form
+// (dadmm_hyper_bn_running_update): up to BN_MAX_LAYERS layers in one pair of launches
+constexpr int BN_MAX_LAYERS = 8;
+struct BnRunArgs {
+    int layers, iters, B, P;
+    int width[BN_MAX_LAYERS];
+    int col0[BN_MAX_LAYERS + 1];          // prefix sums of width (column offsets in the partials)
+    float* rmean[BN_MAX_LAYERS];
+    float* rvar[BN_MAX_LAYERS];
+    int64_t* tracked[BN_MAX_LAYERS];      // num_batches_tracked (nullable)
+    const float* mean[BN_MAX_LAYERS];     // [iters blocks][B][width] at block_stride floats
+    const float* var[BN_MAX_LAYERS];
+    int64_t block_stride;
+    const double* w;                      // [T] momentum (1 - momentum)^(T - 1 - t)
+    double decay;                         // (1 - momentum)^T
+    double* part;                         // [splits][2][col0[layers]] float64 partial sums
+    int splits;
+};
+hipError_t launch_bn_running(const BnRunArgs& a, hipStream_t st);
 // hyper-parameter head: mode 0: hyp = head(z); mode 1: dz = dhyp * head'(z); z, hyp, dhyp [B][4H]
 hipError_t launch_head_act(int mode, int B, int H, const float* z, const float* dhyp, const float* maxv4,
                            float* out, hipStream_t st);

@@ -201,7 +201,8 @@ class GnnTrainFn(torch.autograd.Function):
                 Ds.append(D)
         run.finish()
         if plan.train:   # eval mode (a backward through model.eval()): running statistics are inputs
-            hyper_ops.queue_running_stats(model, plan.stats(arena, K), run.P, defer=False)
+            with torch.cuda.device(dev):
+                plan.update_running_stats(arena, K, hyper_ops._stream(dev))
         ctx.run, ctx.model, ctx.plan, ctx.a_hat, ctx.per_sample, ctx.seeds = run, model, plan, a_hat, per_sample, seeds
         ctx.arena, ctx.svs, ctx.As, ctx.Us, ctx.Ds = arena, svs, As, Us, Ds
         ctx.params = params

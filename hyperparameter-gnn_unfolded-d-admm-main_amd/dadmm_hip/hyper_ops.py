@@ -570,6 +570,7 @@ class NativeHyperPlan:
         self.work = torch.empty(nbytes // 4 + 4, device=dev)
         self.dAtAy = None
         self.wscratch = None
+        self.bn_scratch = None
         self.dsave_per = L.dadmm_hyper_train_dsave_floats(ctypes.byref(net), B)   # floats, multiple of 4
 
     @staticmethod
@@ -608,6 +609,34 @@ class NativeHyperPlan:
             var = blocks[:, self.offs[15 + i]:self.offs[15 + i] + n].view(iters, self.B, self.W[i])
             out.append((bn, mean, var))
         return out
+
+    def update_running_stats(self, arena, iters, stream):
+        """The GCN blocks' BatchNorm running statistics after the training-mode calls of ``iters``
+        blocks of ``arena`` (iters * B per-sample calls in order): _update_running_stats's closed
+        form in one dadmm_hyper_bn_running_update (two launches for all five layers, in place of
+        ~16 torch launches per layer). Falls back to the torch form when the layers' momenta differ
+        or one is None (cumulative averaging)."""
+        moms = {bn.momentum for bn in self.bns}
+        if len(moms) != 1 or None in moms or any(bn.num_batches_tracked is None for bn in self.bns):
+            queue_running_stats(None, self.stats(arena, iters), self.P, False)
+            return
+        m = moms.pop()
+        T = iters * self.B
+        nl = len(self.bns)
+        widths = (ctypes.c_int32 * nl)(*self.W[:nl])
+        vp = ctypes.c_void_p * nl
+        base = arena.data_ptr()
+        nbytes = self.L.dadmm_hyper_bn_running_scratch_bytes(nl, widths, iters, self.B)
+        if self.bn_scratch is None or 4 * self.bn_scratch.numel() < nbytes:
+            self.bn_scratch = torch.empty((nbytes + 3) // 4, device=self.dev)
+        _lib.check("dadmm_hyper_bn_running_update", self.L.dadmm_hyper_bn_running_update(
+            nl, widths, vp(*[bn.running_mean.data_ptr() for bn in self.bns]),
+            vp(*[bn.running_var.data_ptr() for bn in self.bns]),
+            vp(*[bn.num_batches_tracked.data_ptr() for bn in self.bns]),
+            vp(*[base + 4 * self.offs[10 + i] for i in range(nl)]),
+            vp(*[base + 4 * self.offs[15 + i] for i in range(nl)]),
+            self.per, iters, self.B, self.P, _ptr(_rs_weights(T, m, self.dev)), (1.0 - m) ** T,
+            _ptr(self.bn_scratch), stream))
 
     def forward(self, AtAy, Atb, ahat, per_sample, seed, sv, stream):
         _lib.check("dadmm_hyper_train_forward", self.L.dadmm_hyper_train_forward(
@@ -660,8 +689,11 @@ def _native_forward(ctx, L, AtAy, Atb, ahat, model, n, per_sample, seed, defer):
     sv = plan.saved(arena)
     with torch.cuda.device(dev):
         plan.forward(AtAy, Atb, ahat, per_sample, seed, sv, _stream(dev))
-    if plan.train:   # eval mode: the running statistics were inputs
+    if plan.train and defer:   # eval mode: the running statistics were inputs
         queue_running_stats(model, plan.stats(arena, 1), P, defer)
+    elif plan.train:
+        with torch.cuda.device(dev):
+            plan.update_running_stats(arena, 1, _stream(dev))
     ctx.model, ctx.n, ctx.per_sample, ctx.seed = model, n, per_sample, seed
     ctx.arena, ctx.sv, ctx.plan = arena, sv, plan
     ctx.AtAy, ctx.Atb, ctx.ahat = AtAy, Atb, ahat

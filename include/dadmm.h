@@ -455,6 +455,23 @@ int dadmm_hyper_rownorm_bwd(int32_t rows, int32_t C, const float* dy, const floa
 int dadmm_hyper_head_act(int32_t mode, int32_t B, int32_t H, const float* z, const float* dhyp,
                          float alpha_max, float tau_max, float rho_max, float eta_max, float* out,
                          void* stream);
+/* dadmm_hyper_bn_running_update (ABI 17): the BatchNorm1d running statistics of `layers` (<= 8)
+ * layers after T = iters * B sequential train-mode calls over P nodes each (the reference calls
+ * bn_i once per sample, gnn_dlasso_models_progressive.py:52-68), in closed form and float64:
+ *   r <- decay r + sum_t weights[t] s_t   (decay = (1 - m)^T, weights[t] = m (1 - m)^(T - 1 - t)),
+ * s_t the sample's batch mean, resp. its biased variance times P / (P - 1); one pass of partial
+ * sums and one finishing pass for every layer (it replaces ~16 torch launches per layer).
+ * widths / running_mean / running_var / tracked / mean / var are HOST arrays of `layers` entries
+ * (the latter five device pointers; tracked nullable: num_batches_tracked += T). mean[i] / var[i]:
+ * [iters][B][widths[i]] with block_stride floats between iterations. scratch: at least
+ * dadmm_hyper_bn_running_scratch_bytes bytes (8-byte aligned). */
+size_t dadmm_hyper_bn_running_scratch_bytes(int32_t layers, const int32_t* widths, int32_t iters,
+                                            int32_t B);
+int dadmm_hyper_bn_running_update(int32_t layers, const int32_t* widths, float* const* running_mean,
+                                  float* const* running_var, int64_t* const* tracked,
+                                  const float* const* mean, const float* const* var,
+                                  int64_t block_stride, int32_t iters, int32_t B, int32_t P,
+                                  const double* weights, double decay, void* scratch, void* stream);
 
 /* ---- GNN hypernetwork training: parameter gradients on hand-written kernels ------------------
  * Replace the weight / bias gradients torch's autograd computes through hipBLASLt and its sums

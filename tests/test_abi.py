@@ -249,3 +249,25 @@ def test_hyper_train_wgrad_rejects_bad_strides(L):
     assert call(atay - 1, 100, dfl) == -1            # shorter than one AtAy block
     assert call(atay, 0, dfl) == -1                  # every iteration on the same saved block
     assert call(atay, 100, dfl - 4) == -1            # shorter than one dsave block
+
+
+def test_bn_running_update_validation(L):
+    """dadmm_hyper_bn_running_update checks its layer table before launching; empty work is ok."""
+    W = (ctypes.c_int32 * 2)(32, 48)
+    vp = ctypes.c_void_p * 2
+    ptrs = lambda o: vp(*[0x10000 + 256 * (o + i) for i in range(2)])   # noqa: E731
+    assert L.dadmm_hyper_bn_running_scratch_bytes(2, W, 1, 32) == 8 * 2 * 80 * 1        # one split
+    assert L.dadmm_hyper_bn_running_scratch_bytes(2, W, 25, 256) == 8 * 2 * 80 * 100    # 64 rows each
+    assert L.dadmm_hyper_bn_running_scratch_bytes(2, W, 25, 4096) == 8 * 2 * 80 * 256   # capped
+    assert L.dadmm_hyper_bn_running_scratch_bytes(9, W, 1, 1) == 0
+
+    def call(layers=2, widths=W, block=32 * 256 + 48 * 256, iters=25, B=256, P=5, scratch=_fk(9), rm=None):
+        return L.dadmm_hyper_bn_running_update(layers, widths, rm or ptrs(0), ptrs(2), None, ptrs(4), ptrs(6),
+                                               block, iters, B, P, _fk(8), 0.5, scratch, None)
+    assert call(layers=0) == -1
+    assert call(P=1) == -1                                   # unbiased variance needs P >= 2
+    assert call(scratch=None) == -1
+    assert call(block=48 * 256 - 1) == -1                    # an iteration block shorter than [B][width]
+    assert call(rm=vp(0x10000, 0)) == -1                     # a NULL running_mean
+    assert call(widths=(ctypes.c_int32 * 2)(32, 0)) == -1
+    assert call(B=0) == 0 and call(iters=0) == 0
