@@ -1022,6 +1022,41 @@ int dadmm_hyper_gcn_train_bwd(int32_t B, int32_t P, int32_t N, const float* dy, 
     return ok();
 }
 
+int dadmm_hyper_linear_gcn_bwd(int32_t B, int32_t P, int32_t K, int32_t N, const float* x, int32_t ldx,
+                               const float* W, const float* m, const float* mean, const float* var,
+                               const float* bn_weight, float bn_eps, const float* ahat, int32_t ahat_per_sample,
+                               float slope, float drop_p, uint64_t seed, int32_t site, float* dz, float* part,
+                               int32_t bn_eval, void* stream) {
+    if (B < 0 || P < 2 || P > 64 || N < 1) return fail(DADMM_EINVAL, "bad gcn dims B=%d P=%d N=%d", B, P, N);
+    dadmm::HyperArgs a;
+    int rc = hyper_input(B * P, K, N, x, ldx, K, nullptr, 0, W, dz, N, &a);
+    if (rc) return rc;
+    if (!m || !mean || !var || !bn_weight || !ahat || !part) return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if ((N & 3) || !aligned16(dz)) return fail(DADMM_EUNSUPPORTED, "N %% 4 == 0 and a 16-byte aligned dz required");
+    if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(DADMM_EINVAL, "dropout p=%g not in [0, 1)", drop_p);
+    if ((int64_t)B * P * (K > N ? K : N) >= ((int64_t)1 << 31))
+        return fail(DADMM_EUNSUPPORTED, "operand larger than 2^31 floats");
+    a.B = B;
+    a.P = P;
+    a.splits = 1;
+    a.ahat = ahat;
+    a.ahat_per_sample = ahat_per_sample ? 1 : 0;
+    a.save_m = const_cast<float*>(m);
+    a.save_mean = const_cast<float*>(mean);
+    a.save_var = const_cast<float*>(var);
+    a.bn_w = bn_weight;
+    a.bn_eps = bn_eps;
+    a.slope = slope;
+    a.drop_p = drop_p;
+    a.seed = seed;
+    a.site = site;
+    a.part = part;
+    a.bn_eval = bn_eval ? 1 : 0;
+    hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_GCN_BWD, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "linear + gcn backward launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 int dadmm_hyper_linear_ln_train(int32_t rows, int32_t K, int32_t N, const float* x, int32_t ldx,
                                 const float* W, const float* bias, const float* ln_weight,
                                 const float* ln_bias, float eps, int32_t act, float slope, float drop_p,

@@ -132,7 +132,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
     const int tl = xcd_tile(blockIdx.x, gridDim.x);
     const int ct = tl % gn, rt = (tl / gn) % gm, split = tl / (gn * gm);
 
-    constexpr bool GCN = EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN;
+    constexpr bool GCN = EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN || EPI == HYPER_EPI_GCN_BWD;
     int row0, rows_t, s0 = 0;
     if (GCN) {
         s0 = rt * a.S_t;
@@ -427,6 +427,74 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
                     if (4 * g + e < P) emit(sl * P + 4 * g + e, c, v[e]);
             }
         };
+        if constexpr (EPI == HYPER_EPI_GCN_BWD) {
+            // the GCN block backward of the layer whose output gradient dy this GEMM produced (the
+            // tile holds whole samples and 64 of its columns: everything gcn_bwd_kernel reads per
+            // (sample, column)); the same operations in the same order as gcn_bwd_kernel's loop
+            // form, so dz and the partial sums are bit-identical to the unfused pair of launches
+            __syncthreads();
+            const uint32_t thr = drop_threshold(a.drop_p);
+            const float scale = a.drop_p > 0.0f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+            const float inv = 1.0f / (float)P;
+            for (int task = threadIdx.x; task < ns * TN; task += THREADS) {
+                const int sl = task / TN, c = task - sl * TN;
+                if (c >= cols) continue;
+                const int col = col0 + c, s = s0 + sl;
+                const size_t rs = (size_t)row0 + (size_t)sl * P;
+                const float mean = a.save_mean[(size_t)s * a.N + col];
+                const float rstd = 1.0f / sqrtf(a.save_var[(size_t)s * a.N + col] + a.bn_eps);
+                const float gam = a.bn_w[col];
+                float* dc = zt + sl * P * ZS + c;
+                float sb = 0.0f, sg = 0.0f, sbias = 0.0f;
+                for (int p = 0; p < P; ++p) {   // dxn = dropout'(dy), the two BatchNorm sums
+                    const float mv = a.save_m[(rs + p) * a.N + col];
+                    const float t = mv > 0.0f ? mv : mv * a.slope;
+                    const float xh = (t - mean) * rstd;
+                    float g = dc[p * ZS];
+                    if (a.drop_p > 0.0f)
+                        g = drop_hash(a.seed, a.site, (uint32_t)(rs + p), (uint32_t)col) >= thr ? g * scale : 0.0f;
+                    sb += g;
+                    sg += g * xh;
+                    dc[p * ZS] = g;
+                }
+                for (int p = 0; p < P; ++p) {   // BatchNorm and leaky_relu backward -> dM
+                    const float mv = a.save_m[(rs + p) * a.N + col];
+                    const float t = mv > 0.0f ? mv : mv * a.slope;
+                    const float xh = (t - mean) * rstd;
+                    const float g = dc[p * ZS];
+                    const float dt = a.bn_eval ? gam * rstd * g : gam * rstd * (g - sb * inv - xh * (sg * inv));
+                    const float d = mv > 0.0f ? dt : dt * a.slope;
+                    sbias += d;
+                    dc[p * ZS] = d;
+                }
+                a.part[(size_t)s * a.N + col] = sg;                       // dgamma
+                a.part[((size_t)a.B + s) * a.N + col] = sb;               // dbeta
+                a.part[((size_t)2 * a.B + s) * a.N + col] = sbias;        // dbias (GCNConv.bias)
+            }
+            __syncthreads();
+            // dZ[q] = sum_p A_hat[p][q] dM[p] (the mix, transposed), 4 columns per task
+            for (int task = threadIdx.x; task < rows_t * (TN / 4); task += THREADS) {
+                const int r = task / (TN / 4), c = 4 * (task - r * (TN / 4));
+                if (c >= cols) continue;
+                const int sl = r / P, q = r - sl * P;
+                const float* ah = ahs + sl * P * P;
+                const float* dm = zt + sl * P * ZS + c;
+                f32x4 acc4 = zero;
+                for (int p = 0; p < P; ++p) {
+                    const f32x4 d4 = *(const f32x4*)(dm + p * ZS);
+                    const float w = ah[p * P + q];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc4[e] += w * d4[e];
+                }
+                float* dst = a.y + (size_t)(row0 + r) * a.ldy + col0 + c;
+                if (c + 4 <= cols) {
+                    *(f32x4*)dst = acc4;
+                } else {
+                    for (int e = 0; e < cols - c; ++e) dst[e] = acc4[e];
+                }
+            }
+            return;
+        }
         if constexpr (EPI == HYPER_EPI_GCN_TRAIN) {
             // training: BatchNorm on each sample's own statistics over its P nodes, then Dropout
             //   pass 1: M = A_hat Z + bias (LDS mt, and saved for the backward)
@@ -951,7 +1019,7 @@ __global__ __launch_bounds__(THREADS) void rownorm_kernel(RowNormArgs a) {
 template <int WR, int EPI, bool SPLIT, bool DMA>
 hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
     size_t lds = DMA ? 4 * (size_t)DADMM_HYPER_DQ * (2 * WR + 4) * 256 : 0;   // the ring
-    if (EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN) {   // the epilogue (reuses the ring)
+    if (EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN || EPI == HYPER_EPI_GCN_BWD) {   // the epilogue (reuses the ring)
         size_t e = 4 * ((size_t)32 * WR * ZS + (((size_t)a.S_t * a.P * a.P + 3) & ~(size_t)3) + 4 * TN);
         if (EPI == HYPER_EPI_GCN_TRAIN) e += 4 * ((size_t)32 * WR * ZS + 2 * (size_t)a.S_t * TN);
         lds = e > lds ? e : lds;
@@ -968,7 +1036,7 @@ hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
 
 template <int EPI, bool SPLIT>
 hipError_t launch_wr(int wr, bool dma, int grid, const HyperArgs& a, hipStream_t st) {
-    constexpr bool GCN = EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN;
+    constexpr bool GCN = EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN || EPI == HYPER_EPI_GCN_BWD;
     switch (wr) {
         case 1: return launch_one<1, EPI, SPLIT, false>(grid, a, st);
         case 2: return dma ? launch_one<2, EPI, SPLIT, true>(grid, a, st) : launch_one<2, EPI, SPLIT, false>(grid, a, st);
@@ -998,7 +1066,7 @@ hipError_t launch_epi(int wr, int grid, const HyperArgs& a, hipStream_t st) {
 // Row tiling: the largest tile (32 WR rows; whole samples of P rows for the GCN epilogue) that
 // still gives ~two workgroups per CU; smaller tiles for small batches.
 static int pick_tiles(HyperArgs& a, int epi) {
-    const bool gcn = epi == HYPER_EPI_GCN || epi == HYPER_EPI_GCN_TRAIN;
+    const bool gcn = epi == HYPER_EPI_GCN || epi == HYPER_EPI_GCN_TRAIN || epi == HYPER_EPI_GCN_BWD;
     const int unit = gcn ? a.P : 1;                             // rows per tiling unit
     const int units = gcn ? a.B : a.rows;
     a.gn = (a.N + hyper::TN - 1) / hyper::TN;
@@ -1089,7 +1157,7 @@ static bool try_gcn32(HyperArgs& a, hipStream_t st, hipError_t& err) {
 }
 
 hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st) {
-    const int units = (epi == HYPER_EPI_GCN || epi == HYPER_EPI_GCN_TRAIN) ? a.B : a.rows;
+    const int units = (epi == HYPER_EPI_GCN || epi == HYPER_EPI_GCN_TRAIN || epi == HYPER_EPI_GCN_BWD) ? a.B : a.rows;
     if (units <= 0 || a.N <= 0) return hipSuccess;
     if (a.K1 < a.K && (a.K1 & 15)) return hipErrorInvalidValue;
     hipError_t gerr = hipSuccess;
@@ -1110,6 +1178,7 @@ hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st) {
         case HYPER_EPI_GCN: return hyper::launch_epi<HYPER_EPI_GCN>(wr, grid, a, st);
         case HYPER_EPI_HEAD: return hyper::launch_epi<HYPER_EPI_HEAD>(wr, grid, a, st);
         case HYPER_EPI_GCN_TRAIN: return hyper::launch_epi<HYPER_EPI_GCN_TRAIN>(wr, grid, a, st);
+        case HYPER_EPI_GCN_BWD: return hyper::launch_epi<HYPER_EPI_GCN_BWD>(wr, grid, a, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -15,6 +15,7 @@
 // nothing here allocates or synchronises.
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/dadmm.h"
@@ -131,6 +132,13 @@ size_t dsave_layout(const dadmm_hyper_net* net, int B, DSave* d, float* base) {
         take(&d->pgcn[i], (size_t)3 * B * net->width[i]);
     }
     return off;
+}
+
+// DADMM_GCNBWD_FUSE=0 in the environment: the unfused pair (linear, then gcn backward) for A/B
+// timing and the bit-identity test
+bool gcn_bwd_fused() {
+    const char* e = getenv("DADMM_GCNBWD_FUSE");
+    return !(e != nullptr && e[0] == '0');
 }
 
 #define TRY(call)                       \
@@ -254,22 +262,40 @@ static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* At
         }
         dx = nx;
     }
-    // GCN layers, last to first: dZ (gcn backward), [dgamma, dbeta, dbias], dW, dX
+    // GCN layers, last to first: dZ (gcn backward), [dgamma, dbeta, dbias], dW, dX. Layer 5's
+    // gcn backward is its own launch (its dy comes from the LayerNorm backward); layers 4 .. 1 run
+    // theirs in the epilogue of the input-gradient GEMM of the layer above
+    // (dadmm_hyper_linear_gcn_bwd: no dy round trip, one launch instead of two)
+    const bool fuse = gcn_bwd_fused();
+    float* dZ = nullptr;   // this layer's dZ once formed
     for (int i = 4; i >= 0; --i) {
         const int N = net->width[i];
-        float* dZ = defer ? d.dZ[i] : (dx == w.dx[0] ? w.dx[1] : w.dx[0]);
         float* part = defer ? d.pgcn[i] : w.part;
-        TRY(dadmm_hyper_gcn_train_bwd(B, P, N, dx, sv->m[i], sv->mean[i], sv->var[i], net->bn_w[i],
-                                      net->bn_eps[i], ahat, ahat_per_sample, LEAKY, i < 4 ? net->drop_enc : 0.0f,
-                                      seed, i, dZ, part, net->bn_eval, stream));
+        if (dZ == nullptr) {
+            dZ = defer ? d.dZ[i] : (dx == w.dx[0] ? w.dx[1] : w.dx[0]);
+            TRY(dadmm_hyper_gcn_train_bwd(B, P, N, dx, sv->m[i], sv->mean[i], sv->var[i], net->bn_w[i],
+                                          net->bn_eps[i], ahat, ahat_per_sample, LEAKY,
+                                          i < 4 ? net->drop_enc : 0.0f, seed, i, dZ, part, net->bn_eval, stream));
+        }
         if (!defer) TRY(dadmm_hyper_colsum(part, 3, B, N, g->bn_wbc[i], 1, stream));
         if (i > 0) {
             const int Kin = net->width[i - 1];
             if (!defer)
                 TRY(dadmm_hyper_wgrad(rows, N, Kin, dZ, N, sv->y[i - 1], Kin, Kin, nullptr, 0, g->conv_w[i],
                                       nullptr, 1, w.wscr, stream));
-            // dX into the buffer dx held (gcn backward consumed it)
-            TRY(dadmm_hyper_linear(rows, N, Kin, dZ, N, N, nullptr, 0, g->conv_wt[i], nullptr, dx, Kin, stream));
+            if (fuse) {
+                // layer i - 1's dZ straight from this layer's dZ (not the buffer holding it)
+                float* nz = defer ? d.dZ[i - 1] : (dZ == w.dx[0] ? w.dx[1] : w.dx[0]);
+                TRY(dadmm_hyper_linear_gcn_bwd(B, P, N, Kin, dZ, N, g->conv_wt[i], sv->m[i - 1], sv->mean[i - 1],
+                                               sv->var[i - 1], net->bn_w[i - 1], net->bn_eps[i - 1], ahat,
+                                               ahat_per_sample, LEAKY, net->drop_enc, seed, i - 1, nz,
+                                               defer ? d.pgcn[i - 1] : w.part, net->bn_eval, stream));
+                dZ = nz;
+            } else {
+                // dX into the buffer dx held (gcn backward consumed it)
+                TRY(dadmm_hyper_linear(rows, N, Kin, dZ, N, N, nullptr, 0, g->conv_wt[i], nullptr, dx, Kin, stream));
+                dZ = nullptr;
+            }
         } else {
             // layer 1's input cat(AtAy, Atb); only d AtAy (its first n columns) flows back
             if (!defer)

@@ -206,6 +206,8 @@ hipError_t launch_loss_grad(const LossArgs& a, const float* gout, float* dY, hip
 #define HYPER_EPI_HEAD 2   // y = min(clamp(sigmoid(x W^T + bias), 1e-4, 0.9999) * max_c, ...)
 #define HYPER_EPI_GCN_TRAIN 3   // y = Dropout(BN_batch(leaky(A_hat (x W^T) + bias))) per sample,
                                 //     saving M = A_hat (x W^T) + bias and the samples' BN statistics
+#define HYPER_EPI_GCN_BWD 4     // y = gcn_bwd(x W^T): the GCN block backward (dadmm_hyper_train.hip's
+                                //     gcn_bwd_kernel) in the epilogue of the input-gradient GEMM
 struct HyperArgs {
     const float* x1;        // input columns [0, K1): row r at x1 + r * ld1
     const float* x2;        // input columns [K1, K): row r at x2 + r * ld2 (nullable if K1 == K)
@@ -240,6 +242,10 @@ struct HyperArgs {
     // (nullable); raw != 0: y = A_hat (x W^T) (+ addend), no bias / leaky_relu / BatchNorm
     const float* addend;
     int ld_add, raw;
+    // GCN_BWD: save_m / save_mean / save_var are the block's saved activations (read), bn_w its
+    // gamma; part [3][B][N] the per-sample dgamma / dbeta / dbias sums; bn_eval: running statistics
+    float* part;
+    int bn_eval;
 };
 
 // Counter-based dropout mask shared by the training forward and backward kernels (the backward

@@ -60,6 +60,7 @@ EXPORTED_SYMBOLS = (
     "dadmm_hyper_train_backward_deferred",
     "dadmm_hyper_train_wgrad",
     "dadmm_hyper_train_wgrad_scratch_bytes",
+    "dadmm_hyper_linear_gcn_bwd",
     "dadmm_hyper_bn_running_scratch_bytes",
     "dadmm_hyper_bn_running_update",
     "dadmm_gnn_flag_bytes",
@@ -251,6 +252,10 @@ def load() -> ctypes.CDLL:
     L.dadmm_hyper_train_backward_deferred.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, vp, i32, u64,
                                                       ctypes.POINTER(HyperSaved), vp, ctypes.POINTER(HyperGrads),
                                                       vp, vp, vp, i32, vp]
+    L.dadmm_hyper_linear_gcn_bwd.restype = ctypes.c_int
+    L.dadmm_hyper_linear_gcn_bwd.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, ctypes.c_float, vp,
+                                             i32, ctypes.c_float, ctypes.c_float, ctypes.c_uint64, i32, vp, vp,
+                                             i32, vp]
     L.dadmm_hyper_bn_running_scratch_bytes.restype = ctypes.c_size_t
     L.dadmm_hyper_bn_running_scratch_bytes.argtypes = [i32, vp, i32, i32]
     L.dadmm_hyper_bn_running_update.restype = ctypes.c_int

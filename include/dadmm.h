@@ -403,6 +403,19 @@ int dadmm_hyper_linear_ln(int32_t rows, int32_t K, int32_t N, const float* x, in
                           const float* ln_bias, float eps, int32_t act, float slope, float* y,
                           void* scratch, void* stream);
 
+/* dadmm_hyper_linear_gcn_bwd (ABI 17): dadmm_hyper_gcn_train_bwd(dy = x W^T) in ONE launch — the
+ * input-gradient GEMM of GCN layer i + 1 (x = its dZ [B P][K], W = its weight transposed, [N][K])
+ * with layer i's GCN block backward (leaky_relu, per-sample BatchNorm, Dropout, the A_hat mix) in
+ * the epilogue: the GEMM's row tiles hold whole samples, so dy never goes to memory. dz, part and
+ * every argument after W mean what they mean for dadmm_hyper_gcn_train_bwd; results are
+ * bit-identical to dadmm_hyper_linear + dadmm_hyper_gcn_train_bwd. N % 4 == 0, dz 16-byte aligned.
+ * Replaces the pair that follows each of gnn_dlasso_models_progressive.py:52-68's conv_{i+1}
+ * blocks in torch's backward. */
+int dadmm_hyper_linear_gcn_bwd(int32_t B, int32_t P, int32_t K, int32_t N, const float* x, int32_t ldx,
+                               const float* W, const float* m, const float* mean, const float* var,
+                               const float* bn_weight, float bn_eps, const float* ahat, int32_t ahat_per_sample,
+                               float slope, float drop_p, uint64_t seed, int32_t site, float* dz, float* part,
+                               int32_t bn_eval, void* stream);
 /* ---- GNN hypernetwork, training mode ---------------------------------------------------------
  * The same hypernetwork with model.train() semantics (gnn_dlasso_models_progressive.py:52-72:
  * Dropout(0.1) active, BatchNorm1d on each sample's own batch statistics over its P nodes) and the

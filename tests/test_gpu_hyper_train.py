@@ -545,3 +545,48 @@ def test_model_eval_autograd_and_odd_n_use_hip(cuda):
     Y, _ = model(bt, graphs)
     Y.sum().backward()
     assert model.last_backend == "hip-train"
+
+
+@pytest.mark.parametrize("P,n,hidden,B,per_sample", [(5, 64, 16, 40, False), (7, 32, 12, 33, True)])
+def test_fused_gcn_backward_bit_identical(cuda, monkeypatch, P, n, hidden, B, per_sample):
+    """dadmm_hyper_linear_gcn_bwd — GCN layers 4..1's block backward in the epilogue of the layer
+    above's input-gradient GEMM — against the unfused pair (DADMM_GCNBWD_FUSE=0: linear, then
+    dadmm_hyper_gcn_train_bwd): with dropout on, d AtAy and every parameter gradient are
+    bit-identical, through the per-call HyperTrainFn (immediate weight gradients) and through the
+    whole-forward node (deferred weight gradients)."""
+    import copy
+
+    import gnn_dlasso_models_progressive as G
+    import gnn_dlasso_utils as U
+    from dadmm_hip import hyper_ops
+    from dadmm_hip.graph import ingest
+    model0, _, b = _model(cuda, P, n, hidden, "diff", seed=3, B=B)
+    graphs = ([O.connected_er_graph(P, 0.5, seed=70 + s) for s in range(B)] if per_sample
+              else [O.connected_er_graph(P, 0.5, seed=4)] * B)
+    gb = ingest(graphs, P, B, cuda)
+    ahat = G.normalized_adjacency(gb.nbr, P)
+    ahat = (ahat[None] if gb.shared else ahat).contiguous()
+    g = torch.Generator(device=cuda).manual_seed(9)
+    AtAy0 = torch.randn(B, P, n, device=cuda, generator=g)
+    Atb = torch.randn(B, P, n, device=cuda, generator=g)
+    R = None
+    bt = torch.from_numpy(b[:B]).to(cuda)[..., None]
+    label = torch.randn(B, n, 1, device=cuda, generator=g)
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("DADMM_GCNBWD_FUSE", fuse)
+        model = copy.deepcopy(model0)
+        AtAy = AtAy0.clone().requires_grad_(True)
+        hyp = hyper_ops.hypernetwork_train(model, AtAy, Atb, n, ahat, per_sample, seed=0xABCDEF)
+        if R is None:
+            R = torch.randn(hyp.shape, device=cuda, generator=g)
+        (hyp * R).sum().backward()
+        per_call = [AtAy.grad.clone()] + [p.grad.clone() for p in model.parameters()]
+        model = copy.deepcopy(model0)
+        torch.manual_seed(5)
+        Y, h = model(bt, graphs, 3)
+        assert model.last_backend == "hip-train", model.last_backend
+        (U.compute_loss(Y, label)[1] + 0.1 * sum(x.sum() for x in h)).backward()
+        out[fuse] = (per_call, [p.grad.clone() for p in model.parameters()])
+    for got, want in zip(out["1"][0] + out["1"][1], out["0"][0] + out["0"][1]):
+        assert torch.equal(got, want), (got - want).abs().max()
