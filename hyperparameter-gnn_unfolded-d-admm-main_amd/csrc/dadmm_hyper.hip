@@ -233,6 +233,29 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
         for (int u = 0; u < D; ++u)
             if (t0 + u < te) mma(ar[u], br[u]);
     };
+    // GCN_BWD: the block's saved M tile [rows][64] and its samples' BatchNorm statistics go
+    // HBM -> LDS (LDS-DMA) now, under the GEMM, into a region past the ring and the epilogue tile
+    // (the epilogue then never waits on memory; its loads were the fused kernel's critical path)
+    [[maybe_unused]] float* pf = nullptr;
+    [[maybe_unused]] const int SR = (a.S_t + 3) & ~3;
+    if constexpr (EPI == HYPER_EPI_GCN_BWD) {
+        constexpr int RING = DMA ? DADMM_HYPER_DQ * (2 * WR + 4) * 256 : 0;   // floats
+        const int epi = TM * ZS + ((a.S_t * a.P * a.P + 3) & ~3) + 4 * TN;
+        pf = zt + (RING > epi ? RING : epi);
+        float* pst = pf + TM * TN;                                   // mean [SR][64], var [SR][64]
+        const rsrc_t rm = make_rsrc(a.save_m, (size_t)a.B * a.P * a.N * 4);
+        const rsrc_t rmu = make_rsrc(a.save_mean, (size_t)a.B * a.N * 4);
+        const rsrc_t rva = make_rsrc(a.save_var, (size_t)a.B * a.N * 4);
+        const int rr = lane >> 4, c4 = 4 * (lane & 15);   // lane-linear: 4 rows x 64 columns per copy
+        for (int q = w; 4 * q < rows_t; q += 4)
+            dma16(rm, pf + q * 256, (uint32_t)(((size_t)(row0 + 4 * q + rr) * a.N + col0 + c4) * 4));
+        const int nsm = rows_t / a.P;
+        for (int q = w; 4 * q < nsm; q += 4) {
+            const uint32_t o = (uint32_t)(((size_t)(s0 + 4 * q + rr) * a.N + col0 + c4) * 4);
+            dma16(rmu, pst + q * 256, o);
+            dma16(rva, pst + SR * TN + q * 256, o);
+        }
+    }
     if constexpr (DMA) {
         // ring slot: the tile's NBA row blocks, then its 4 column blocks (16 x 16 floats each, as
         // lane-linear fragment images: lane (j, h) of block q holds row/column 16 q + j, k 4h..4h+3)
@@ -432,7 +455,10 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             // tile holds whole samples and 64 of its columns: everything gcn_bwd_kernel reads per
             // (sample, column)); the same operations in the same order as gcn_bwd_kernel's loop
             // form, so dz and the partial sums are bit-identical to the unfused pair of launches
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's prefetch copies landed
             __syncthreads();
+            const float* pmu = pf + TM * TN;
+            const float* pva = pmu + SR * TN;
             const uint32_t thr = drop_threshold(a.drop_p);
             const float scale = a.drop_p > 0.0f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
             const float inv = 1.0f / (float)P;
@@ -441,13 +467,14 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
                 if (c >= cols) continue;
                 const int col = col0 + c, s = s0 + sl;
                 const size_t rs = (size_t)row0 + (size_t)sl * P;
-                const float mean = a.save_mean[(size_t)s * a.N + col];
-                const float rstd = 1.0f / sqrtf(a.save_var[(size_t)s * a.N + col] + a.bn_eps);
+                const float mean = pmu[sl * TN + c];
+                const float rstd = 1.0f / sqrtf(pva[sl * TN + c] + a.bn_eps);
                 const float gam = a.bn_w[col];
                 float* dc = zt + sl * P * ZS + c;
+                const float* mc = pf + sl * P * TN + c;
                 float sb = 0.0f, sg = 0.0f, sbias = 0.0f;
                 for (int p = 0; p < P; ++p) {   // dxn = dropout'(dy), the two BatchNorm sums
-                    const float mv = a.save_m[(rs + p) * a.N + col];
+                    const float mv = mc[p * TN];
                     const float t = mv > 0.0f ? mv : mv * a.slope;
                     const float xh = (t - mean) * rstd;
                     float g = dc[p * ZS];
@@ -458,7 +485,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
                     dc[p * ZS] = g;
                 }
                 for (int p = 0; p < P; ++p) {   // BatchNorm and leaky_relu backward -> dM
-                    const float mv = a.save_m[(rs + p) * a.N + col];
+                    const float mv = mc[p * TN];
                     const float t = mv > 0.0f ? mv : mv * a.slope;
                     const float xh = (t - mean) * rstd;
                     const float g = dc[p * ZS];
@@ -1023,6 +1050,8 @@ hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
         size_t e = 4 * ((size_t)32 * WR * ZS + (((size_t)a.S_t * a.P * a.P + 3) & ~(size_t)3) + 4 * TN);
         if (EPI == HYPER_EPI_GCN_TRAIN) e += 4 * ((size_t)32 * WR * ZS + 2 * (size_t)a.S_t * TN);
         lds = e > lds ? e : lds;
+        // the prefetched M tile and statistics, past both the ring and the epilogue tile
+        if (EPI == HYPER_EPI_GCN_BWD) lds += 4 * ((size_t)32 * WR * TN + 2 * (size_t)((a.S_t + 3) & ~3) * TN);
     }
     if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
     if (lds > 64 * 1024) {

@@ -134,11 +134,17 @@ size_t dsave_layout(const dadmm_hyper_net* net, int B, DSave* d, float* base) {
     return off;
 }
 
-// DADMM_GCNBWD_FUSE=0 in the environment: the unfused pair (linear, then gcn backward) for A/B
-// timing and the bit-identity test
-bool gcn_bwd_fused() {
+// Whether a GCN layer's block backward runs in the epilogue of the input-gradient GEMM above it.
+// It pays while that GEMM's grid leaves the chip idle (~2 workgroups per CU: B = 256, the step is
+// launch-bound, 9.31 -> 9.10 ms); on full grids the longer epilogue and its LDS cost more than the
+// launch saved (B = 4096: 49.6 -> 50.5 ms, profiles/r05/gcn_bwd_fuse_r05m.txt).
+// DADMM_GCNBWD_FUSE=0 / =1 in the environment: never / always (A/B timing, the bit-identity test).
+bool gcn_bwd_fused(int B, int P, int Kin) {
     const char* e = getenv("DADMM_GCNBWD_FUSE");
-    return !(e != nullptr && e[0] == '0');
+    if (e != nullptr && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+    const long st = P <= 32 ? 32 / P : 1;
+    const long tiles = (B + st - 1) / st * ((Kin + 63) / 64);
+    return tiles < 480;
 }
 
 #define TRY(call)                       \
@@ -266,7 +272,6 @@ static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* At
     // gcn backward is its own launch (its dy comes from the LayerNorm backward); layers 4 .. 1 run
     // theirs in the epilogue of the input-gradient GEMM of the layer above
     // (dadmm_hyper_linear_gcn_bwd: no dy round trip, one launch instead of two)
-    const bool fuse = gcn_bwd_fused();
     float* dZ = nullptr;   // this layer's dZ once formed
     for (int i = 4; i >= 0; --i) {
         const int N = net->width[i];
@@ -283,7 +288,7 @@ static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* At
             if (!defer)
                 TRY(dadmm_hyper_wgrad(rows, N, Kin, dZ, N, sv->y[i - 1], Kin, Kin, nullptr, 0, g->conv_w[i],
                                       nullptr, 1, w.wscr, stream));
-            if (fuse) {
+            if (gcn_bwd_fused(B, P, Kin)) {
                 // layer i - 1's dZ straight from this layer's dZ (not the buffer holding it)
                 float* nz = defer ? d.dZ[i - 1] : (dZ == w.dx[0] ? w.dx[1] : w.dx[0]);
                 TRY(dadmm_hyper_linear_gcn_bwd(B, P, N, Kin, dZ, N, g->conv_wt[i], sv->m[i - 1], sv->mean[i - 1],

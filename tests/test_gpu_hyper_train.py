@@ -573,7 +573,7 @@ def test_fused_gcn_backward_bit_identical(cuda, monkeypatch, P, n, hidden, B, pe
     bt = torch.from_numpy(b[:B]).to(cuda)[..., None]
     label = torch.randn(B, n, 1, device=cuda, generator=g)
     out = {}
-    for fuse in ("1", "0"):
+    for fuse in ("1", "0"):   # always / never fused (the default decides by grid size)
         monkeypatch.setenv("DADMM_GCNBWD_FUSE", fuse)
         model = copy.deepcopy(model0)
         AtAy = AtAy0.clone().requires_grad_(True)
