@@ -486,7 +486,41 @@ int dadmm_gnn_step_backward(const dadmm_dims* d, int32_t k, const int32_t* visit
     a.Atb = Atb;
     a.U = U;
     a.D = D;
-    dadmm::GnnGrads g{gy1, gU1, gd1, gy, gU, gd, gAtAy, ghyp};
+    dadmm::GnnGrads g{gy1, gU1, gd1, gy, gU, gd, gAtAy, ghyp, nullptr, nullptr, nullptr, nullptr, {}};
+    return hip_rc(dadmm::gnn_launch_step_backward(a, k, g, (hipStream_t)stream), "step backward launch");
+}
+
+int dadmm_gnn_step_backward_ex(const dadmm_dims* d, int32_t k, const int32_t* visit_ptr,
+                               const uint8_t* visit_q, const float* deg, const float* hyp_k,
+                               const float* y_k, const float* AtAy, const float* Atb, const float* U,
+                               const float* D, const float* gy1, const float* gU1, const float* gd1,
+                               float* gy, float* gU, float* gd, float* gAtAy, float* ghyp,
+                               const float* gy_add, const dadmm_head_bwd* head, void* stream) {
+    dadmm::GnnArgs a;
+    int rc = gnn_common(d, &a);
+    if (rc) return rc;
+    if (k < 0 || k >= d->K) return fail(DADMM_EINVAL, "k=%d outside [0, K)", k);
+    if (d->B == 0) return ok();
+    if (!visit_ptr || !visit_q || !deg || !hyp_k || !y_k || !AtAy || !Atb || !U || !D || !gy ||
+        !gU || !gd || !gAtAy || !ghyp)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (head && (!head->z || !head->dz)) return fail(DADMM_EINVAL, "head: z and dz are required");
+    a.vptr = visit_ptr;
+    a.vq = visit_q;
+    a.deg = deg;
+    a.hyp = hyp_k;
+    a.yk = y_k;
+    a.AtAy = AtAy;
+    a.Atb = Atb;
+    a.U = U;
+    a.D = D;
+    dadmm::GnnGrads g{gy1, gU1, gd1, gy, gU, gd, gAtAy, ghyp, gy_add, nullptr, nullptr, nullptr, {}};
+    if (head) {
+        g.ghyp_add = head->ghyp_add;
+        g.hz = head->z;
+        g.hdz = head->dz;
+        for (int c = 0; c < 4; ++c) g.hmax[c] = head->maxv[c];
+    }
     return hip_rc(dadmm::gnn_launch_step_backward(a, k, g, (hipStream_t)stream), "step backward launch");
 }
 
@@ -857,6 +891,29 @@ int dadmm_hyper_head(int32_t B, int32_t K, int32_t H, const float* x, int32_t ld
     a.maxv[1] = tau_max;
     a.maxv[2] = rho_max;
     a.maxv[3] = eta_max;
+    hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_HEAD, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "head launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
+int dadmm_hyper_head_train(int32_t B, int32_t K, int32_t H, const float* x, int32_t ldx, const float* W,
+                           const float* bias, float alpha_max, float tau_max, float rho_max, float eta_max,
+                           float* z, float* hyp, void* stream) {
+    if (!z) return fail(DADMM_EINVAL, "z is NULL");
+    if (H < 1) return fail(DADMM_EINVAL, "bad head rows H=%d", H);
+    dadmm::HyperArgs a;
+    int rc = hyper_input(B, K, 4 * H, x, ldx, K, nullptr, 0, W, hyp, 4 * H, &a);
+    if (rc) return rc;
+    if (!bias) return fail(DADMM_EINVAL, "bias is NULL");
+    a.bias = bias;
+    a.P = 1;
+    a.B = B;
+    a.H = H;
+    a.maxv[0] = alpha_max;
+    a.maxv[1] = tau_max;
+    a.maxv[2] = rho_max;
+    a.maxv[3] = eta_max;
+    a.save_m = z;
     hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_HEAD, (hipStream_t)stream);
     if (e != hipSuccess) return fail(DADMM_EHIP, "head launch: %s", hipGetErrorString(e));
     return ok();

@@ -976,7 +976,7 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
                 const float grb = inside(gr, -gclip, gclip) ? -al * zb : 0.0f;
                 pt = grb * sg;
                 pr = grb * a.D[off];
-                gg.gy[off] = zb;
+                gg.gy[off] = gg.gy_add != nullptr ? zb + gg.gy_add[off] : zb;
                 gg.gU[off] = gg.gU[off] + grb * a.deg[g0 + p];
                 gg.gd[off] = grb * rh;
                 gg.gAtAy[off] = grb;
@@ -990,7 +990,21 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
     const int SW = 3 * P * 64 + 4 * P + VW;     // floats per wave slice
     for (int i = threadIdx.x; i < 4 * H; i += THREADS) {
         const float* r0 = lds + 3 * P * 64 + i;
-        gg.ghyp[(size_t)s * 4 * H + i] = ((r0[0] + r0[SW]) + r0[2 * SW]) + r0[3 * SW];
+        const size_t idx = (size_t)s * 4 * H + i;
+        float g = ((r0[0] + r0[SW]) + r0[2 * SW]) + r0[3 * SW];
+        if (gg.ghyp_add != nullptr) g = g + gg.ghyp_add[idx];
+        gg.ghyp[idx] = g;
+        if (gg.hdz != nullptr) {
+            // the hyper-parameter head's backward (dadmm_hyper_train.hip head_act_kernel, mode 1)
+            const int c = i / H;
+            const float mx = gg.hmax[c];
+            const float sg = 1.0f / (1.0f + expf(-gg.hz[idx]));
+            const float v = fminf(fmaxf(sg, 1e-4f), 0.9999f) * mx;
+            if (c > 0 && !(v <= 0.9999f)) g = 0.0f;           // clamp(max=0.9999)
+            g = g * mx;
+            if (!(sg >= 1e-4f && sg <= 0.9999f)) g = 0.0f;    // clamp(1e-4, 0.9999)
+            gg.hdz[idx] = g * ((1.0f - sg) * sg);              // sigmoid
+        }
     }
 }
 

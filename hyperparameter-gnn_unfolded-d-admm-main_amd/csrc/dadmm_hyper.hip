@@ -393,6 +393,8 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
                     if (EPI == HYPER_EPI_BIAS && a.addend != nullptr)
                         v = a.addend[(size_t)(row0 + rr) * a.ld_add + col] + v;
                     if (EPI == HYPER_EPI_HEAD) {
+                        // training: the logits too (the head's backward reads them)
+                        if (a.save_m != nullptr) a.save_m[(size_t)(row0 + rr) * a.ldy + col] = v;
                         v = 1.0f / (1.0f + expf(-v));                  // torch.sigmoid  (:170)
                         v = fminf(fmaxf(v, 1e-4f), 0.9999f);          // clamp          (:171)
                         v = v * mx;                                   // * *_max        (:180-189)

@@ -8,7 +8,7 @@
 //   x_i = Dropout(BN_batch(leaky(A_hat (x_{i-1} W_i^T) + b_i)))   5 x dadmm_hyper_gcn_train
 //   e   = LayerNorm(x_5)                                          dadmm_hyper_rownorm
 //   d_j = LReLU(LN(Dropout(d_{j-1} D_j^T + c_j)))                 3 x dadmm_hyper_linear_ln_train
-//   z   = d_3 fc^T + f; hyp = head(z)                             dadmm_hyper_linear, _head_act
+//   z   = d_3 fc^T + f; hyp = head(z)                             dadmm_hyper_head_train
 // Backward: the same stages reversed; the parameter gradients are accumulated IN PLACE into the
 // caller's buffers (dadmm_hyper_wgrad / dadmm_hyper_colsum: G += ...), the input gradients run as
 // dadmm_hyper_linear with the caller's transposed weights. Everything is enqueued on `stream`;
@@ -204,17 +204,18 @@ int dadmm_hyper_train_forward(const dadmm_hyper_net* net, int32_t B, const float
         width = N;
     }
     const int H4 = 4 * net->H;
-    TRY(dadmm_hyper_linear(B, width, H4, x, width, width, nullptr, 0, net->fc_w, net->fc_b, sv->z, H4, stream));
-    TRY(dadmm_hyper_head_act(0, B, net->H, sv->z, nullptr, net->maxv[0], net->maxv[1], net->maxv[2],
-                             net->maxv[3], sv->hyp, stream));
+    // fc and the head in one launch (the logits saved for the backward)
+    TRY(dadmm_hyper_head_train(B, width, net->H, x, width, net->fc_w, net->fc_b, net->maxv[0], net->maxv[1],
+                               net->maxv[2], net->maxv[3], sv->z, sv->hyp, stream));
     return DADMM_OK;
 }
 
 static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
                           const float* ahat, int32_t ahat_per_sample, uint64_t seed, const dadmm_hyper_saved* sv,
                           const float* dhyp, const dadmm_hyper_grads* g, float* dAtAy, void* work, float* dsave,
-                          bool acc_dA, void* stream) {
-    if (check_net(net, B) != DADMM_OK || !sv || !dhyp || !g || !dAtAy || !work) return DADMM_EINVAL;
+                          bool acc_dA, void* stream, bool dz_ready = false) {
+    if (check_net(net, B) != DADMM_OK || !sv || (!dhyp && !dz_ready) || !g || !dAtAy || !work) return DADMM_EINVAL;
+    if (dz_ready && !dsave) return DADMM_EINVAL;
     if (B == 0) return DADMM_OK;
     Work w;
     layout(net, B, &w, (char*)work);
@@ -227,8 +228,9 @@ static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* At
     if (n & 15) return DADMM_EUNSUPPORTED;
     float* dzh = defer ? d.dz : w.dz;
     // head (sigmoid, clamps, maxima) -> d logits
-    TRY(dadmm_hyper_head_act(1, B, net->H, sv->z, dhyp, net->maxv[0], net->maxv[1], net->maxv[2],
-                             net->maxv[3], dzh, stream));
+    if (!dz_ready)
+        TRY(dadmm_hyper_head_act(1, B, net->H, sv->z, dhyp, net->maxv[0], net->maxv[1], net->maxv[2],
+                                 net->maxv[3], dzh, stream));
     // fc: dW, db; dx = dz fc
     const int hid = net->dec_width[2];
     if (!defer)
@@ -335,7 +337,7 @@ int dadmm_hyper_train_backward_deferred(const dadmm_hyper_net* net, int32_t B, c
                                         void* stream) {
     if (!dsave || ((uintptr_t)dsave & 15)) return DADMM_EINVAL;
     return train_backward(net, B, AtAy, Atb, ahat, ahat_per_sample, seed, sv, dhyp, g, dAtAy, work, dsave,
-                          accumulate != 0, stream);
+                          (accumulate & 1) != 0, stream, (accumulate & 2) != 0);
 }
 
 // the (R, N, K) of every batched weight gradient of one deferred pass, in launch order

@@ -146,6 +146,12 @@ struct GnnGrads {
     float* gd;              // dL/ddelta_k
     float* gAtAy;           // dL/dAtAy_k
     float* ghyp;            // dL/dhyp_k [B][4][hyp_rows]
+    // training-backward epilogues (dadmm_gnn_step_backward_ex), all nullable
+    const float* gy_add;    // gy = direct + gy_add (the loss's own gradient on y_k)
+    const float* ghyp_add;  // added to dL/dhyp_k
+    const float* hz;        // the head's logits [B][4 H]: with hdz, the head backward runs here
+    float* hdz;             // d logits [B][4 H]
+    float hmax[4];
 };
 hipError_t gnn_launch_zero(int32_t* p, int words, hipStream_t st);
 hipError_t gnn_launch_check0(const GnnArgs& a, const float* y0, hipStream_t st);

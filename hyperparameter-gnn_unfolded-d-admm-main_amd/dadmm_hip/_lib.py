@@ -61,6 +61,7 @@ EXPORTED_SYMBOLS = (
     "dadmm_hyper_train_wgrad",
     "dadmm_hyper_train_wgrad_scratch_bytes",
     "dadmm_hyper_linear_gcn_bwd",
+    "dadmm_hyper_head_train",
     "dadmm_hyper_bn_running_scratch_bytes",
     "dadmm_hyper_bn_running_update",
     "dadmm_gnn_flag_bytes",
@@ -70,6 +71,7 @@ EXPORTED_SYMBOLS = (
     "dadmm_gnn_step",
     "dadmm_gnn_finish",
     "dadmm_gnn_step_backward",
+    "dadmm_gnn_step_backward_ex",
     "dadmm_normal_offset_step",
     "dadmm_prologue",
     "dadmm_tiled_scratch_bytes",
@@ -128,6 +130,12 @@ class HyperSaved(ctypes.Structure):
     _fields_ = [("y", ctypes.c_void_p * 5), ("m", ctypes.c_void_p * 5), ("mean", ctypes.c_void_p * 5),
                 ("var", ctypes.c_void_p * 5), ("e", ctypes.c_void_p), ("dec_y", ctypes.c_void_p * 3),
                 ("dec_xd", ctypes.c_void_p * 3), ("z", ctypes.c_void_p), ("hyp", ctypes.c_void_p)]
+
+
+class HeadBwd(ctypes.Structure):
+    """dadmm_head_bwd: the head-backward epilogue of dadmm_gnn_step_backward_ex."""
+    _fields_ = [("z", ctypes.c_void_p), ("ghyp_add", ctypes.c_void_p), ("maxv", ctypes.c_float * 4),
+                ("dz", ctypes.c_void_p)]
 
 
 class HyperGrads(ctypes.Structure):
@@ -201,7 +209,8 @@ def load() -> ctypes.CDLL:
                        ("dadmm_gnn_gram_acc", [D] + [vp] * 4),
                        ("dadmm_gnn_step", [D, i32] + [vp] * 14),
                        ("dadmm_gnn_finish", [D] + [vp] * 4),
-                       ("dadmm_gnn_step_backward", [D, i32] + [vp] * 18)):
+                       ("dadmm_gnn_step_backward", [D, i32] + [vp] * 18),
+                       ("dadmm_gnn_step_backward_ex", [D, i32] + [vp] * 18 + [ctypes.POINTER(HeadBwd), vp])):
         f = getattr(L, name)
         f.restype = ctypes.c_int
         f.argtypes = args
@@ -252,6 +261,9 @@ def load() -> ctypes.CDLL:
     L.dadmm_hyper_train_backward_deferred.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, vp, i32, u64,
                                                       ctypes.POINTER(HyperSaved), vp, ctypes.POINTER(HyperGrads),
                                                       vp, vp, vp, i32, vp]
+    L.dadmm_hyper_head_train.restype = ctypes.c_int
+    L.dadmm_hyper_head_train.argtypes = [i32, i32, i32, vp, i32, vp, vp, ctypes.c_float, ctypes.c_float,
+                                         ctypes.c_float, ctypes.c_float, vp, vp, vp]
     L.dadmm_hyper_linear_gcn_bwd.restype = ctypes.c_int
     L.dadmm_hyper_linear_gcn_bwd.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, ctypes.c_float, vp,
                                              i32, ctypes.c_float, ctypes.c_float, ctypes.c_uint64, i32, vp, vp,

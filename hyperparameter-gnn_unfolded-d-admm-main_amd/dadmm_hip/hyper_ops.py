@@ -653,10 +653,12 @@ class NativeHyperPlan:
             ctypes.byref(sv), _ptr(dhyp), ctypes.byref(g), _ptr(self.dAtAy), _ptr(self.work), stream))
         return self.dAtAy
 
-    def backward_deferred(self, AtAy, Atb, ahat, per_sample, seed, sv, dhyp, g, dsave, k, stream, acc=None):
+    def backward_deferred(self, AtAy, Atb, ahat, per_sample, seed, sv, dhyp, g, dsave, k, stream, acc=None,
+                          dz_ready=False):
         """backward with the parameter gradients deferred: their operands go to block k of
         ``dsave`` (blocks of ``dsave_per`` floats) for one ``wgrad`` call after the last iteration.
-        ``acc`` [B, P, ns]: d AtAy is added into it (in the last linear's epilogue) and returned."""
+        ``acc`` [B, P, ns]: d AtAy is added into it (in the last linear's epilogue) and returned.
+        ``dz_ready``: the head's logit gradient is already in block k (dhyp unused)."""
         if acc is None and self.dAtAy is None:
             self.dAtAy = torch.zeros((self.B, self.P, self.ns), device=self.dev)
         out = self.dAtAy if acc is None else acc
@@ -664,7 +666,8 @@ class NativeHyperPlan:
         _lib.check("dadmm_hyper_train_backward_deferred", self.L.dadmm_hyper_train_backward_deferred(
             ctypes.byref(self.net), self.B, _ptr(AtAy), _ptr(Atb), _ptr(ahat), int(per_sample), seed,
             ctypes.byref(sv), _ptr(dhyp), ctypes.byref(g), _ptr(out), _ptr(self.work),
-            ctypes.c_void_p(dsave.data_ptr() + 4 * k * self.dsave_per), 0 if acc is None else 1, stream))
+            ctypes.c_void_p(dsave.data_ptr() + 4 * k * self.dsave_per),
+            (0 if acc is None else 1) | (2 if dz_ready else 0), stream))
         return out
 
     def wgrad(self, iters, As, Atb, arena, dsave, g, stream):

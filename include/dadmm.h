@@ -320,6 +320,26 @@ int dadmm_gnn_step_backward(const dadmm_dims* d, int32_t k, const int32_t* visit
                             const float* D, const float* gy1, const float* gU1, const float* gd1,
                             float* gy, float* gU, float* gd, float* gAtAy, float* ghyp,
                             void* stream);
+/* dadmm_gnn_step_backward_ex (ABI 17): dadmm_gnn_step_backward with the training backward's next
+ * two element-wise steps in its epilogue (one launch each saved per iteration):
+ *   gy_add (nullable): gy = (direct dL/dy_k) + gy_add — the loss's own gradient on y_k;
+ *   head (nullable): dL/dhyp_k += head->ghyp_add (nullable), then the hyper-parameter head's
+ *     backward (dadmm_hyper_head_act mode 1 on the logits head->z [B][4H], bit-identical) into
+ *     head->dz [B][4H], the gradient dadmm_hyper_train_backward_deferred takes with flag bit 1.
+ * Replaces the step's adjoint + the adds + the head's derivative of
+ * gnn_dlasso_models_progressive.py:165-237 under torch's backward. */
+typedef struct dadmm_head_bwd {
+    const float* z;         /* [B][4H] logits (dadmm_hyper_saved.z) */
+    const float* ghyp_add;  /* nullable: added to dL/dhyp_k first */
+    float maxv[4];          /* alpha_max, tau_max, rho_max, eta_max */
+    float* dz;              /* [B][4H] out */
+} dadmm_head_bwd;
+int dadmm_gnn_step_backward_ex(const dadmm_dims* d, int32_t k, const int32_t* visit_ptr,
+                               const uint8_t* visit_q, const float* deg, const float* hyp_k,
+                               const float* y_k, const float* AtAy, const float* Atb, const float* U,
+                               const float* D, const float* gy1, const float* gU1, const float* gd1,
+                               float* gy, float* gU, float* gd, float* gAtAy, float* ghyp,
+                               const float* gy_add, const dadmm_head_bwd* head, void* stream);
 
 /* ---- the drivers' loss, fused ----------------------------------------------------------------
  * gnn_dlasso_utils.compute_loss (gnn_dlasso_utils.py:27-88) on the iterates Y [K][B*P][n_store]
@@ -416,6 +436,13 @@ int dadmm_hyper_linear_gcn_bwd(int32_t B, int32_t P, int32_t K, int32_t N, const
                                const float* bn_weight, float bn_eps, const float* ahat, int32_t ahat_per_sample,
                                float slope, float drop_p, uint64_t seed, int32_t site, float* dz, float* part,
                                int32_t bn_eval, void* stream);
+/* dadmm_hyper_head_train (ABI 17): dadmm_hyper_head that also writes the logits z = x fc^T + f
+ * [B][4H] (the training forward's saved activation for dadmm_hyper_head_act's backward) — the
+ * training forward's fc and head activation in one launch; hyp bit-identical to
+ * dadmm_hyper_linear + dadmm_hyper_head_act(mode 0). */
+int dadmm_hyper_head_train(int32_t B, int32_t K, int32_t H, const float* x, int32_t ldx, const float* W,
+                           const float* bias, float alpha_max, float tau_max, float rho_max, float eta_max,
+                           float* z, float* hyp, void* stream);
 /* ---- GNN hypernetwork, training mode ---------------------------------------------------------
  * The same hypernetwork with model.train() semantics (gnn_dlasso_models_progressive.py:52-72:
  * Dropout(0.1) active, BatchNorm1d on each sample's own batch statistics over its P nodes) and the
@@ -592,8 +619,11 @@ int dadmm_hyper_train_backward(const dadmm_hyper_net* net, int32_t B, const floa
  * dsave + k dsave_stride and its AtAy at AtAy + k atay_stride (Atb shared). Replaces ~19
  * launches per iteration by ~19 in all (gnn_dlasso_progressive.py:207-214's backward at small
  * batches is bound by launches, not by work). */
-/* accumulate != 0 (ABI 16): dAtAy += the input gradient (the adjoint's running AtAy gradient, added
- * in the last linear's epilogue: the same bits as writing it and adding after); 0: dAtAy = it. */
+/* accumulate, bit 0 (ABI 16): dAtAy += the input gradient (the adjoint's running AtAy gradient,
+ * added in the last linear's epilogue: the same bits as writing it and adding after); clear:
+ * dAtAy = it. Bit 1 (ABI 17): the head's logit gradient is already in the iteration's dsave block
+ * (its first [B][4H] floats, written by dadmm_gnn_step_backward_ex's head epilogue): dhyp is not
+ * read (may be NULL) and the head's backward launch is skipped. */
 size_t dadmm_hyper_train_dsave_floats(const dadmm_hyper_net* net, int32_t B);
 int dadmm_hyper_train_backward_deferred(const dadmm_hyper_net* net, int32_t B, const float* AtAy,
                                         const float* Atb, const float* ahat, int32_t ahat_per_sample,
