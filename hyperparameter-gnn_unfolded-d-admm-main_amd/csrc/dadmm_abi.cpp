@@ -973,6 +973,22 @@ int dadmm_hyper_gcn_train(int32_t B, int32_t P, int32_t K, int32_t N, const floa
                           int32_t site, float* y, int32_t ldy, float* m_out, float* mean_out,
                           float* var_out, const float* bn_running_mean, const float* bn_running_var,
                           void* stream) {
+    return dadmm::gcn_train_impl(B, P, K, N, x1, ld1, K1, x2, ld2, W, K, nullptr, 0, bias, ahat, ahat_per_sample,
+                                 bn_weight, bn_bias, bn_eps, slope, drop_p, seed, site, y, ldy, m_out, mean_out,
+                                 var_out, bn_running_mean, bn_running_var, stream);
+}
+
+}  // extern "C"
+
+// dadmm_hyper_gcn_train with a column slice of W (row stride ldw) and an addend [B*P][ld_add]
+// added to the mix before the bias (layer 1's Atb half, formed once per forward)
+int dadmm::gcn_train_impl(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1, int32_t ld1, int32_t K1,
+                          const float* x2, int32_t ld2, const float* W, int32_t ldw, const float* addend,
+                          int32_t ld_add, const float* bias, const float* ahat, int32_t ahat_per_sample,
+                          const float* bn_weight, const float* bn_bias, float bn_eps, float slope, float drop_p,
+                          uint64_t seed, int32_t site, float* y, int32_t ldy, float* m_out, float* mean_out,
+                          float* var_out, const float* bn_running_mean, const float* bn_running_var,
+                          void* stream) {
     if ((bn_running_mean == nullptr) != (bn_running_var == nullptr))
         return fail(DADMM_EINVAL, "running mean and variance: both or neither");
     if (B < 0 || P < 2 || P > 160)
@@ -1003,10 +1019,18 @@ int dadmm_hyper_gcn_train(int32_t B, int32_t P, int32_t K, int32_t N, const floa
     a.drop_p = drop_p;
     a.seed = seed;
     a.site = site;
+    if (ldw < K || (ldw & 3)) return fail(DADMM_EINVAL, "ldw=%d < K=%d or not a multiple of 4", ldw, K);
+    a.ldw = ldw;
+    if (addend && (ld_add < N || (ld_add & 3) || !aligned16(addend)))
+        return fail(DADMM_EINVAL, "addend: ld_add=%d < N=%d or misaligned", ld_add, N);
+    a.addend = addend;
+    a.ld_add = ld_add;
     hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_GCN_TRAIN, (hipStream_t)stream);
     if (e != hipSuccess) return fail(DADMM_EHIP, "gcn train launch: %s", hipGetErrorString(e));
     return ok();
 }
+
+extern "C" {
 
 static int bn_running_splits(int32_t iters, int32_t B) {
     // ~64 rows per split (16 per wave): enough blocks to spread the sums over the chip

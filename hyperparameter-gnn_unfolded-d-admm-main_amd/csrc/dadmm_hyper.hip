@@ -540,6 +540,16 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             }
             __syncthreads();
             mix([&](int r, int c, f32x4 v) {
+                if (a.addend != nullptr) {   // layer 1's Atb half (formed once per forward)
+                    const float* src = a.addend + (size_t)(row0 + r) * a.ld_add + col0 + c;
+                    f32x4 ad = zero;
+                    if (c + 4 <= cols) {
+                        ad = *(const f32x4*)src;
+                    } else {
+                        for (int e = 0; e < cols - c; ++e) ad[e] = src[e];
+                    }
+                    v = v + ad;
+                }
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = v[e] + colp[c + e];
                 *(f32x4*)(mt + r * ZS + c) = v;

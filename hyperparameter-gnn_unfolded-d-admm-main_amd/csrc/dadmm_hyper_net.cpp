@@ -163,9 +163,25 @@ size_t dadmm_hyper_train_work_bytes(const dadmm_hyper_net* net, int32_t B) {
     return layout(net, B, &w, nullptr);
 }
 
+int dadmm_hyper_train_atb_mix(const dadmm_hyper_net* net, int32_t B, const float* Atb, const float* ahat,
+                              int32_t ahat_per_sample, float* out, void* stream) {
+    if (check_net(net, B) != DADMM_OK || !Atb || !ahat || !out) return DADMM_EINVAL;
+    if (net->n & 15) return DADMM_EUNSUPPORTED;
+    const int n = net->n, N = net->width[0];
+    // raw GCN epilogue: A_hat (Atb W1[:, n:2n]^T), no bias / activation / normalisation
+    return dadmm_hyper_gcn_ex(B, net->P, n, N, Atb, net->ld, net->conv_w[0] + n, 2 * n, nullptr, 0, nullptr, ahat,
+                              ahat_per_sample, nullptr, nullptr, nullptr, nullptr, 0.0f, 0.0f, 1, out, N, stream);
+}
+
 int dadmm_hyper_train_forward(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
                               const float* ahat, int32_t ahat_per_sample, uint64_t seed,
                               const dadmm_hyper_saved* sv, void* work, void* stream) {
+    return dadmm_hyper_train_forward_ex(net, B, AtAy, Atb, nullptr, ahat, ahat_per_sample, seed, sv, work, stream);
+}
+
+int dadmm_hyper_train_forward_ex(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
+                                 const float* atb_mix, const float* ahat, int32_t ahat_per_sample, uint64_t seed,
+                                 const dadmm_hyper_saved* sv, void* work, void* stream) {
     if (check_net(net, B) != DADMM_OK || !sv || !work) return DADMM_EINVAL;
     if (B == 0) return DADMM_OK;
     Work w;
@@ -178,7 +194,11 @@ int dadmm_hyper_train_forward(const dadmm_hyper_net* net, int32_t B, const float
     if (n & 15) return DADMM_EUNSUPPORTED;   // the caller concatenates in that case (dadmm_hip)
     for (int i = 0; i < 5; ++i) {
         const int N = net->width[i];
-        TRY(dadmm_hyper_gcn_train(B, P, K, N, x1, ld1, K1, x2, ld2, net->conv_w[i], net->conv_b[i], ahat,
+        // layer 1 with the Atb half precomputed (atb_mix): its GEMM runs over AtAy alone, the first
+        // n columns of W1, and the mix of the Atb half is added before the bias
+        const bool half = i == 0 && atb_mix != nullptr;
+        TRY(dadmm::gcn_train_impl(B, P, half ? n : K, N, x1, ld1, half ? n : K1, half ? nullptr : x2, half ? 0 : ld2,
+                                  net->conv_w[i], K, half ? atb_mix : nullptr, half ? N : 0, net->conv_b[i], ahat,
                                   ahat_per_sample, net->bn_w[i], net->bn_b[i], net->bn_eps[i], LEAKY,
                                   i < 4 ? net->drop_enc : 0.0f, seed, i, sv->y[i], N, sv->m[i], sv->mean[i],
                                   sv->var[i], net->bn_eval ? net->bn_rm[i] : nullptr,

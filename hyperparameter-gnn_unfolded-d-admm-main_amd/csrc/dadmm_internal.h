@@ -323,6 +323,14 @@ struct GcnBwdArgs {
     int bn_eval;            // BatchNorm on constant (running) statistics: no batch-statistics terms
 };
 hipError_t launch_gcn_bwd(const GcnBwdArgs& a, hipStream_t st);
+// dadmm_hyper_gcn_train with a column slice of W (row stride ldw >= K) and an addend
+// [B*P][ld_add] (nullable) added to the mix A_hat (x W^T) before the bias (dadmm_abi.cpp)
+int gcn_train_impl(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1, int32_t ld1, int32_t K1,
+                   const float* x2, int32_t ld2, const float* W, int32_t ldw, const float* addend, int32_t ld_add,
+                   const float* bias, const float* ahat, int32_t ahat_per_sample, const float* bn_weight,
+                   const float* bn_bias, float bn_eps, float slope, float drop_p, uint64_t seed, int32_t site,
+                   float* y, int32_t ldy, float* m_out, float* mean_out, float* var_out,
+                   const float* bn_running_mean, const float* bn_running_var, void* stream);
 
 // BatchNorm running statistics after T = iters * B sequential train-mode calls, closed form
 // (dadmm_hyper_bn_running_update): up to BN_MAX_LAYERS layers in one pair of launches

@@ -55,6 +55,8 @@ EXPORTED_SYMBOLS = (
     "dadmm_hyper_transpose",
     "dadmm_hyper_train_work_bytes",
     "dadmm_hyper_train_forward",
+    "dadmm_hyper_train_forward_ex",
+    "dadmm_hyper_train_atb_mix",
     "dadmm_hyper_train_backward",
     "dadmm_hyper_train_dsave_floats",
     "dadmm_hyper_train_backward_deferred",
@@ -251,6 +253,11 @@ def load() -> ctypes.CDLL:
     L.dadmm_hyper_train_forward.restype = ctypes.c_int
     L.dadmm_hyper_train_forward.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, vp, i32, u64,
                                             ctypes.POINTER(HyperSaved), vp, vp]
+    L.dadmm_hyper_train_forward_ex.restype = ctypes.c_int
+    L.dadmm_hyper_train_forward_ex.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, vp, vp, i32, u64,
+                                               ctypes.POINTER(HyperSaved), vp, vp]
+    L.dadmm_hyper_train_atb_mix.restype = ctypes.c_int
+    L.dadmm_hyper_train_atb_mix.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, i32, vp, vp]
     L.dadmm_hyper_train_backward.restype = ctypes.c_int
     L.dadmm_hyper_train_backward.argtypes = [ctypes.POINTER(HyperNet), i32, vp, vp, vp, i32, u64,
                                              ctypes.POINTER(HyperSaved), vp, ctypes.POINTER(HyperGrads),

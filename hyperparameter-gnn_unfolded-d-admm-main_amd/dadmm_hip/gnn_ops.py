@@ -197,9 +197,10 @@ class GnnTrainFn(torch.autograd.Function):
         # GCN layer reads them at a fixed stride
         As = torch.empty((K, run.B, run.P, run.op.n_store), device=dev)
         with torch.cuda.device(dev):
+            c1 = plan.atb_mix(run.Atb, a_hat, per_sample, stream)
             for k in range(K):
                 AtAy = run.gram(k, out=As[k])
-                plan.forward(AtAy, run.Atb, a_hat, per_sample, seeds[k], svs[k], stream)
+                plan.forward(AtAy, run.Atb, a_hat, per_sample, seeds[k], svs[k], stream, atb_mix=c1)
                 _, U, D = run.step(k, AtAy, plan.hyp(arena, k), U, D)
                 Us.append(U)
                 Ds.append(D)

@@ -571,6 +571,7 @@ class NativeHyperPlan:
         self.dAtAy = None
         self.wscratch = None
         self.bn_scratch = None
+        self.c1 = None              # layer 1's Atb half (atb_mix), one buffer per plan
         self.dsave_per = L.dadmm_hyper_train_dsave_floats(ctypes.byref(net), B)   # floats, multiple of 4
 
     @staticmethod
@@ -638,10 +639,21 @@ class NativeHyperPlan:
             self.per, iters, self.B, self.P, _ptr(_rs_weights(T, m, self.dev)), (1.0 - m) ** T,
             _ptr(self.bn_scratch), stream))
 
-    def forward(self, AtAy, Atb, ahat, per_sample, seed, sv, stream):
-        _lib.check("dadmm_hyper_train_forward", self.L.dadmm_hyper_train_forward(
-            ctypes.byref(self.net), self.B, _ptr(AtAy), _ptr(Atb), _ptr(ahat), int(per_sample), seed,
-            ctypes.byref(sv), _ptr(self.work), stream))
+    def atb_mix(self, Atb, ahat, per_sample, stream):
+        """Layer 1's Atb half A_hat (Atb W1[:, n:]^T), once per forward (dadmm_hyper_train_atb_mix),
+        for forward(..., atb_mix=); None where the in-place two-segment layout does not apply."""
+        if self.n % 16 or os.environ.get("DADMM_HYPER_ATB_HOIST", "1") == "0":   # (env: A/B timing)
+            return None
+        if self.c1 is None:
+            self.c1 = torch.empty((self.B * self.P, self.W[0]), device=self.dev)
+        _lib.check("dadmm_hyper_train_atb_mix", self.L.dadmm_hyper_train_atb_mix(
+            ctypes.byref(self.net), self.B, _ptr(Atb), _ptr(ahat), int(per_sample), _ptr(self.c1), stream))
+        return self.c1
+
+    def forward(self, AtAy, Atb, ahat, per_sample, seed, sv, stream, atb_mix=None):
+        _lib.check("dadmm_hyper_train_forward_ex", self.L.dadmm_hyper_train_forward_ex(
+            ctypes.byref(self.net), self.B, _ptr(AtAy), _ptr(Atb), _ptr(atb_mix), _ptr(ahat), int(per_sample),
+            seed, ctypes.byref(sv), _ptr(self.work), stream))
 
     def backward(self, AtAy, Atb, ahat, per_sample, seed, sv, dhyp, g, stream):
         """d AtAy (a buffer of the plan, overwritten by the next call) from d hyp; the parameter

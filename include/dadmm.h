@@ -603,6 +603,16 @@ size_t dadmm_hyper_train_work_bytes(const dadmm_hyper_net* net, int32_t B);
 int dadmm_hyper_train_forward(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
                               const float* ahat, int32_t ahat_per_sample, uint64_t seed,
                               const dadmm_hyper_saved* sv, void* work, void* stream);
+/* ABI 17: layer 1's input is cat(AtAy_k, Atb) (:165) and Atb does not change between the
+ * iterations of a forward, so its half of the GCNConv, A_hat (Atb W1[:, n:]^T) [B*P][width_0], is
+ * formed once per forward (dadmm_hyper_train_atb_mix) and dadmm_hyper_train_forward_ex adds it to
+ * layer 1's mix before the bias, running that GEMM over AtAy alone (half the depth). atb_mix NULL:
+ * dadmm_hyper_train_forward. The backward and the weight gradients read AtAy and Atb as before. */
+int dadmm_hyper_train_atb_mix(const dadmm_hyper_net* net, int32_t B, const float* Atb, const float* ahat,
+                              int32_t ahat_per_sample, float* out, void* stream);
+int dadmm_hyper_train_forward_ex(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
+                                 const float* atb_mix, const float* ahat, int32_t ahat_per_sample, uint64_t seed,
+                                 const dadmm_hyper_saved* sv, void* work, void* stream);
 int dadmm_hyper_train_backward(const dadmm_hyper_net* net, int32_t B, const float* AtAy, const float* Atb,
                                const float* ahat, int32_t ahat_per_sample, uint64_t seed,
                                const dadmm_hyper_saved* sv, const float* dhyp, const dadmm_hyper_grads* g,
