@@ -575,7 +575,14 @@ __global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int 
 //   optimistic flags, every block exits; else the update again with g = 0 (:216-218), writing the
 //   guard flags themselves.
 constexpr int UP_CH = 4;
-constexpr int UCB = 128;
+// columns per item: 128 (a wave instruction covers 2 agent rows) or 64 (4 rows; half the LDS per
+// workgroup, so more workgroups fit per CU at large P)
+#ifndef DADMM_STEP_UCB
+#define DADMM_STEP_UCB 128
+#endif
+constexpr int UCB = DADMM_STEP_UCB;
+constexpr int RPI = 256 / UCB;    // agent rows per wave instruction (UCB / 4 lanes per row)
+static_assert(UCB == 64 || UCB == 128, "UCB");
 // DADMM_STEP_KEEPU=1: the step keeps phase 1's U rows in registers for phase 2 (one fewer HBM
 // stream) — 97 instead of 82 VGPRs, four instead of five waves per SIMD: 86.1-86.4 vs 84.7-85.0 ms
 // at the configs[4] shard forward (profiles/r04/variants_r04o_step_keepu.txt), so off
@@ -605,9 +612,9 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     const int ncb = (n + UCB - 1) / UCB;
     const int s = item / ncb;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int half = lane >> 5;
-    const int c = (item % ncb) * UCB + 4 * (lane & 31);
-    const int cl = 4 * (lane & 31);                  // column within the block
+    const int half = lane / (UCB / 4);               // the lane's row within the instruction's RPI
+    const int c = (item % ncb) * UCB + 4 * (lane % (UCB / 4));
+    const int cl = 4 * (lane % (UCB / 4));                  // column within the block
     const bool cv = c < n;
     const size_t base = (size_t)s * P * n + (cv ? c : 0);
     bool yzero = false;
@@ -628,7 +635,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     const float* __restrict__ U = a.U;
     float* __restrict__ Yk = a.yptr[k + 1];
     const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
-    // row pairs: wave w handles pairs w, w + 4, ...; lane half selects the row of the pair
+    // row groups (RPI rows): wave w handles groups w, w + 4, ...; `half` selects the lane's row
     bool bad_y = false, bad_g = false;
     constexpr int UMAX = KEEPU ? 4 : 1;               // 2 * WAVES * UP_CH * UMAX = 64 rows
     f32x4 ukeep[UMAX][UP_CH];
@@ -644,7 +651,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
             bool okv[UP_CH];
 #pragma unroll
             for (int u = 0; u < UP_CH; ++u) {
-                const int p = 2 * (q0 + WAVES * u) + half;
+                const int p = RPI * (q0 + WAVES * u) + half;
                 const int pc = p < P ? p : P - 1;
                 okv[u] = p < P && cv;
                 const size_t off = base + (size_t)pc * n;
@@ -670,7 +677,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
                     dv[u][r] = ok ? dv[u][r] : 0.0f;
                 }
                 if constexpr (KEEPU) ukeep[it][u] = uv[u];
-                const int p = 2 * (q0 + WAVES * u) + half;
+                const int p = RPI * (q0 + WAVES * u) + half;
                 if (ok && fix != nullptr) *(f32x4*)(fix + base + (size_t)p * n) = yv[u];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -687,7 +694,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
             f32x4 tv[UP_CH], bv[UP_CH], uv[UP_CH], dv[UP_CH];
 #pragma unroll
             for (int u = 0; u < UP_CH; ++u) {
-                const int p = 2 * (q0 + WAVES * u) + half;
+                const int p = RPI * (q0 + WAVES * u) + half;
                 tv[u] = bv[u] = uv[u] = dv[u] = yv[u] = z4;
                 if (p < P && cv) {
                     const size_t off = base + (size_t)p * n;
@@ -701,7 +708,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
             }
 #pragma unroll
             for (int u = 0; u < UP_CH; ++u) {
-                const int p = 2 * (q0 + WAVES * u) + half;
+                const int p = RPI * (q0 + WAVES * u) + half;
                 gv[u] = z4;
                 if (p < P && cv) {
                     const float ta = hyp_at(a, s, 1, p), rh = hyp_at(a, s, 2, p);
@@ -722,14 +729,14 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
         } else {   // resolve: the batch's gradient is zero (:216-218)
 #pragma unroll
             for (int u = 0; u < UP_CH; ++u) {
-                const int p = 2 * (q0 + WAVES * u) + half;
+                const int p = RPI * (q0 + WAVES * u) + half;
                 gv[u] = yv[u] = z4;
                 if (p < P && cv && !yzero) yv[u] = *(const f32x4*)(ys + base + (size_t)p * n);
             }
         }
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
-            const int p = 2 * (q0 + WAVES * u) + half;
+            const int p = RPI * (q0 + WAVES * u) + half;
             if (p < P) {
                 f32x4 v = z4;
                 if (cv) {
@@ -748,9 +755,9 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     if constexpr (KEEPU) {
 #pragma unroll
         for (int it = 0; it < UMAX; ++it)
-            if (2 * (w + it * WAVES * UP_CH) < P) phase1(w + it * WAVES * UP_CH, it);
+            if (RPI * (w + it * WAVES * UP_CH) < P) phase1(w + it * WAVES * UP_CH, it);
     } else {
-        for (int q0 = w; 2 * q0 < P; q0 += WAVES * UP_CH) phase1(q0, 0);
+        for (int q0 = w; RPI * q0 < P; q0 += WAVES * UP_CH) phase1(q0, 0);
     }
     __syncthreads();
     bool bad_u = false;
@@ -759,7 +766,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
         float etv[UP_CH];
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
-            const int p = 2 * (q0 + WAVES * u) + half;
+            const int p = RPI * (q0 + WAVES * u) + half;
             if constexpr (KEEPU) {
                 uv[u] = ukeep[it][u];
             } else if constexpr (FUSED && DADMM_STEP_NOBR) {
@@ -776,7 +783,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
         }
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
-            const int p = 2 * (q0 + WAVES * u) + half;
+            const int p = RPI * (q0 + WAVES * u) + half;
             if (p >= P || !cv) continue;
             const f32x4 yp = *(const f32x4*)(yl + p * UCB + cl);
             f32x4 acc = z4;
@@ -803,9 +810,9 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     if constexpr (KEEPU) {
 #pragma unroll
         for (int it = 0; it < UMAX; ++it)
-            if (2 * (w + it * WAVES * UP_CH) < P) phase2(w + it * WAVES * UP_CH, it);
+            if (RPI * (w + it * WAVES * UP_CH) < P) phase2(w + it * WAVES * UP_CH, it);
     } else {
-        for (int q0 = w; 2 * q0 < P; q0 += WAVES * UP_CH) phase2(q0, 0);
+        for (int q0 = w; RPI * q0 < P; q0 += WAVES * UP_CH) phase2(q0, 0);
     }
     if (FUSED) {
         flag_or(a.flags + GNN_F_GBAD(k), bad_g);
@@ -820,7 +827,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
 // the fused pass: one workgroup per item
 __global__ __launch_bounds__(THREADS) void step_kernel(GnnArgs a, int k) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    if (DADMM_STEP_KEEPU && a.P <= 2 * WAVES * 2 * 4)
+    if (DADMM_STEP_KEEPU && a.P <= RPI * WAVES * DADMM_STEP_UPCH * 4)
         update_item<true, true>(a, k, blockIdx.x, lds);
     else
         update_item<true>(a, k, blockIdx.x, lds);

@@ -703,7 +703,10 @@ def _native_forward(ctx, L, AtAy, Atb, ahat, model, n, per_sample, seed, defer):
     arena = torch.empty(plan.per, device=dev)
     sv = plan.saved(arena)
     with torch.cuda.device(dev):
-        plan.forward(AtAy, Atb, ahat, per_sample, seed, sv, _stream(dev))
+        # layer 1's Atb half as the whole-forward node forms it (there once per forward; here per
+        # call), so that both paths give the same bits
+        c1 = plan.atb_mix(Atb, ahat, per_sample, _stream(dev))
+        plan.forward(AtAy, Atb, ahat, per_sample, seed, sv, _stream(dev), atb_mix=c1)
     if plan.train and defer:   # eval mode: the running statistics were inputs
         queue_running_stats(model, plan.stats(arena, 1), P, defer)
     elif plan.train:
