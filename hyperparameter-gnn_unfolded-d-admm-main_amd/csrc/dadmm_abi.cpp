@@ -405,7 +405,8 @@ int dadmm_gnn_gram(const dadmm_dims* d, const void* op, int32_t k, float* const*
     return hip_rc(dadmm::gnn_launch_gram(a, k, x, out, 0, (hipStream_t)stream), "gram launch");
 }
 
-int dadmm_gnn_gram_acc(const dadmm_dims* d, const void* op, const float* x, float* out, void* stream) {
+int dadmm_gnn_gram_acc(const dadmm_dims* d, const void* op, const float* x, float* out, const float* addend,
+                       void* stream) {
     dadmm::GnnArgs a;
     int rc = gnn_common(d, &a);
     if (rc) return rc;
@@ -415,7 +416,9 @@ int dadmm_gnn_gram_acc(const dadmm_dims* d, const void* op, const float* x, floa
         return fail(DADMM_EINVAL, "op, x and out must be 16-byte aligned");
     if (dadmm::gnn_gram_lds(a.m_pad) > 160 * 1024)
         return fail(DADMM_EUNSUPPORTED, "m=%d too large for the gram tile", d->m);
+    if (addend && !aligned16(addend)) return fail(DADMM_EINVAL, "addend must be 16-byte aligned");
     set_op(&a, op);
+    a.acc_add = addend;
     return hip_rc(dadmm::gnn_launch_gram(a, 0, x, out, 2, (hipStream_t)stream), "gram launch");
 }
 
@@ -486,7 +489,7 @@ int dadmm_gnn_step_backward(const dadmm_dims* d, int32_t k, const int32_t* visit
     a.Atb = Atb;
     a.U = U;
     a.D = D;
-    dadmm::GnnGrads g{gy1, gU1, gd1, gy, gU, gd, gAtAy, ghyp, nullptr, nullptr, nullptr, nullptr, {}};
+    dadmm::GnnGrads g{gy1, gU1, gd1, gy, gU, gd, gAtAy, ghyp, nullptr, nullptr, nullptr, {}};
     return hip_rc(dadmm::gnn_launch_step_backward(a, k, g, (hipStream_t)stream), "step backward launch");
 }
 
@@ -495,7 +498,7 @@ int dadmm_gnn_step_backward_ex(const dadmm_dims* d, int32_t k, const int32_t* vi
                                const float* y_k, const float* AtAy, const float* Atb, const float* U,
                                const float* D, const float* gy1, const float* gU1, const float* gd1,
                                float* gy, float* gU, float* gd, float* gAtAy, float* ghyp,
-                               const float* gy_add, const dadmm_head_bwd* head, void* stream) {
+                               const dadmm_head_bwd* head, void* stream) {
     dadmm::GnnArgs a;
     int rc = gnn_common(d, &a);
     if (rc) return rc;
@@ -514,7 +517,7 @@ int dadmm_gnn_step_backward_ex(const dadmm_dims* d, int32_t k, const int32_t* vi
     a.Atb = Atb;
     a.U = U;
     a.D = D;
-    dadmm::GnnGrads g{gy1, gU1, gd1, gy, gU, gd, gAtAy, ghyp, gy_add, nullptr, nullptr, nullptr, {}};
+    dadmm::GnnGrads g{gy1, gU1, gd1, gy, gU, gd, gAtAy, ghyp, nullptr, nullptr, nullptr, {}};
     if (head) {
         g.ghyp_add = head->ghyp_add;
         g.hz = head->z;

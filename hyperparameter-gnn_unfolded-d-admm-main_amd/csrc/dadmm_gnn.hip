@@ -321,7 +321,9 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
         const int n0 = 16 * nb + 4 * h;
         if (mg == MG - 1 && sv && n0 < n) {
             f32x4* o = (f32x4*)(out + ((size_t)s * P + p) * n + n0);
-            *o = mode == 2 ? (DADMM_GRAM_OPF ? ocur : *o) + gc : gc;
+            f32x4 v = mode == 2 ? (DADMM_GRAM_OPF ? ocur : *o) + gc : gc;
+            if (mode == 2 && a.acc_add != nullptr) v = v + *(const f32x4*)(a.acc_add + ((size_t)s * P + p) * n + n0);
+            *o = v;
         }
         ocur = onxt;
 #pragma unroll
@@ -428,7 +430,9 @@ __global__ __launch_bounds__(THREADS) void gram_w1_kernel(GnnArgs a, int k, cons
         const int n0 = 16 * nb + 4 * h;
         if (sv && n0 < n) {
             f32x4* o = (f32x4*)(out + ((size_t)s * P + p) * n + n0);
-            *o = mode == 2 ? *o + gc : gc;
+            f32x4 v = mode == 2 ? *o + gc : gc;
+            if (mode == 2 && a.acc_add != nullptr) v = v + *(const f32x4*)(a.acc_add + ((size_t)s * P + p) * n + n0);
+            *o = v;
         }
     }
 }
@@ -481,6 +485,9 @@ __global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int 
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), 0, zero ? 0 : (int)sbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)sbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t roi = __builtin_amdgcn_make_buffer_rsrc(out, 0, mode == 2 ? (int)sbytes : 0, 0x00020000);
+    const bool has_add = mode == 2 && a.acc_add != nullptr;
+    const __amdgpu_buffer_rsrc_t rad =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.acc_add), 0, has_add ? (int)sbytes : 0, 0x00020000);
     __syncthreads();
 
     const int t_end = min(tiles, (grp + 1) * tpw);
@@ -532,8 +539,13 @@ __global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int 
             const uint32_t off = (nb < NT && 16 * nb + 4 * h < n && sv) ? rowoff + (uint32_t)(64 * nb + 16 * h) : 0x80000000u;
             return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(roi, off, 0, 0));
         };
-        // mode 2's out rows two pairs ahead (oc: this pair, on: the next)
+        auto ldd = [&](int nb) -> f32x4 {   // mode 2's addend rows (zeros when there is none)
+            const uint32_t off = (nb < NT && 16 * nb + 4 * h < n && sv) ? rowoff + (uint32_t)(64 * nb + 16 * h) : 0x80000000u;
+            return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rad, off, 0, 0));
+        };
+        // mode 2's out rows (and addend rows) two pairs ahead (oc: this pair, on: the next)
         f32x4 oc0 = ldo(0), oc1 = ldo(1), on0 = ldo(2), on1 = ldo(3);
+        f32x4 dc0 = ldd(0), dc1 = ldd(1), dn0 = ldd(2), dn1 = ldd(3);
         for (int n0 = 0; n0 < NT; n0 += 2) {
             f32x4 at0[MQ], at1[MQ];
             ldt(at0, n0);
@@ -546,8 +558,12 @@ __global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int 
                     g0 = mfma4(at0[g][r], R[g][r], g0);
                     g1 = mfma4(at1[g][r], R[g][r], g1);
                 }
-            const f32x4 o0 = mode == 2 ? oc0 + g0 : g0;
-            const f32x4 o1 = mode == 2 ? oc1 + g1 : g1;
+            f32x4 o0 = mode == 2 ? oc0 + g0 : g0;
+            f32x4 o1 = mode == 2 ? oc1 + g1 : g1;
+            if (has_add) {
+                o0 = o0 + dc0;
+                o1 = o1 + dc1;
+            }
             const uint32_t s0 = (16 * n0 + 4 * h < n && sv) ? rowoff + (uint32_t)(64 * n0 + 16 * h) : 0x80000000u;
             const uint32_t s1 = (n0 + 1 < NT && 16 * (n0 + 1) + 4 * h < n && sv)
                                     ? rowoff + (uint32_t)(64 * (n0 + 1) + 16 * h) : 0x80000000u;
@@ -557,6 +573,10 @@ __global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int 
             oc1 = on1;
             on0 = ldo(n0 + 4);
             on1 = ldo(n0 + 5);
+            dc0 = dn0;
+            dc1 = dn1;
+            dn0 = ldd(n0 + 4);
+            dn1 = ldd(n0 + 5);
         }
     }
 }
@@ -983,7 +1003,7 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
                 const float grb = inside(gr, -gclip, gclip) ? -al * zb : 0.0f;
                 pt = grb * sg;
                 pr = grb * a.D[off];
-                gg.gy[off] = gg.gy_add != nullptr ? zb + gg.gy_add[off] : zb;
+                gg.gy[off] = zb;
                 gg.gU[off] = gg.gU[off] + grb * a.deg[g0 + p];
                 gg.gd[off] = grb * rh;
                 gg.gAtAy[off] = grb;

@@ -136,6 +136,7 @@ struct GnnArgs {
     int32_t* flags;         // [GNN_FLAG_WORDS(K)]
     int32_t* status;        // nullable
     int B, P, m, m_pad, n, n_pad, K, hyp_rows, variant, graph_shared;
+    const float* acc_add;   // gram mode 2 (out += A^T A x): then + acc_add [B][P][n] (nullable)
 };
 struct GnnGrads {
     const float* gy1;       // dL/dy_{k+1} (nullable = 0)
@@ -146,8 +147,7 @@ struct GnnGrads {
     float* gd;              // dL/ddelta_k
     float* gAtAy;           // dL/dAtAy_k
     float* ghyp;            // dL/dhyp_k [B][4][hyp_rows]
-    // training-backward epilogues (dadmm_gnn_step_backward_ex), all nullable
-    const float* gy_add;    // gy = direct + gy_add (the loss's own gradient on y_k)
+    // training-backward epilogue (dadmm_gnn_step_backward_ex), all nullable
     const float* ghyp_add;  // added to dL/dhyp_k
     const float* hz;        // the head's logits [B][4 H]: with hdz, the head backward runs here
     float* hdz;             // d logits [B][4 H]

@@ -208,11 +208,11 @@ def load() -> ctypes.CDLL:
     L.dadmm_gnn_flag_bytes.argtypes = [i32]
     for name, args in (("dadmm_gnn_begin", [D] + [vp] * 7),
                        ("dadmm_gnn_gram", [D, vp, i32] + [vp] * 5),
-                       ("dadmm_gnn_gram_acc", [D] + [vp] * 4),
+                       ("dadmm_gnn_gram_acc", [D] + [vp] * 5),
                        ("dadmm_gnn_step", [D, i32] + [vp] * 14),
                        ("dadmm_gnn_finish", [D] + [vp] * 4),
                        ("dadmm_gnn_step_backward", [D, i32] + [vp] * 18),
-                       ("dadmm_gnn_step_backward_ex", [D, i32] + [vp] * 18 + [ctypes.POINTER(HeadBwd), vp])):
+                       ("dadmm_gnn_step_backward_ex", [D, i32] + [vp] * 17 + [ctypes.POINTER(HeadBwd), vp])):
         f = getattr(L, name)
         f.restype = ctypes.c_int
         f.argtypes = args

@@ -70,12 +70,17 @@ class GnnRun:
                 _ptr(x), _ptr(out), _stream(self.dev)))
         return out
 
-    def gram_acc(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-        """out += A^T A x in one launch (== out.add_(self.gram(0, x=x)), bit for bit)."""
+    def gram_acc(self, x: torch.Tensor, out: torch.Tensor, addend: torch.Tensor = None) -> torch.Tensor:
+        """out += A^T A x in one launch (== out.add_(self.gram(0, x=x)), bit for bit), then
+        out += addend when given (the same bits as a separate add after)."""
         x = _pad_n(x.float(), self.op.n_store).contiguous()
+        if addend is not None:
+            addend = addend.contiguous()
+            assert addend.shape == out.shape
         with torch.cuda.device(self.dev):
             _lib.check("dadmm_gnn_gram_acc", self.L.dadmm_gnn_gram_acc(
-                ctypes.byref(self.d), _ptr(self.op.workspace), _ptr(x), _ptr(out), _stream(self.dev)))
+                ctypes.byref(self.d), _ptr(self.op.workspace), _ptr(x), _ptr(out), _ptr(addend),
+                _stream(self.dev)))
         return out
 
     def step(self, k: int, AtAy, hyp_k, U, D):
@@ -97,20 +102,19 @@ class GnnRun:
                 _stream(self.dev)))
         return self.status
 
-    def step_backward(self, k, y_k, AtAy, hyp_k, U, D, gy1, gU1, gd1, gy_add=None, head=None):
-        """The step's adjoint; ``gy_add`` (dL/dy_k from elsewhere) is added to gy, and ``head``
-        (a _lib.HeadBwd) runs the hyper-parameter head's backward in the same launch
-        (dadmm_gnn_step_backward_ex)."""
+    def step_backward(self, k, y_k, AtAy, hyp_k, U, D, gy1, gU1, gd1, head=None):
+        """The step's adjoint; ``head`` (a _lib.HeadBwd) runs the hyper-parameter head's backward
+        in the same launch (dadmm_gnn_step_backward_ex)."""
         g = self.graphs
         mk = lambda t: None if t is None else t.contiguous()
-        gy1, gU1, gd1, gy_add = mk(gy1), mk(gU1), mk(gd1), mk(gy_add)
+        gy1, gU1, gd1 = mk(gy1), mk(gU1), mk(gd1)
         gy, gU, gd, gA = (torch.empty_like(U) for _ in range(4))
         ghyp = torch.empty((self.B, 4, self.H), device=self.dev)
         with torch.cuda.device(self.dev):
             _lib.check("dadmm_gnn_step_backward_ex", self.L.dadmm_gnn_step_backward_ex(
                 ctypes.byref(self.d), k, _ptr(g.vptr), _ptr(g.vq), _ptr(g.deg), _ptr(hyp_k),
                 _ptr(y_k), _ptr(AtAy), _ptr(self.Atb), _ptr(U), _ptr(D), _ptr(gy1), _ptr(gU1),
-                _ptr(gd1), _ptr(gy), _ptr(gU), _ptr(gd), _ptr(gA), _ptr(ghyp), _ptr(gy_add),
+                _ptr(gd1), _ptr(gy), _ptr(gU), _ptr(gd), _ptr(gA), _ptr(ghyp),
                 None if head is None else ctypes.byref(head), _stream(self.dev)))
         return gy, gU, gd, gA, ghyp
 
@@ -240,22 +244,21 @@ class GnnTrainFn(torch.autograd.Function):
         with torch.cuda.device(dev):
             for k in range(K - 1, -1, -1):
                 hyp_k = plan.hyp(ctx.arena, k)
-                # in the step adjoint's epilogue: + the loss's gradient on y_k (gY[k - 1]), and the
-                # head's backward (d logits into the iteration's dsave block, ghyp_last added first)
+                # in the step adjoint's epilogue: the head's backward (d logits into the
+                # iteration's dsave block, ghyp_last added first)
                 head.z = ctx.svs[k].z
                 head.ghyp_add = ghyp_last.data_ptr() if (k == K - 1 and ghyp_last is not None) else None
                 head.dz = dsave.data_ptr() + 4 * k * plan.dsave_per
                 gy, gU, gd, gA, ghyp = run.step_backward(k, run.ys[k], ctx.As[k], hyp_k, ctx.Us[k], ctx.Ds[k],
-                                                         gy1, gU1, gd1,
-                                                         gy_add=gY[k - 1] if (gY is not None and k > 0) else None,
-                                                         head=head)
+                                                         gy1, gU1, gd1, head=head)
                 # gA += d AtAy from the hypernetwork (in its last linear's epilogue); at k = 0 the
                 # sum is not used (y_0, U_0, delta_0 are the random inits: no gradient)
                 plan.backward_deferred(ctx.As[k], run.Atb, ctx.a_hat, ctx.per_sample, ctx.seeds[k],
                                        ctx.svs[k], None, g, dsave, k, stream, acc=gA, dz_ready=True)
                 if k == 0:
                     break
-                run.gram_acc(gA, gy)
+                # gy += A^T A gA, then + the loss's own gradient on y_k (gY[k - 1]), one launch
+                run.gram_acc(gA, gy, addend=gY[k - 1] if gY is not None else None)
                 gy1, gU1, gd1 = gy, gU, gd
             plan.wgrad(K, ctx.As, run.Atb, ctx.arena, dsave, g, stream)
         ctx.arena = ctx.svs = ctx.As = ctx.Us = ctx.Ds = None

@@ -300,8 +300,11 @@ int dadmm_gnn_begin(const dadmm_dims* d, const void* op, const float* b, const f
 int dadmm_gnn_gram(const dadmm_dims* d, const void* op, int32_t k, float* const* yptr,
                    const int32_t* flags, const float* x, float* out, void* stream);
 /* out += A^T (A x) (ABI 15): the GNN adjoint's y gradient picks up the gram of the AtAy gradient
- * in one launch instead of a gram and an add (bit-identical: out + the gram's value, one rounding). */
-int dadmm_gnn_gram_acc(const dadmm_dims* d, const void* op, const float* x, float* out, void* stream);
+ * in one launch instead of a gram and an add (bit-identical: out + the gram's value, one rounding).
+ * ABI 17: then out += addend [B][P][n] (nullable; 16-byte aligned) in the same epilogue — the
+ * loss's own gradient on y_k, (out + gram) + addend, the bits of a separate add after. */
+int dadmm_gnn_gram_acc(const dadmm_dims* d, const void* op, const float* x, float* out, const float* addend,
+                       void* stream);
 /* One iteration: reads y_k (resolved), U_k (U, reset by the guard), delta_k (D), AtAy_k, Atb and
  * hyp_k [B][4][H]; writes y_{k+1} to yptr[k+1], U_{k+1} to U_next, delta_{k+1} to D_next.
  * G: [B][P][n] scratch. */
@@ -321,12 +324,11 @@ int dadmm_gnn_step_backward(const dadmm_dims* d, int32_t k, const int32_t* visit
                             float* gy, float* gU, float* gd, float* gAtAy, float* ghyp,
                             void* stream);
 /* dadmm_gnn_step_backward_ex (ABI 17): dadmm_gnn_step_backward with the training backward's next
- * two element-wise steps in its epilogue (one launch each saved per iteration):
- *   gy_add (nullable): gy = (direct dL/dy_k) + gy_add — the loss's own gradient on y_k;
+ * element-wise step in its epilogue (the add and the head's launch saved per iteration):
  *   head (nullable): dL/dhyp_k += head->ghyp_add (nullable), then the hyper-parameter head's
  *     backward (dadmm_hyper_head_act mode 1 on the logits head->z [B][4H], bit-identical) into
  *     head->dz [B][4H], the gradient dadmm_hyper_train_backward_deferred takes with flag bit 1.
- * Replaces the step's adjoint + the adds + the head's derivative of
+ * Replaces the step's adjoint + the add + the head's derivative of
  * gnn_dlasso_models_progressive.py:165-237 under torch's backward. */
 typedef struct dadmm_head_bwd {
     const float* z;         /* [B][4H] logits (dadmm_hyper_saved.z) */
@@ -339,7 +341,7 @@ int dadmm_gnn_step_backward_ex(const dadmm_dims* d, int32_t k, const int32_t* vi
                                const float* y_k, const float* AtAy, const float* Atb, const float* U,
                                const float* D, const float* gy1, const float* gU1, const float* gd1,
                                float* gy, float* gU, float* gd, float* gAtAy, float* ghyp,
-                               const float* gy_add, const dadmm_head_bwd* head, void* stream);
+                               const dadmm_head_bwd* head, void* stream);
 
 /* ---- the drivers' loss, fused ----------------------------------------------------------------
  * gnn_dlasso_utils.compute_loss (gnn_dlasso_utils.py:27-88) on the iterates Y [K][B*P][n_store]

@@ -242,7 +242,8 @@ def test_features_are_the_reference_gram_and_atb(cuda):
 @pytest.mark.parametrize("P,m,n,B", [(4, 24, 48, 10), (16, 32, 256, 96), (50, 32, 1024, 40)])
 def test_gram_acc_equals_gram_plus_add(cuda, P, m, n, B):
     """dadmm_gnn_gram_acc (out += A^T A x, the adjoint's one-launch accumulation) == out + the
-    gram of x, bit for bit, on the item kernel and the LDS-resident gram."""
+    gram of x, bit for bit, on the item kernel and the LDS-resident gram; with an addend, the bits
+    of a separate add after."""
     from dadmm_hip import _lib
     from dadmm_hip.gnn_ops import GnnRun
     from dadmm_hip.graph import ingest
@@ -259,6 +260,11 @@ def test_gram_acc_equals_gram_plus_add(cuda, P, m, n, B):
     want = out0 + run.gram(0, x=xin)
     got = run.gram_acc(xin, out0.clone())
     assert torch.equal(got[..., :n], want[..., :n])
+    # with the addend (ABI 17: the training backward's loss gradient on y_k): (out + gram) + addend
+    add = torch.zeros(B, P, ns, device=cuda)
+    add[..., :n] = torch.randn(B, P, n, device=cuda, generator=g)
+    got = run.gram_acc(xin, out0.clone(), addend=add)
+    assert torch.equal(got[..., :n], (want + add)[..., :n])
 
 
 @pytest.mark.parametrize("mode,n,directed", [("diff", 32, False), ("same", 32, False),
