@@ -69,9 +69,11 @@ __device__ __forceinline__ uint32_t fresh_s(uint32_t x) {
 constexpr int WAVES = DADMM_BWD_WAVES;
 static_assert(WAVES == 8 || WAVES == 4, "adjoint workgroup: 4 or 8 waves");
 // GEMM2's A^T operand through a per-wave LDS ring filled by LDS-DMA, as in the forward
-// (dadmm_fused.hip): BWD_QD quarter-chains of 1 KB per wave, BWD_QD - 1 in flight
+// (dadmm_fused.hip): BWD_QD quarter-chains of 1 KB per wave, BWD_QD - 1 in flight. The 4-wave form
+// reads it straight from L2 instead (its loads sit in the 512-register budget): 1.19-1.21 vs
+// 1.22-1.23 ms at H (profiles/r05/adjoint_variants_r05p.txt)
 #ifndef DADMM_BWD_AT_DMA
-#define DADMM_BWD_AT_DMA 1
+#define DADMM_BWD_AT_DMA (DADMM_BWD_WAVES == 4 ? 0 : 1)
 #endif
 constexpr int BWD_QD = 5;
 // DADMM_BWD_ROT=1: the elementwise phase walks the wave's T2 row tiles in a runtime loop and
