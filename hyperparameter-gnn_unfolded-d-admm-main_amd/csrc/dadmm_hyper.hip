@@ -71,6 +71,9 @@ __device__ __forceinline__ void mem_fence() { __builtin_amdgcn_sched_barrier(0);
 #ifndef DADMM_HYPER_DQ
 #define DADMM_HYPER_DQ 4
 #endif
+#ifndef DADMM_HYPER_D1
+#define DADMM_HYPER_D1 4
+#endif
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, size_t bytes) {
@@ -121,7 +124,9 @@ __device__ __forceinline__ int xcd_tile(int bid, int G) {
 // has no masks; a K tail that is not a multiple of 16 runs as one masked step.
 template <int WR, int EPI, bool SPLIT, bool DMA>
 __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
-    [[maybe_unused]] constexpr int D = WR >= 5 ? 3 : 4;   // register ring depth (k-steps in flight; 2 waves/SIMD)
+    // register ring depth (k-steps in flight; 2 waves/SIMD); DADMM_HYPER_D1: the depth of the
+    // one-row-block tiles (small batches: one workgroup per CU, latency-bound K loops)
+    [[maybe_unused]] constexpr int D = WR >= 5 ? 3 : (WR == 1 ? DADMM_HYPER_D1 : 4);
     constexpr int TM = 32 * WR;                    // rows per workgroup tile
     extern __shared__ __attribute__((aligned(16))) float zt[];   // GCN epilogue (dynamic)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

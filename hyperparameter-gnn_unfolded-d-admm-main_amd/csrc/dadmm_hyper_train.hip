@@ -348,15 +348,30 @@ __global__ __launch_bounds__(256) void bn_running_part_kernel(BnRunArgs a) {
     const double uf = (double)a.P / (double)(a.P - 1);
     double sm = 0.0, sv = 0.0;
     if (cc < N) {
+        // the wave's rows t0 + wv, + 4, ...: their offsets first, then the loads in groups of 8 in
+        // flight, then the sums in row order (the same order as one row at a time)
         int k = t0 / a.B, b = t0 - k * a.B + wv;
         while (b >= a.B) { b -= a.B; ++k; }
-        for (int t = t0 + wv; t < t1; t += 4) {
-            const size_t o = (size_t)k * a.block_stride + (size_t)b * N + cc;
-            const double wt = a.w[t];
-            sm += wt * (double)mean[o];
-            sv += wt * ((double)var[o] * uf);
-            b += 4;
-            while (b >= a.B) { b -= a.B; ++k; }
+        for (int t = t0 + wv; t < t1; t += 32) {
+            float mv[8], vv[8];
+            double wt[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const bool in = t + 4 * u < t1;
+                const size_t o = (size_t)k * a.block_stride + (size_t)b * N + cc;
+                mv[u] = in ? mean[o] : 0.0f;
+                vv[u] = in ? var[o] : 0.0f;
+                wt[u] = in ? a.w[t + 4 * u] : 0.0;
+                b += 4;
+                while (b >= a.B) { b -= a.B; ++k; }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (t + 4 * u < t1) {
+                    sm += wt[u] * (double)mv[u];
+                    sv += wt[u] * ((double)vv[u] * uf);
+                }
+            }
         }
     }
     red[wv][0][lane] = sm;

@@ -41,8 +41,10 @@ class GnnRun:
         else:
             self.Y = torch.empty((K, B, P, ns), device=dev)
             self.ys = [self.y0] + list(self.Y.unbind(0))
-        self.yptr = torch.tensor([t.data_ptr() for t in self.ys], dtype=torch.int64).to(
-            dev, non_blocking=False)
+        # from pinned memory, asynchronously: a pageable copy would make the host wait for the
+        # stream to drain (the previous train step's backward) before enqueueing this forward
+        self.yptr = torch.tensor([t.data_ptr() for t in self.ys], dtype=torch.int64,
+                                 pin_memory=True).to(dev, non_blocking=True)
         self.flags = torch.empty(max(self.L.dadmm_gnn_flag_bytes(K) // 4, 1), dtype=torch.int32,
                                  device=dev)
         self.Atb = torch.empty((B, P, ns), device=dev)
@@ -119,13 +121,27 @@ class GnnRun:
         return gy, gU, gd, gA, ghyp
 
 
+def _stage_status(run: GnnRun):
+    """After the forward's finish: the status word copied to pinned host memory behind an event,
+    so that the backward can read it without draining the stream (_check_guards)."""
+    run.status_host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+    run.status_host.copy_(run.status, non_blocking=True)
+    run.status_event = torch.cuda.Event()
+    run.status_event.record()
+
+
 def _check_guards(run: GnnRun):
-    """Once per backward pass (one host sync): the adjoint assumes no guard fired."""
+    """Once per backward pass: the adjoint assumes no guard fired. With a staged status word
+    (_stage_status) this waits only for the forward; else one host sync."""
     if getattr(run, "_checked", False):
         return
     # (any adjacency: the step adjoint applies compute_delta through the forward's visit lists,
     # and that map is symmetric for directed graphs too; oracle.laplacians)
-    st = int(run.status.item())
+    if getattr(run, "status_event", None) is not None:
+        run.status_event.synchronize()
+        st = int(run.status_host[0])
+    else:
+        st = int(run.status.item())
     run._checked = True
     if st:
         from .autograd import GuardAdjointError
@@ -209,6 +225,7 @@ class GnnTrainFn(torch.autograd.Function):
                 Us.append(U)
                 Ds.append(D)
         run.finish()
+        _stage_status(run)
         if plan.train:   # eval mode (a backward through model.eval()): running statistics are inputs
             with torch.cuda.device(dev):
                 plan.update_running_stats(arena, K, hyper_ops._stream(dev))
@@ -225,7 +242,6 @@ class GnnTrainFn(torch.autograd.Function):
             raise RuntimeError("GnnTrainFn: a second backward through the same training forward "
                                "(retain_graph=True) is not supported; its saved activations were "
                                "released by the first backward")
-        _check_guards(run)
         K, dev = run.K, run.dev
         stream = _stream(dev)
         # this node's own accumulator: its sums are returned to autograd below
@@ -262,6 +278,10 @@ class GnnTrainFn(torch.autograd.Function):
                 gy1, gU1, gd1 = gy, gU, gd
             plan.wgrad(K, ctx.As, run.Atb, ctx.arena, dsave, g, stream)
         ctx.arena = ctx.svs = ctx.As = ctx.Us = ctx.Ds = None
+        # the guard check after the enqueue (the forward's status, staged behind an event, is
+        # ready by now in the common case: no stall between the forward and this backward); if a
+        # guard fired the gradients just computed are discarded with the error
+        _check_guards(run)
         grads = tuple(acc.view(p) if p.requires_grad else None for p in ctx.params)
         ctx.params = None
         return (None,) * 6 + grads

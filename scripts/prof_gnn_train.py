@@ -45,9 +45,10 @@ if os.environ.get("CPROF"):   # host-side profile of the timed steps
 t0 = time.perf_counter()
 for _ in range(steps):
     step()
+t_enq = time.perf_counter()   # the host's enqueue time (the GPU may still be running)
 torch.cuda.synchronize()
 if os.environ.get("CPROF"):
     pr.disable()
     pstats.Stats(pr).sort_stats("tottime").print_stats(35)
 print(f"B={B} K={K} P={P} m={m} n={n}: {1e3 * (time.perf_counter() - t0) / steps:.2f} ms per train step "
-      f"(graphs pre-ingested, backend {gnn.last_backend})")
+      f"(graphs pre-ingested, backend {gnn.last_backend}; host enqueue {1e3 * (t_enq - t0) / steps:.2f} ms)")

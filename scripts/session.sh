@@ -2,6 +2,7 @@
 # One GPU session: each step under its own time limit, chained with &&; the first failure ends
 # the session (no retries). Output under gpurun_out/$TAG/.
 #   TAG=name STEPS="tests:<pytest args> | ab | prologue | bench:<args> | prof:<bench args> | cmd:<shell>" bash scripts/session.sh
+# (steps are split on "|": a cmd step must not contain one — chain with && instead)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp

@@ -594,3 +594,25 @@ def test_fused_gcn_backward_bit_identical(cuda, monkeypatch, P, n, hidden, B, pe
         out[fuse] = (per_call, [p.grad.clone() for p in model.parameters()])
     for got, want in zip(out["1"][0] + out["1"][1], out["0"][0] + out["0"][1]):
         assert torch.equal(got, want), (got - want).abs().max()
+
+
+def test_whole_forward_node_guard_raises_in_backward(cuda):
+    """A guard that fired in the training forward (a NaN in y0) makes the whole-forward node's
+    backward raise GuardAdjointError (the status word is staged behind an event in the forward
+    and checked after the backward's enqueue), and no parameter gradient is delivered."""
+    import gnn_dlasso_utils as U
+    from dadmm_hip.autograd import GuardAdjointError
+    P, n, hidden, K = 5, 32, 8, 2
+    model, ref, graphs, inits, bt, label = _train_pair(cuda, P, n, hidden, "diff", False)
+    y0 = inits[0].clone()
+    y0[3, 2, 7] = float("nan")
+    Y, _ = model(bt, graphs, K, inits=(y0, inits[1], inits[2]))
+    assert int(model.last_status.item()) & 1
+    model.zero_grad()
+    with pytest.raises(GuardAdjointError):
+        U.compute_loss(Y, label)[1].backward()
+    assert all(p.grad is None for p in model.parameters())
+    # and a clean step afterwards works
+    Y, _ = model(bt, graphs, K, inits=inits)
+    U.compute_loss(Y, label)[1].backward()
+    assert all(p.grad is not None for p in model.parameters())
