@@ -898,6 +898,12 @@ __global__ __launch_bounds__(THREADS) void finish_kernel(GnnArgs a) {
 // hyper-parameter gradients reduce over the columns: wave shuffles per chunk, accumulated per wave
 // in LDS in chunk order, then the 4 waves' sums in wave order (deterministic). (One wave per sample
 // left most CUs idle at training batch sizes: B = 256 samples filled 64 workgroups.)
+// PR > 0 (P <= PR agents): every agent's operands of the lane's column are loaded at once into
+// registers (rows past P re-read agent P - 1, never used) and kept through the four phases, so a
+// wave waits for memory once per chunk instead of once per agent and phase (the per-agent loads of
+// the loop form serialised ~10 HBM round trips: 22 us per iteration at B = 256). The same
+// operations in the same order as the loop form: bit-identical.
+template <int PR>
 __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k, GnnGrads gg) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int P = a.P, n = a.n, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -935,82 +941,182 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
     const float* __restrict__ U_r = a.U;
     const float* __restrict__ D_r = a.D;
     const float* __restrict__ ys_r = ys;
-    for (int c0 = 64 * wv; c0 < n; c0 += 64 * WAVES) {
-        const int c = c0 + lane;
-        const bool cv = c < n;
-        const size_t base = (size_t)s * P * n + (cv ? c : n - 1);
-        // recompute y_{k+1} for every agent of this column
-#pragma unroll 4
-        for (int p = 0; p < P; ++p) {
-            const size_t off = base + (size_t)p * n;
-            const float y = ys_r[off];
-            const float ta = hyp_at(a, s, 1, p);
-            const float st = sign_times(y, ta);
-            float gr = AtAy_r[off] - Atb_r[off];
-            gr = gr + st;
-            gr = gr + U_r[off] * a.deg[g0 + p];
-            gr = gr + D_r[off] * hyp_at(a, s, 2, p);
-            const float g = clamp_t(gr, -gclip, gclip);
-            const float y1 = clamp_t(y - hyp_at(a, s, 0, p) * g, -vclip, vclip);
-            y1l[p * 64 + lane] = cv ? y1 : 0.0f;
-        }
-        // dual update adjoint; d_bar_raw (w.r.t. 2 L y_{k+1} before the GNN clamp)
-        for (int p = 0; p < P; ++p) {
-            const float yp = y1l[p * 64 + lane];
-            float acc = 0.0f;
-            const int t1 = vpl[p + 1];
-            for (int t = vpl[p]; t < t1; ++t) acc = acc + (yp - y1l[(int)vql[t] * 64 + lane]);
-            float dbr = 0.0f, pe = 0.0f;
-            if (cv) {
-                const size_t off = base + (size_t)p * n;
-                const float d1 = a.variant != 0 ? clamp_t(acc, -20.0f, 20.0f) : acc;
-                const float et = hyp_at(a, s, 3, p);
-                const float wvv = a.U[off] + d1 * et;
-                const float wb = (gg.gU1 != nullptr && inside(wvv, -vclip, vclip)) ? gg.gU1[off] : 0.0f;
-                pe = wb * d1;
-                const float db = (gg.gd1 != nullptr ? gg.gd1[off] : 0.0f) + wb * et;
-                dbr = (a.variant == 0 || inside(acc, -20.0f, 20.0f)) ? db : 0.0f;
-                gg.gU[off] = wb;
+    if constexpr (PR > 0) {
+        for (int c0 = 64 * wv; c0 < n; c0 += 64 * WAVES) {
+            const int c = c0 + lane;
+            const bool cv = c < n;
+            const size_t base = (size_t)s * P * n + (cv ? c : n - 1);
+            float ry[PR], rA[PR], rB[PR], rU[PR], rD[PR], rgy1[PR], rgU1[PR], rgd1[PR], rwb[PR];
+#pragma unroll
+            for (int p = 0; p < PR; ++p) {
+                const size_t off = base + (size_t)(p < P ? p : P - 1) * n;
+                ry[p] = ys_r[off];
+                rA[p] = AtAy_r[off];
+                rB[p] = Atb_r[off];
+                rU[p] = U_r[off];
+                rD[p] = D_r[off];
+                rgy1[p] = gg.gy1 != nullptr ? gg.gy1[off] : 0.0f;
+                rgU1[p] = gg.gU1 != nullptr ? gg.gU1[off] : 0.0f;
+                rgd1[p] = gg.gd1 != nullptr ? gg.gd1[off] : 0.0f;
             }
-            accum(3, p, pe);
-            dbl[p * 64 + lane] = dbr;
-        }
-        for (int p = 0; p < P; ++p) {   // 2 L d_bar_raw, same visit lists (the map is symmetric)
-            const float xp = dbl[p * 64 + lane];
-            float acc = 0.0f;
-            const int t1 = vpl[p + 1];
-            for (int t = vpl[p]; t < t1; ++t) acc = acc + (xp - dbl[(int)vql[t] * 64 + lane]);
-            ybl[p * 64 + lane] = acc;
-        }
-        // primal update + gradient clamp adjoint
-        for (int p = 0; p < P; ++p) {
-            float pa = 0.0f, pt = 0.0f, pr = 0.0f;
-            if (cv) {
-                const size_t off = base + (size_t)p * n;
-                const float al = hyp_at(a, s, 0, p), ta = hyp_at(a, s, 1, p), rh = hyp_at(a, s, 2, p);
-                const float y = ys[off];
-                const float sg = sign_times(y, 1.0f);
+            // recompute y_{k+1} for every agent of this column
+#pragma unroll
+            for (int p = 0; p < PR; ++p) {
+                if (p >= P) break;
+                const float y = ry[p];
+                const float ta = hyp_at(a, s, 1, p);
                 const float st = sign_times(y, ta);
-                float gr = a.AtAy[off] - a.Atb[off];
+                float gr = rA[p] - rB[p];
                 gr = gr + st;
-                gr = gr + a.U[off] * a.deg[g0 + p];
-                gr = gr + a.D[off] * rh;
+                gr = gr + rU[p] * a.deg[g0 + p];
+                gr = gr + rD[p] * hyp_at(a, s, 2, p);
                 const float g = clamp_t(gr, -gclip, gclip);
-                const float z = y - al * g;
-                const float yb = (gg.gy1 != nullptr ? gg.gy1[off] : 0.0f) + ybl[p * 64 + lane];
-                const float zb = inside(z, -vclip, vclip) ? yb : 0.0f;
-                pa = -zb * g;
-                const float grb = inside(gr, -gclip, gclip) ? -al * zb : 0.0f;
-                pt = grb * sg;
-                pr = grb * a.D[off];
-                gg.gy[off] = zb;
-                gg.gU[off] = gg.gU[off] + grb * a.deg[g0 + p];
-                gg.gd[off] = grb * rh;
-                gg.gAtAy[off] = grb;
+                const float y1 = clamp_t(y - hyp_at(a, s, 0, p) * g, -vclip, vclip);
+                y1l[p * 64 + lane] = cv ? y1 : 0.0f;
             }
-            accum(0, p, pa);
-            accum(1, p, pt);
-            accum(2, p, pr);
+            // dual update adjoint; d_bar_raw (w.r.t. 2 L y_{k+1} before the GNN clamp)
+#pragma unroll
+            for (int p = 0; p < PR; ++p) {
+                if (p >= P) break;
+                const float yp = y1l[p * 64 + lane];
+                float acc = 0.0f;
+                const int t1 = vpl[p + 1];
+                for (int t = vpl[p]; t < t1; ++t) acc = acc + (yp - y1l[(int)vql[t] * 64 + lane]);
+                float dbr = 0.0f, pe = 0.0f;
+                rwb[p] = 0.0f;
+                if (cv) {
+                    const float d1 = a.variant != 0 ? clamp_t(acc, -20.0f, 20.0f) : acc;
+                    const float et = hyp_at(a, s, 3, p);
+                    const float wvv = rU[p] + d1 * et;
+                    const float wb = (gg.gU1 != nullptr && inside(wvv, -vclip, vclip)) ? rgU1[p] : 0.0f;
+                    pe = wb * d1;
+                    const float db = (gg.gd1 != nullptr ? rgd1[p] : 0.0f) + wb * et;
+                    dbr = (a.variant == 0 || inside(acc, -20.0f, 20.0f)) ? db : 0.0f;
+                    rwb[p] = wb;
+                }
+                accum(3, p, pe);
+                dbl[p * 64 + lane] = dbr;
+            }
+#pragma unroll
+            for (int p = 0; p < PR; ++p) {   // 2 L d_bar_raw, same visit lists (the map is symmetric)
+                if (p >= P) break;
+                const float xp = dbl[p * 64 + lane];
+                float acc = 0.0f;
+                const int t1 = vpl[p + 1];
+                for (int t = vpl[p]; t < t1; ++t) acc = acc + (xp - dbl[(int)vql[t] * 64 + lane]);
+                ybl[p * 64 + lane] = acc;
+            }
+            // primal update + gradient clamp adjoint
+#pragma unroll
+            for (int p = 0; p < PR; ++p) {
+                if (p >= P) break;
+                float pa = 0.0f, pt = 0.0f, pr = 0.0f;
+                if (cv) {
+                    const size_t off = base + (size_t)p * n;
+                    const float al = hyp_at(a, s, 0, p), ta = hyp_at(a, s, 1, p), rh = hyp_at(a, s, 2, p);
+                    const float y = ry[p];
+                    const float sg = sign_times(y, 1.0f);
+                    const float st = sign_times(y, ta);
+                    float gr = rA[p] - rB[p];
+                    gr = gr + st;
+                    gr = gr + rU[p] * a.deg[g0 + p];
+                    gr = gr + rD[p] * rh;
+                    const float g = clamp_t(gr, -gclip, gclip);
+                    const float z = y - al * g;
+                    const float yb = (gg.gy1 != nullptr ? rgy1[p] : 0.0f) + ybl[p * 64 + lane];
+                    const float zb = inside(z, -vclip, vclip) ? yb : 0.0f;
+                    pa = -zb * g;
+                    const float grb = inside(gr, -gclip, gclip) ? -al * zb : 0.0f;
+                    pt = grb * sg;
+                    pr = grb * rD[p];
+                    gg.gy[off] = zb;
+                    gg.gU[off] = rwb[p] + grb * a.deg[g0 + p];
+                    gg.gd[off] = grb * rh;
+                    gg.gAtAy[off] = grb;
+                }
+                accum(0, p, pa);
+                accum(1, p, pt);
+                accum(2, p, pr);
+            }
+        }
+    } else {
+        for (int c0 = 64 * wv; c0 < n; c0 += 64 * WAVES) {
+            const int c = c0 + lane;
+            const bool cv = c < n;
+            const size_t base = (size_t)s * P * n + (cv ? c : n - 1);
+            // recompute y_{k+1} for every agent of this column
+    #pragma unroll 4
+            for (int p = 0; p < P; ++p) {
+                const size_t off = base + (size_t)p * n;
+                const float y = ys_r[off];
+                const float ta = hyp_at(a, s, 1, p);
+                const float st = sign_times(y, ta);
+                float gr = AtAy_r[off] - Atb_r[off];
+                gr = gr + st;
+                gr = gr + U_r[off] * a.deg[g0 + p];
+                gr = gr + D_r[off] * hyp_at(a, s, 2, p);
+                const float g = clamp_t(gr, -gclip, gclip);
+                const float y1 = clamp_t(y - hyp_at(a, s, 0, p) * g, -vclip, vclip);
+                y1l[p * 64 + lane] = cv ? y1 : 0.0f;
+            }
+            // dual update adjoint; d_bar_raw (w.r.t. 2 L y_{k+1} before the GNN clamp)
+            for (int p = 0; p < P; ++p) {
+                const float yp = y1l[p * 64 + lane];
+                float acc = 0.0f;
+                const int t1 = vpl[p + 1];
+                for (int t = vpl[p]; t < t1; ++t) acc = acc + (yp - y1l[(int)vql[t] * 64 + lane]);
+                float dbr = 0.0f, pe = 0.0f;
+                if (cv) {
+                    const size_t off = base + (size_t)p * n;
+                    const float d1 = a.variant != 0 ? clamp_t(acc, -20.0f, 20.0f) : acc;
+                    const float et = hyp_at(a, s, 3, p);
+                    const float wvv = a.U[off] + d1 * et;
+                    const float wb = (gg.gU1 != nullptr && inside(wvv, -vclip, vclip)) ? gg.gU1[off] : 0.0f;
+                    pe = wb * d1;
+                    const float db = (gg.gd1 != nullptr ? gg.gd1[off] : 0.0f) + wb * et;
+                    dbr = (a.variant == 0 || inside(acc, -20.0f, 20.0f)) ? db : 0.0f;
+                    gg.gU[off] = wb;
+                }
+                accum(3, p, pe);
+                dbl[p * 64 + lane] = dbr;
+            }
+            for (int p = 0; p < P; ++p) {   // 2 L d_bar_raw, same visit lists (the map is symmetric)
+                const float xp = dbl[p * 64 + lane];
+                float acc = 0.0f;
+                const int t1 = vpl[p + 1];
+                for (int t = vpl[p]; t < t1; ++t) acc = acc + (xp - dbl[(int)vql[t] * 64 + lane]);
+                ybl[p * 64 + lane] = acc;
+            }
+            // primal update + gradient clamp adjoint
+            for (int p = 0; p < P; ++p) {
+                float pa = 0.0f, pt = 0.0f, pr = 0.0f;
+                if (cv) {
+                    const size_t off = base + (size_t)p * n;
+                    const float al = hyp_at(a, s, 0, p), ta = hyp_at(a, s, 1, p), rh = hyp_at(a, s, 2, p);
+                    const float y = ys[off];
+                    const float sg = sign_times(y, 1.0f);
+                    const float st = sign_times(y, ta);
+                    float gr = a.AtAy[off] - a.Atb[off];
+                    gr = gr + st;
+                    gr = gr + a.U[off] * a.deg[g0 + p];
+                    gr = gr + a.D[off] * rh;
+                    const float g = clamp_t(gr, -gclip, gclip);
+                    const float z = y - al * g;
+                    const float yb = (gg.gy1 != nullptr ? gg.gy1[off] : 0.0f) + ybl[p * 64 + lane];
+                    const float zb = inside(z, -vclip, vclip) ? yb : 0.0f;
+                    pa = -zb * g;
+                    const float grb = inside(gr, -gclip, gclip) ? -al * zb : 0.0f;
+                    pt = grb * sg;
+                    pr = grb * a.D[off];
+                    gg.gy[off] = zb;
+                    gg.gU[off] = gg.gU[off] + grb * a.deg[g0 + p];
+                    gg.gd[off] = grb * rh;
+                    gg.gAtAy[off] = grb;
+                }
+                accum(0, p, pa);
+                accum(1, p, pt);
+                accum(2, p, pr);
+            }
         }
     }
     __syncthreads();
@@ -1150,12 +1256,15 @@ hipError_t gnn_launch_step_backward(const GnnArgs& a, int k, const GnnGrads& gg,
     const size_t lds = 4 * (size_t)gnn::WAVES * (3 * a.P * 64 + 4 * a.P + (a.P + 1) + (2 * a.P * a.P + 3) / 4);
     if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)gnn::step_backward_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
+        for (const void* f : {(const void*)gnn::step_backward_kernel<8>, (const void*)gnn::step_backward_kernel<0>}) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
     }
-    hipLaunchKernelGGL(gnn::step_backward_kernel, dim3(a.B),
-                       dim3(gnn::THREADS), lds, st, a, k, gg);
+    if (a.P <= 8)
+        hipLaunchKernelGGL(gnn::step_backward_kernel<8>, dim3(a.B), dim3(gnn::THREADS), lds, st, a, k, gg);
+    else
+        hipLaunchKernelGGL(gnn::step_backward_kernel<0>, dim3(a.B), dim3(gnn::THREADS), lds, st, a, k, gg);
     return hipGetLastError();
 }
 
