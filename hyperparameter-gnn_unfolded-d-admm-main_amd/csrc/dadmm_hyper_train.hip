@@ -399,9 +399,20 @@ __global__ __launch_bounds__(256) void bn_running_finish_kernel(BnRunArgs a) {
         if (i < a.layers && c >= a.col0[i]) L = i;
     const int cc = c - bn_pick(a.col0, L);
     double m = 0.0, v = 0.0;
-    for (int sp = 0; sp < a.splits; ++sp) {
-        m += a.part[((size_t)sp * 2) * total + c];
-        v += a.part[((size_t)sp * 2 + 1) * total + c];
+    for (int sp0 = 0; sp0 < a.splits; sp0 += 8) {   // 8 splits' loads in flight, added in order
+        double pm[8], pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int sp = sp0 + u < a.splits ? sp0 + u : a.splits - 1;
+            pm[u] = a.part[((size_t)sp * 2) * total + c];
+            pv[u] = a.part[((size_t)sp * 2 + 1) * total + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (sp0 + u < a.splits) {
+                m += pm[u];
+                v += pv[u];
+            }
     }
     float* rm = bn_pick(a.rmean, L);
     float* rv = bn_pick(a.rvar, L);

@@ -257,8 +257,8 @@ def test_bn_running_update_validation(L):
     vp = ctypes.c_void_p * 2
     ptrs = lambda o: vp(*[0x10000 + 256 * (o + i) for i in range(2)])   # noqa: E731
     assert L.dadmm_hyper_bn_running_scratch_bytes(2, W, 1, 32) == 8 * 2 * 80 * 1        # one split
-    assert L.dadmm_hyper_bn_running_scratch_bytes(2, W, 25, 256) == 8 * 2 * 80 * 25     # 256 rows each
-    assert L.dadmm_hyper_bn_running_scratch_bytes(2, W, 25, 4096) == 8 * 2 * 80 * 128   # capped
+    assert L.dadmm_hyper_bn_running_scratch_bytes(2, W, 25, 256) == 8 * 2 * 80 * 100    # 64 rows each
+    assert L.dadmm_hyper_bn_running_scratch_bytes(2, W, 25, 4096) == 8 * 2 * 80 * 256   # capped
     assert L.dadmm_hyper_bn_running_scratch_bytes(9, W, 1, 1) == 0
 
     def call(layers=2, widths=W, block=32 * 256 + 48 * 256, iters=25, B=256, P=5, scratch=_fk(9), rm=None):
