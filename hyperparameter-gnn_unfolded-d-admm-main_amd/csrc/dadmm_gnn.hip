@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "dadmm_internal.h"
 
 namespace dadmm {
@@ -56,6 +58,14 @@ constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
 // gram_kernel mode 2: the out rows prefetched one GEMM2 unit ahead
 #ifndef DADMM_GRAM_OPF
 #define DADMM_GRAM_OPF 1
+#endif
+// gram_kernel (round 5): GEMM1's ring 8 deep where the column steps divide, and a wave's whole
+// GEMM2 (<= 4 units) loaded at once
+#ifndef DADMM_GRAM_GD8
+#define DADMM_GRAM_GD8 1
+#endif
+#ifndef DADMM_GRAM_G2ALL
+#define DADMM_GRAM_G2ALL 1
 #endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
@@ -228,25 +238,33 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
                     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                         rx, 16 * t + 4 * h < n && sv ? xoff + 64u * t : 0x80000000u, 0, 0));
                 };
-                constexpr int GD = 4;
                 const int T = NP / 16;
-                f32x4 ar[GD], xr[GD];
-#pragma unroll
-                for (int u = 0; u < GD; ++u) {
-                    ar[u] = *(const f32x4*)(arow + 16 * u);
-                    xr[u] = ldx(u);
-                }
-                for (int t0 = 0; t0 < T; t0 += GD) {
+                // ring depth 8 where the steps divide (round 5: half the exposed round trips of the
+                // latency-bound small-batch grams), else 4; the chain is the same either way
+                auto gemm1 = [&](auto gd) {
+                    constexpr int GD = decltype(gd)::value;
+                    f32x4 ar[GD], xr[GD];
 #pragma unroll
                     for (int u = 0; u < GD; ++u) {
+                        ar[u] = *(const f32x4*)(arow + 16 * u);
+                        xr[u] = ldx(u);
+                    }
+                    for (int t0 = 0; t0 < T; t0 += GD) {
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) acc = mfma4(ar[u][r], xr[u][r], acc);
-                        if (t0 + GD + u < T) {
-                            ar[u] = *(const f32x4*)(arow + 16 * (t0 + GD + u));
-                            xr[u] = ldx(t0 + GD + u);
+                        for (int u = 0; u < GD; ++u) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) acc = mfma4(ar[u][r], xr[u][r], acc);
+                            if (t0 + GD + u < T) {
+                                ar[u] = *(const f32x4*)(arow + 16 * (t0 + GD + u));
+                                xr[u] = ldx(t0 + GD + u);
+                            }
                         }
                     }
-                }
+                };
+                if (DADMM_GRAM_GD8 && T % 8 == 0)
+                    gemm1(std::integral_constant<int, 8>{});
+                else
+                    gemm1(std::integral_constant<int, 4>{});
             }
             *(f32x4*)(Rlds + j * RS + 16 * mq + 4 * h) = acc;
         }
@@ -281,6 +299,39 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
             if (4 * mg + t < mbk) dst[t] = *(const f32x4*)(atb + (size_t)16 * nb * MP + 64 * mg + 16 * t);
     };
     const int units = (NP / 16 - w + WAVES - 1) / WAVES * MG;
+    if (DADMM_GRAM_G2ALL && MG == 1 && units <= 4) {
+        // (round 5) every unit's A^T rows (and mode 2's out rows) loaded at once: one memory wait
+        // for the wave's whole GEMM2 instead of one per unit; the chains are the loop's below
+        f32x4 at_all[4][4], oall[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u < units) {
+                load_at(at_all[u], u);
+                const int n0 = 16 * (w + WAVES * u) + 4 * h;
+                const bool st = sv && n0 < n;
+                oall[u] = (mode == 2 && st) ? *(const f32x4*)(out + ((size_t)s * P + p) * n + n0)
+                                            : (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+            }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (u >= units) break;
+            f32x4 g = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (t < mbk) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) g = mfma4(at_all[u][t][r], rv0[t][r], g);
+                }
+            }
+            const int n0 = 16 * (w + WAVES * u) + 4 * h;
+            if (sv && n0 < n) {
+                f32x4 v = mode == 2 ? oall[u] + g : g;
+                if (mode == 2 && a.acc_add != nullptr) v = v + *(const f32x4*)(a.acc_add + ((size_t)s * P + p) * n + n0);
+                *(f32x4*)(out + ((size_t)s * P + p) * n + n0) = v;
+            }
+        }
+        return;
+    }
     if (units > 0) load_at(at_cur, 0);
     f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
     // mode 2 (out += ...): the out rows of the unit that completes a tile are loaded one unit
