@@ -147,6 +147,48 @@ bool gcn_bwd_fused(int B, int P, int Kin) {
     return tiles < 480;
 }
 
+// The decoder tail (blocks 2, 3, fc, head) as one launch each way (dadmm_hyper_tail.hip), where
+// its results are the separate launches' bits: the separate path would not split K of blocks 2 and 3
+// (dadmm_hyper_linear_ln_train's split-K), and the tiles fit LDS. DADMM_HYPER_TAIL=0: the separate
+// launches (A/B timing, the bit-identity test).
+bool tail_usable(const dadmm_hyper_net* net, int B) {
+    const char* e = getenv("DADMM_HYPER_TAIL");
+    if (e != nullptr && e[0] == '0') return false;
+    for (int j = 0; j < 3; ++j)
+        if (net->dec_width[j] > 2048) return false;
+    if (dadmm::hyper_linear_splits(B, net->dec_width[0], net->dec_width[1]) != 1 ||
+        dadmm::hyper_linear_splits(B, net->dec_width[1], net->dec_width[2]) != 1)
+        return false;
+    dadmm::TailArgs t{};
+    t.H = net->H;
+    for (int j = 0; j < 3; ++j) t.D[j] = net->dec_width[j];
+    return dadmm::tail_lds_bytes(t, true) <= 160 * 1024;
+}
+
+dadmm::TailArgs tail_args(const dadmm_hyper_net* net, int B, uint64_t seed) {
+    dadmm::TailArgs t{};
+    t.B = B;
+    t.H = net->H;
+    for (int j = 0; j < 3; ++j) t.D[j] = net->dec_width[j];
+    t.W[0] = net->dec_w[1];
+    t.W[1] = net->dec_w[2];
+    t.W[2] = net->fc_w;
+    t.bias[0] = net->dec_b[1];
+    t.bias[1] = net->dec_b[2];
+    t.bias[2] = net->fc_b;
+    for (int q = 0; q < 2; ++q) {
+        t.lnw[q] = net->ln_w[1 + q];
+        t.lnb[q] = net->ln_b[1 + q];
+        t.eps[q] = net->ln_eps[1 + q];
+        t.slope[q] = net->dec_slope[1 + q];
+        t.drop[q] = net->dec_drop[1 + q];
+    }
+    t.seed = seed;
+    t.site0 = 5;   // the dropout sites of decoder blocks j are 4 + j
+    for (int c = 0; c < 4; ++c) t.maxv[c] = net->maxv[c];
+    return t;
+}
+
 #define TRY(call)                       \
     do {                                \
         const int rc_ = (call);         \
@@ -215,7 +257,8 @@ int dadmm_hyper_train_forward_ex(const dadmm_hyper_net* net, int32_t B, const fl
     TRY(dadmm_hyper_rownorm(rows, C, sv->y[4], net->norm_w, net->norm_b, net->norm_eps, 0, 0.0f, sv->e, stream));
     const float* x = sv->e;
     int width = P * C;
-    for (int j = 0; j < 3; ++j) {
+    const bool tail = tail_usable(net, B);
+    for (int j = 0; j < (tail ? 1 : 3); ++j) {
         const int N = net->dec_width[j];
         TRY(dadmm_hyper_linear_ln_train(B, width, N, x, width, net->dec_w[j], net->dec_b[j], net->ln_w[j],
                                         net->ln_b[j], net->ln_eps[j], 1, net->dec_slope[j], net->dec_drop[j],
@@ -223,7 +266,17 @@ int dadmm_hyper_train_forward_ex(const dadmm_hyper_net* net, int32_t B, const fl
         x = sv->dec_y[j];
         width = N;
     }
-    const int H4 = 4 * net->H;
+    if (tail) {   // blocks 2, 3, fc and the head in one launch
+        dadmm::TailArgs t = tail_args(net, B, seed);
+        t.x0 = sv->dec_y[0];
+        t.xd[0] = sv->dec_xd[1];
+        t.xd[1] = sv->dec_xd[2];
+        t.y[0] = sv->dec_y[1];
+        t.y[1] = sv->dec_y[2];
+        t.z = sv->z;
+        t.hyp = sv->hyp;
+        return dadmm::launch_tail(t, false, (hipStream_t)stream) == hipSuccess ? DADMM_OK : DADMM_EHIP;
+    }
     // fc and the head in one launch (the logits saved for the backward)
     TRY(dadmm_hyper_head_train(B, width, net->H, x, width, net->fc_w, net->fc_b, net->maxv[0], net->maxv[1],
                                net->maxv[2], net->maxv[3], sv->z, sv->hyp, stream));
@@ -257,9 +310,28 @@ static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* At
         TRY(dadmm_hyper_wgrad(B, H4, hid, dzh, H4, sv->dec_y[2], hid, hid, nullptr, 0, g->fc_w, g->fc_b, 1, w.wscr,
                               stream));
     float* dx = w.dx[0];
-    TRY(dadmm_hyper_linear(B, H4, hid, dzh, H4, H4, nullptr, 0, g->fc_wt, nullptr, dx, hid, stream));
+    // deferred: fc's input gradient and decoder blocks 3 and 2 in one launch (dadmm_hyper_tail.hip),
+    // their dZ and LayerNorm partials into the iteration's dsave block
+    const bool tail = defer && tail_usable(net, B);
+    if (tail) {
+        dadmm::TailArgs t = tail_args(net, B, seed);
+        t.xd[0] = sv->dec_xd[1];
+        t.xd[1] = sv->dec_xd[2];
+        t.dz = dzh;
+        t.Wt[0] = g->dec_wt[1];
+        t.Wt[1] = g->dec_wt[2];
+        t.Wt[2] = g->fc_wt;
+        t.dv[0] = d.dv[1];
+        t.dv[1] = d.dv[2];
+        t.part[0] = d.pdec[1];
+        t.part[1] = d.pdec[2];
+        t.dx0 = dx;
+        if (dadmm::launch_tail(t, true, (hipStream_t)stream) != hipSuccess) return DADMM_EHIP;
+    } else {
+        TRY(dadmm_hyper_linear(B, H4, hid, dzh, H4, H4, nullptr, 0, g->fc_wt, nullptr, dx, hid, stream));
+    }
     // decoder blocks, last to first
-    for (int j = 2; j >= 0; --j) {
+    for (int j = tail ? 0 : 2; j >= 0; --j) {
         const int N = net->dec_width[j];
         const int Kin = j > 0 ? net->dec_width[j - 1] : P * net->width[4];
         const float* xin = j > 0 ? sv->dec_y[j - 1] : sv->e;

@@ -332,6 +332,33 @@ int gcn_train_impl(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1, 
                    float* y, int32_t ldy, float* m_out, float* mean_out, float* var_out,
                    const float* bn_running_mean, const float* bn_running_var, void* stream);
 
+// The decoder tail of the training hypernetwork, one launch each way (dadmm_hyper_tail.hip): decoder
+// blocks 2 and 3 (index 1, 2), fc and the head; 16 samples per workgroup
+struct TailArgs {
+    int B, H;
+    int D[3];                 // decoder widths (dec_width 0..2)
+    const float* x0;          // fwd: dec_y[0] [B][D0]
+    const float* W[3];        // fwd: dec_w[1] [D1][D0], dec_w[2] [D2][D1], fc_w [4H][D2]
+    const float* bias[3];     // dec_b[1], dec_b[2], fc_b
+    const float* lnw[2];      // ln_w[1], ln_w[2] (and ln_b)
+    const float* lnb[2];
+    float eps[2], slope[2], drop[2];
+    uint64_t seed;
+    int site0;                // the dropout site of block index 1 (block 2: site0 + 1)
+    float* xd[2];             // dec_xd[1], dec_xd[2] (fwd: written; bwd: read)
+    float* y[2];              // fwd: dec_y[1], dec_y[2]
+    float* z;                 // fwd: [B][4H] logits
+    float* hyp;               // fwd: [B][4H]
+    float maxv[4];
+    const float* dz;          // bwd: [B][4H] logit gradient
+    const float* Wt[3];       // bwd: dec_wt[1] [D0][D1], dec_wt[2] [D1][D2], fc_wt [D2][4H]
+    float* dv[2];             // bwd: the blocks' dZ [B][D1], [B][D2]
+    float* part[2];           // bwd: their LayerNorm partials [ceil(B / 8)][2][D]
+    float* dx0;               // bwd: [B][D0] gradient of dec_y[0]
+};
+size_t tail_lds_bytes(const TailArgs& a, bool bwd);
+hipError_t launch_tail(const TailArgs& a, bool bwd, hipStream_t st);
+
 // BatchNorm running statistics after T = iters * B sequential train-mode calls, closed form
 // (dadmm_hyper_bn_running_update): up to BN_MAX_LAYERS layers in one pair of launches
 constexpr int BN_MAX_LAYERS = 8;

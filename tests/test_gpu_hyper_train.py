@@ -551,13 +551,17 @@ def test_model_eval_autograd_and_odd_n_use_hip(cuda):
     assert model.last_backend == "hip-train"
 
 
+@pytest.mark.parametrize("knob", ["DADMM_GCNBWD_FUSE", "DADMM_HYPER_TAIL"])
 @pytest.mark.parametrize("P,n,hidden,B,per_sample", [(5, 64, 16, 40, False), (7, 32, 12, 33, True)])
-def test_fused_gcn_backward_bit_identical(cuda, monkeypatch, P, n, hidden, B, per_sample):
-    """dadmm_hyper_linear_gcn_bwd — GCN layers 4..1's block backward in the epilogue of the layer
-    above's input-gradient GEMM — against the unfused pair (DADMM_GCNBWD_FUSE=0: linear, then
-    dadmm_hyper_gcn_train_bwd): with dropout on, d AtAy and every parameter gradient are
-    bit-identical, through the per-call HyperTrainFn (immediate weight gradients) and through the
-    whole-forward node (deferred weight gradients)."""
+def test_fused_gcn_backward_bit_identical(cuda, monkeypatch, knob, P, n, hidden, B, per_sample):
+    """Two fusions of the training hypernetwork against their separate launches, with dropout on:
+    DADMM_GCNBWD_FUSE — GCN layers 4..1's block backward in the epilogue of the layer above's
+    input-gradient GEMM (dadmm_hyper_linear_gcn_bwd) vs linear + dadmm_hyper_gcn_train_bwd;
+    DADMM_HYPER_TAIL — decoder blocks 2, 3, fc and the head as one launch each way
+    (dadmm_hyper_tail.hip) vs the ten separate ones (B = 33: a partial 16-sample tile and partial
+    8-row LayerNorm blocks). d AtAy and every parameter gradient are bit-identical, through the
+    per-call HyperTrainFn (immediate weight gradients) and through the whole-forward node
+    (deferred weight gradients), and so are the iterates and hyper-parameters."""
     import copy
 
     import gnn_dlasso_models_progressive as G
@@ -577,8 +581,8 @@ def test_fused_gcn_backward_bit_identical(cuda, monkeypatch, P, n, hidden, B, pe
     bt = torch.from_numpy(b[:B]).to(cuda)[..., None]
     label = torch.randn(B, n, 1, device=cuda, generator=g)
     out = {}
-    for fuse in ("1", "0"):   # always / never fused (the default decides by grid size)
-        monkeypatch.setenv("DADMM_GCNBWD_FUSE", fuse)
+    for fuse in ("1", "0"):   # always / never fused (the defaults decide by grid size / fit)
+        monkeypatch.setenv(knob, fuse)
         model = copy.deepcopy(model0)
         AtAy = AtAy0.clone().requires_grad_(True)
         hyp = hyper_ops.hypernetwork_train(model, AtAy, Atb, n, ahat, per_sample, seed=0xABCDEF)
@@ -591,7 +595,8 @@ def test_fused_gcn_backward_bit_identical(cuda, monkeypatch, P, n, hidden, B, pe
         Y, h = model(bt, graphs, 3)
         assert model.last_backend == "hip-train", model.last_backend
         (U.compute_loss(Y, label)[1] + 0.1 * sum(x.sum() for x in h)).backward()
-        out[fuse] = (per_call, [p.grad.clone() for p in model.parameters()])
+        out[fuse] = (per_call + [hyp.detach().clone(), Y.detach().clone()] + [x.detach().clone() for x in h],
+                     [p.grad.clone() for p in model.parameters()])
     for got, want in zip(out["1"][0] + out["1"][1], out["0"][0] + out["0"][1]):
         assert torch.equal(got, want), (got - want).abs().max()
 
