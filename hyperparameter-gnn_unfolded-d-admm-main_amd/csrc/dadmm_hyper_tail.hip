@@ -35,7 +35,9 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 }
 
 // out[16][N] (LDS, row stride ldo) = X[16][K] (LDS, row stride ldx) W^T, W [N][K] (row stride K):
-// the column blocks of 16 dealt to the waves; W streams through a 4-deep register ring
+// the column blocks of 16 dealt to the waves; W loaded whole per block (K <= 16 WALL) or through a
+// 4-deep register ring
+constexpr int WALL = 32;
 __device__ void gemm16(const float* X, int ldx, const float* __restrict__ W, int K, int N, float* out, int ldo) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int j = lane & 15, h = lane >> 4;
@@ -46,6 +48,21 @@ __device__ void gemm16(const float* X, int ldx, const float* __restrict__ W, int
         const float* wrow = W + (size_t)(col < N ? col : N - 1) * K + 4 * h;
         const float* xrow = X + j * ldx + 4 * h;
         f32x4 acc = z4, wr[4];
+        if (KF <= WALL) {
+            // the column block's whole W row segment in flight at once (one memory wait per block:
+            // with 16 rows per workgroup the chains are short, the round trips were the time)
+            f32x4 wall[WALL];
+#pragma unroll
+            for (int t = 0; t < WALL; ++t)
+                if (t < KF) wall[t] = *(const f32x4*)(wrow + 16 * t);
+#pragma unroll
+            for (int t = 0; t < WALL; ++t)
+                if (t < KF) {
+                    const f32x4 xa = *(const f32x4*)(xrow + 16 * t);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc = mfma4(xa[r], wall[t][r], acc);
+                }
+        } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u) wr[u] = u < KF ? *(const f32x4*)(wrow + 16 * u) : z4;
         for (int t0 = 0; t0 < KF; t0 += 4) {
@@ -60,6 +77,7 @@ __device__ void gemm16(const float* X, int ldx, const float* __restrict__ W, int
                     for (int r = 0; r < 4; ++r) acc = mfma4(xa[r], wv[r], acc);
                 }
             }
+        }
         }
         if (K & 15) {   // the last K mod 16 columns: lanes past K feed zeros
             const bool kin = 16 * KF + 4 * h < K;
