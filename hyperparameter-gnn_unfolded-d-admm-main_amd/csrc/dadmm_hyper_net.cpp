@@ -149,11 +149,15 @@ bool gcn_bwd_fused(int B, int P, int Kin) {
 
 // The decoder tail (blocks 2, 3, fc, head) as one launch each way (dadmm_hyper_tail.hip), where
 // its results are the separate launches' bits: the separate path would not split K of blocks 2 and 3
-// (dadmm_hyper_linear_ln_train's split-K), and the tiles fit LDS. DADMM_HYPER_TAIL=0: the separate
-// launches (A/B timing, the bit-identity test).
+// (dadmm_hyper_linear_ln_train's split-K), and the tiles fit LDS. By default only from B = 2048:
+// at B = 256 its 16 workgroups walk the stages' memory round trips one after another (27 + 33.5 us
+// per iteration, as long as the ten launches it replaces: 8.62-8.69 vs 8.48-8.54 ms per train step),
+// at B = 4096 it is 0.1-0.2 ms ahead (profiles/r05/decoder_tail_r05ad.txt).
+// DADMM_HYPER_TAIL=0 / =1: never / always (A/B timing, the bit-identity test).
 bool tail_usable(const dadmm_hyper_net* net, int B) {
     const char* e = getenv("DADMM_HYPER_TAIL");
     if (e != nullptr && e[0] == '0') return false;
+    if (!(e != nullptr && e[0] == '1') && B < 2048) return false;
     for (int j = 0; j < 3; ++j)
         if (net->dec_width[j] > 2048) return false;
     if (dadmm::hyper_linear_splits(B, net->dec_width[0], net->dec_width[1]) != 1 ||
