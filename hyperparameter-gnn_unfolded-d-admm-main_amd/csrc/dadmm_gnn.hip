@@ -67,10 +67,6 @@ constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
 #ifndef DADMM_GRAM_G2ALL
 #define DADMM_GRAM_G2ALL 1
 #endif
-// gram_lds_kernel's split of the tiles over workgroups priced by the tiles per CU (0: per wave)
-#ifndef DADMM_GRAM_COST_TILES
-#define DADMM_GRAM_COST_TILES 1
-#endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -1238,14 +1234,9 @@ hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* o
         if ((long)a.P * ((tiles + gnn::GL_WAVES - 1) / gnn::GL_WAVES) * 2 < cus) goto item_kernel;
         int best_s = 1;
         long best = -1;
-        const int smax = DADMM_GRAM_COST_TILES ? tiles : (tiles + gnn::GL_WAVES - 1) / gnn::GL_WAVES;
-        for (int S = 1; S <= smax; ++S) {
+        for (int S = 1; S <= (tiles + gnn::GL_WAVES - 1) / gnn::GL_WAVES; ++S) {
             const int tpw = (tiles + S - 1) / S;
-            // (round 5) the tiles a CU runs, not the tiles per wave: a CU's waves share its matrix
-            // pipe and memory path, so 13 tiles on each of 250 CUs beat 16 on each of 200
-            // (configs[4]'s shard: P = 50, 64 tiles; the old model tied them and took the latter)
-            const long per = DADMM_GRAM_COST_TILES ? tpw : (tpw + gnn::GL_WAVES - 1) / gnn::GL_WAVES;
-            const long cost = (long)((a.P * S + cus - 1) / cus) * per;
+            const long cost = (long)((a.P * S + cus - 1) / cus) * ((tpw + gnn::GL_WAVES - 1) / gnn::GL_WAVES);
             if (best < 0 || cost < best) {
                 best = cost;
                 best_s = S;
