@@ -680,7 +680,10 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
 // (buffer range checks), so the loop is branch-free. The epilogue is linear_kernel's inference
 // GCN epilogue (mix with A_hat, the optional addend, bias, leaky_relu, BatchNorm) on the 256-row
 // Z tile.
-constexpr int G32_TM = 256, G32_WAVES = 8, G32_DQ = 4;
+#ifndef DADMM_G32_DQ
+#define DADMM_G32_DQ 4          // LDS-DMA ring stages in flight (timing builds: 3, 5, 6)
+#endif
+constexpr int G32_TM = 256, G32_WAVES = 8, G32_DQ = DADMM_G32_DQ;
 constexpr int G32_STAGE = (G32_TM + TN) * 16;                  // floats per ring stage
 #ifndef DADMM_G32_AHAT_LDS
 #define DADMM_G32_AHAT_LDS 0
