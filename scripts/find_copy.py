@@ -23,15 +23,21 @@ bt = b[..., None].to(dev)
 G = O.er_graph(P, 0.5, seed=7)
 args = argparse.Namespace(GHN_iter_num=K, DADMM_mode="diff", alpha_max=0.1, tau_max=0.99, rho_max=0.99,
                           eta_max=0.99, max_penalty_threshold=0.8, penalty_reduction_factor=0.95)
-model = unfolded_DLASSO.DLASSO_unfolded(torch.from_numpy(A)[None].to(dev), args).to(dev).eval()
+model = unfolded_DLASSO.DLASSO_unfolded(torch.from_numpy(A)[None].to(dev), args).to(dev)
+import numpy as np  # noqa: E402
+param = np.load(os.path.join(ROOT, "tests", "golden", "fixture_25_iter_general_learning_seq_hyp_param.npy"))
+with torch.no_grad():   # as bench.py: the trained table, eval mode, ONE graph list object reused
+    model.seq_hyp.param.copy_(torch.from_numpy(param))
+model.eval()
+graph_list = [G] * B
 with torch.no_grad():
     for _ in range(3):
-        model(bt, [G] * B)
+        model(bt, graph_list)
 torch.cuda.synchronize()
 from torch.profiler import profile, ProfilerActivity  # noqa: E402
 with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
     with torch.no_grad():
         for _ in range(3):
-            model(bt, [G] * B)
+            model(bt, graph_list)
     torch.cuda.synchronize()
-print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=25))
+print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=40))
