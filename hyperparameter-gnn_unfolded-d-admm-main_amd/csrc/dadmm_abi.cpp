@@ -798,9 +798,9 @@ int dadmm_hyper_linear(int32_t rows, int32_t K, int32_t N, const float* x1, int3
     return ok();
 }
 
-int dadmm_hyper_linear_ex(int32_t rows, int32_t K, int32_t N, const float* x1, int32_t ld1, int32_t K1,
-                          const float* x2, int32_t ld2, const float* W, const float* bias, const float* addend,
-                          int32_t ld_add, float* y, int32_t ldy, void* stream) {
+static int hyper_linear_ex_kw(int32_t kwave, int32_t rows, int32_t K, int32_t N, const float* x1, int32_t ld1,
+                              int32_t K1, const float* x2, int32_t ld2, const float* W, const float* bias,
+                              const float* addend, int32_t ld_add, float* y, int32_t ldy, void* stream) {
     dadmm::HyperArgs a;
     int rc = hyper_input(rows, K, N, x1, ld1, K1, x2, ld2, W, y, ldy, &a);
     if (rc) return rc;
@@ -811,9 +811,25 @@ int dadmm_hyper_linear_ex(int32_t rows, int32_t K, int32_t N, const float* x1, i
     a.P = 1;
     a.B = rows;
     a.splits = 1;
+    a.kwave = kwave;
     hipError_t e = dadmm::launch_hyper(a, HYPER_EPI_BIAS, (hipStream_t)stream);
     if (e != hipSuccess) return fail(DADMM_EHIP, "linear launch: %s", hipGetErrorString(e));
     return ok();
+}
+
+int dadmm_hyper_linear_ex(int32_t rows, int32_t K, int32_t N, const float* x1, int32_t ld1, int32_t K1,
+                          const float* x2, int32_t ld2, const float* W, const float* bias, const float* addend,
+                          int32_t ld_add, float* y, int32_t ldy, void* stream) {
+    return hyper_linear_ex_kw(0, rows, K, N, x1, ld1, K1, x2, ld2, W, bias, addend, ld_add, y, ldy, stream);
+}
+
+extern "C++" {
+namespace dadmm {
+int hyper_linear_gcn_dx(int32_t P, int32_t rows, int32_t K, int32_t N, const float* x, int32_t ldx, const float* W,
+                        const float* addend, int32_t ld_add, float* y, int32_t ldy, void* stream) {
+    return hyper_linear_ex_kw(P, rows, K, N, x, ldx, K, nullptr, 0, W, nullptr, addend, ld_add, y, ldy, stream);
+}
+}  // namespace dadmm
 }
 
 int dadmm_hyper_gcn(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1, int32_t ld1,
@@ -831,6 +847,7 @@ int dadmm_hyper_gcn(int32_t B, int32_t P, int32_t K, int32_t N, const float* x1,
     a.bias = bias;
     a.B = B;
     a.P = P;
+    a.kwave = P;   // GCN-class GEMM (the K split may apply, hyper_kwave)
     a.ahat = ahat;
     a.ahat_per_sample = ahat_per_sample ? 1 : 0;
     a.bn_mean = bn_mean;
@@ -865,6 +882,7 @@ int dadmm_hyper_gcn_ex(int32_t B, int32_t P, int32_t K, int32_t N, const float* 
     a.bias = bias;
     a.B = B;
     a.P = P;
+    a.kwave = P;   // GCN-class GEMM (the K split may apply, hyper_kwave)
     a.ahat = ahat;
     a.ahat_per_sample = ahat_per_sample ? 1 : 0;
     a.bn_mean = bn_mean;
@@ -1007,6 +1025,7 @@ int dadmm::gcn_train_impl(int32_t B, int32_t P, int32_t K, int32_t N, const floa
     a.bias = bias;
     a.B = B;
     a.P = P;
+    a.kwave = P;   // GCN-class GEMM (the K split may apply, hyper_kwave)
     a.ahat = ahat;
     a.ahat_per_sample = ahat_per_sample ? 1 : 0;
     a.bn_w = bn_weight;
@@ -1123,6 +1142,7 @@ int dadmm_hyper_linear_gcn_bwd(int32_t B, int32_t P, int32_t K, int32_t N, const
         return fail(DADMM_EUNSUPPORTED, "operand larger than 2^31 floats");
     a.B = B;
     a.P = P;
+    a.kwave = P;   // GCN-class GEMM (the K split may apply, hyper_kwave)
     a.splits = 1;
     a.ahat = ahat;
     a.ahat_per_sample = ahat_per_sample ? 1 : 0;

@@ -122,8 +122,15 @@ __device__ __forceinline__ int xcd_tile(int bid, int G) {
 // accumulators). Operands stream from L2 into a register ring D k-steps (16 k) deep; rows past the
 // tile / columns past N load clamped (valid) rows whose results are never stored, so the main loop
 // has no masks; a K tail that is not a multiple of 16 runs as one masked step.
-template <int WR, int EPI, bool SPLIT, bool DMA>
-__global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
+// KS = 2 (small grids, register ring only): 8 waves, the two halves of the tile's k-steps on two
+// wave sets (kh = 0: the first half), added through LDS once (first half + second half) before the
+// epilogue, which then runs on all 512 threads. Each wave's dependent chain is half as long; the
+// result differs from the KS = 1 chain by that one association (launch_hyper decides KS from the
+// GEMM shape alone, so every caller of one shape gets the same bits).
+template <int WR, int EPI, bool SPLIT, bool DMA, int KS>
+__global__ __launch_bounds__(THREADS * KS) void linear_kernel(HyperArgs a) {
+    static_assert(KS == 1 || (KS == 2 && !DMA), "the K split runs on the register ring");
+    constexpr int NT = THREADS * KS;               // threads per workgroup
     // register ring depth (k-steps in flight; 2 waves/SIMD); DADMM_HYPER_D1: the depth of the
     // one-row-block tiles (small batches: one workgroup per CU, latency-bound K loops)
     [[maybe_unused]] constexpr int D = WR >= 5 ? 3 : (WR == 1 ? DADMM_HYPER_D1 : 4);
@@ -131,7 +138,8 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
     extern __shared__ __attribute__((aligned(16))) float zt[];   // GCN epilogue (dynamic)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int j = lane & 15, h = lane >> 4;
-    const int wr = w >> 1, wcol = w & 1;
+    const int wq = w & 3, kh = KS == 2 ? (w >> 2) : 0;   // the wave's tile position, its k half
+    const int wr = wq >> 1, wcol = wq & 1;
 
     const int gm = a.gm, gn = a.gn;
     const int tl = xcd_tile(blockIdx.x, gridDim.x);
@@ -153,9 +161,14 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
     // k-steps of this split: [t_begin, t_end) of the full steps, plus the tail step in the last
     const int KF = K / 16;                          // full 16-wide steps
     const int per = (KF + a.splits - 1) / a.splits;
-    const int t_begin = split * per;
-    const int t_end = t_begin + per < KF ? t_begin + per : KF;
-    const bool tail = (K & 15) != 0 && split == a.splits - 1;
+    int t_begin = split * per;
+    int t_end = t_begin + per < KF ? t_begin + per : KF;
+    if constexpr (KS == 2) {   // the wave set's half (the first half the longer one)
+        const int mid = t_begin + (t_end - t_begin + 1) / 2;
+        if (kh == 0) t_end = mid;
+        else t_begin = mid;
+    }
+    const bool tail = (K & 15) != 0 && split == a.splits - 1 && kh == KS - 1;
 
     // operand rows (clamped into range)
     size_t oa[WR], ob[WR];
@@ -252,10 +265,10 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
         const rsrc_t rmu = make_rsrc(a.save_mean, (size_t)a.B * a.N * 4);
         const rsrc_t rva = make_rsrc(a.save_var, (size_t)a.B * a.N * 4);
         const int rr = lane >> 4, c4 = 4 * (lane & 15);   // lane-linear: 4 rows x 64 columns per copy
-        for (int q = w; 4 * q < rows_t; q += 4)
+        for (int q = w; 4 * q < rows_t; q += 4 * KS)
             dma16(rm, pf + q * 256, (uint32_t)(((size_t)(row0 + 4 * q + rr) * a.N + col0 + c4) * 4));
         const int nsm = rows_t / a.P;
-        for (int q = w; 4 * q < nsm; q += 4) {
+        for (int q = w; 4 * q < nsm; q += 4 * KS) {
             const uint32_t o = (uint32_t)(((size_t)(s0 + 4 * q + rr) * a.N + col0 + c4) * 4);
             dma16(rmu, pst + q * 256, o);
             dma16(rva, pst + SR * TN + q * 256, o);
@@ -371,9 +384,27 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
         for (int c = 0; c < 2; ++c) bv[c] = kin ? *(const f32x4*)(a.W + ow[c] + 16 * t) : zero;
         mma(av, bv);
     }
+    if constexpr (KS == 2) {   // acc = (first half) + (second half), on the kh = 0 waves
+        __shared__ f32x4 kred[4 * 2 * WR * 64];
+        if (kh == 1) {
+#pragma unroll
+            for (int i = 0; i < WR; ++i)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) kred[((wq * WR + i) * 2 + c) * 64 + lane] = acc[i][c];
+        }
+        __syncthreads();
+        if (kh == 0) {
+#pragma unroll
+            for (int i = 0; i < WR; ++i)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) acc[i][c] = acc[i][c] + kred[((wq * WR + i) * 2 + c) * 64 + lane];
+        }
+    }
 
     // lane (j, h) holds rows 16 (wr WR + i) + 4 h + r of column col0 + 16 (2 wcol + c) + j
+    // (KS = 2: the kh = 0 waves hold the sums)
     if constexpr (!GCN) {
+        if (kh != 0) return;
         float* y = a.y + (size_t)split * a.split_stride;
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -416,19 +447,21 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
         const int P = a.P;
         float* ahs = zt + TM * ZS;                     // [S_t][P][P]
         float* colp = ahs + ((a.S_t * P * P + 3) & ~3);
+        if (kh == 0) {
 #pragma unroll
-        for (int i = 0; i < WR; ++i)
+            for (int i = 0; i < WR; ++i)
 #pragma unroll
-            for (int c = 0; c < 2; ++c)
+                for (int c = 0; c < 2; ++c)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    zt[(16 * (wr * WR + i) + 4 * h + r) * ZS + 16 * (2 * wcol + c) + j] = acc[i][c][r];
+                    for (int r = 0; r < 4; ++r)
+                        zt[(16 * (wr * WR + i) + 4 * h + r) * ZS + 16 * (2 * wcol + c) + j] = acc[i][c][r];
+        }
         const int ns = rows_t / P;
         const float* agl = a.ahat + (a.ahat_per_sample ? (size_t)s0 * P * P : 0);
         if (a.ahat_per_sample) {
-            for (int i = threadIdx.x; i < ns * P * P; i += THREADS) ahs[i] = agl[i];
+            for (int i = threadIdx.x; i < ns * P * P; i += NT) ahs[i] = agl[i];
         } else {
-            for (int i = threadIdx.x; i < P * P; i += THREADS)
+            for (int i = threadIdx.x; i < P * P; i += NT)
                 for (int sl = 0; sl < ns; ++sl) ahs[sl * P * P + i] = agl[i];
         }
         const int cols = a.N - col0 < TN ? a.N - col0 : TN;
@@ -437,7 +470,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
         // 4 fma and made the epilogue as long as the 400-deep GEMM). emit(row, col, sums).
         auto mix = [&](auto&& emit) {
             const int ng = (P + 3) >> 2;
-            for (int task = threadIdx.x; task < ns * ng * (TN / 4); task += THREADS) {
+            for (int task = threadIdx.x; task < ns * ng * (TN / 4); task += NT) {
                 const int cq = task % (TN / 4), rest = task / (TN / 4);
                 const int g = rest % ng, sl = rest / ng;
                 const int c = 4 * cq;
@@ -469,7 +502,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             const uint32_t thr = drop_threshold(a.drop_p);
             const float scale = a.drop_p > 0.0f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
             const float inv = 1.0f / (float)P;
-            for (int task = threadIdx.x; task < ns * TN; task += THREADS) {
+            for (int task = threadIdx.x; task < ns * TN; task += NT) {
                 const int sl = task / TN, c = task - sl * TN;
                 if (c >= cols) continue;
                 const int col = col0 + c, s = s0 + sl;
@@ -507,7 +540,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             }
             __syncthreads();
             // dZ[q] = sum_p A_hat[p][q] dM[p] (the mix, transposed), 4 columns per task
-            for (int task = threadIdx.x; task < rows_t * (TN / 4); task += THREADS) {
+            for (int task = threadIdx.x; task < rows_t * (TN / 4); task += NT) {
                 const int r = task / (TN / 4), c = 4 * (task - r * (TN / 4));
                 if (c >= cols) continue;
                 const int sl = r / P, q = r - sl * P;
@@ -566,7 +599,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
                 }
             });
             __syncthreads();
-            for (int task = threadIdx.x; task < ns * TN; task += THREADS) {
+            for (int task = threadIdx.x; task < ns * TN; task += NT) {
                 const int sl = task / TN, c = task - sl * TN;
                 if (c >= cols) continue;
                 if (a.bn_mean != nullptr) {
@@ -601,7 +634,7 @@ __global__ __launch_bounds__(THREADS) void linear_kernel(HyperArgs a) {
             __syncthreads();
             const uint32_t thr = drop_threshold(a.drop_p);
             const float scale = a.drop_p > 0.0f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
-            for (int task = threadIdx.x; task < rows_t * (TN / 4); task += THREADS) {
+            for (int task = threadIdx.x; task < rows_t * (TN / 4); task += NT) {
                 const int r = task / (TN / 4), c = 4 * (task - r * (TN / 4));
                 if (c >= cols) continue;
                 const int sl = r / P;
@@ -1063,7 +1096,7 @@ __global__ __launch_bounds__(THREADS) void rownorm_kernel(RowNormArgs a) {
     }
 }
 
-template <int WR, int EPI, bool SPLIT, bool DMA>
+template <int WR, int EPI, bool SPLIT, bool DMA, int KS = 1>
 hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
     size_t lds = DMA ? 4 * (size_t)DADMM_HYPER_DQ * (2 * WR + 4) * 256 : 0;   // the ring
     if (EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN || EPI == HYPER_EPI_GCN_BWD) {   // the epilogue (reuses the ring)
@@ -1073,21 +1106,22 @@ hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
         // the prefetched M tile and statistics, past both the ring and the epilogue tile
         if (EPI == HYPER_EPI_GCN_BWD) lds += 4 * ((size_t)32 * WR * TN + 2 * (size_t)((a.S_t + 3) & ~3) * TN);
     }
-    if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
-    if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)linear_kernel<WR, EPI, SPLIT, DMA>,
+    // (KS = 2: plus the static 8 KB x WR of the K-half sums)
+    if (lds + (KS == 2 ? (size_t)8192 * WR : 0) > 160 * 1024) return hipErrorInvalidConfiguration;
+    if (lds > 64 * 1024 - (KS == 2 ? (size_t)8192 * WR : 0)) {
+        hipError_t e = hipFuncSetAttribute((const void*)linear_kernel<WR, EPI, SPLIT, DMA, KS>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((linear_kernel<WR, EPI, SPLIT, DMA>), dim3(grid), dim3(THREADS), lds, st, a);
+    hipLaunchKernelGGL((linear_kernel<WR, EPI, SPLIT, DMA, KS>), dim3(grid), dim3(THREADS * KS), lds, st, a);
     return hipGetLastError();
 }
 
 template <int EPI, bool SPLIT>
-hipError_t launch_wr(int wr, bool dma, int grid, const HyperArgs& a, hipStream_t st) {
+hipError_t launch_wr(int wr, bool dma, int ks, int grid, const HyperArgs& a, hipStream_t st) {
     constexpr bool GCN = EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN || EPI == HYPER_EPI_GCN_BWD;
     switch (wr) {
-        case 1: return launch_one<1, EPI, SPLIT, false>(grid, a, st);
+        case 1: return ks == 2 ? launch_one<1, EPI, SPLIT, false, 2>(grid, a, st) : launch_one<1, EPI, SPLIT, false>(grid, a, st);
         case 2: return dma ? launch_one<2, EPI, SPLIT, true>(grid, a, st) : launch_one<2, EPI, SPLIT, false>(grid, a, st);
         case 4: return dma ? launch_one<4, EPI, SPLIT, true>(grid, a, st) : launch_one<4, EPI, SPLIT, false>(grid, a, st);
         case 5:   // 160-row tiles: whole samples with little padding (3 x 50 nodes, 32 x 5)
@@ -1099,15 +1133,19 @@ hipError_t launch_wr(int wr, bool dma, int grid, const HyperArgs& a, hipStream_t
     }
 }
 
+// the LDS-DMA ring pays for its per-step barrier on long K loops (configs[4]: the 2n-deep first
+// GCN layer 360 -> 310 us, the split-K decoder 247 -> 185 us) and not on short ones (the 400-deep
+// GCN layers: 191 -> 200 us)
+static bool use_dma(int K, int splits) {
+    const int per = (K / 16 + splits - 1) / splits;
+    return DADMM_HYPER_DMA && per >= DADMM_HYPER_DMA_MIN;
+}
+
 template <int EPI>
-hipError_t launch_epi(int wr, int grid, const HyperArgs& a, hipStream_t st) {
-    // the LDS-DMA ring pays for its per-step barrier on long K loops (configs[4]: the 2n-deep
-    // first GCN layer 360 -> 310 us, the split-K decoder 247 -> 185 us) and not on short ones
-    // (the 400-deep GCN layers: 191 -> 200 us)
-    const int per = (a.K / 16 + a.splits - 1) / a.splits;
-    const bool dma = DADMM_HYPER_DMA && per >= DADMM_HYPER_DMA_MIN;
-    if (a.K1 < a.K) return launch_wr<EPI, true>(wr, dma, grid, a, st);
-    return launch_wr<EPI, false>(wr, dma, grid, a, st);
+hipError_t launch_epi(int wr, int ks, int grid, const HyperArgs& a, hipStream_t st) {
+    const bool dma = use_dma(a.K, a.splits);
+    if (a.K1 < a.K) return launch_wr<EPI, true>(wr, dma, ks, grid, a, st);
+    return launch_wr<EPI, false>(wr, dma, ks, grid, a, st);
 }
 
 }  // namespace hyper
@@ -1205,14 +1243,47 @@ static bool try_gcn32(HyperArgs& a, hipStream_t st, hipError_t& err) {
     return true;
 }
 
+// The K split over two wave sets of a workgroup (linear_kernel KS = 2): where the grid of 32-row
+// tiles leaves the CUs idle (< ~2 workgroups per CU) and the register ring runs the whole K loop,
+// each wave's dependent chain halves. Decided from the GEMM shape (rows, K, N) and the GCN P alone,
+// so that a GCN layer's input-gradient GEMM gives the same bits fused with the block backward or
+// alone. a.kwave: 0 = never (the decoder's linears), else the P whose whole-sample tiles pair
+// with this GEMM (the split needs 32-row tiles of whole samples: P <= 32).
+// DADMM_HYPER_KW=0 in the environment: never (A/B timing).
+#ifndef DADMM_HYPER_KW_MIN
+#define DADMM_HYPER_KW_MIN 8    // k-steps (16 k each) from which the K loop is split
+#endif
+static bool hyper_kwave(const HyperArgs& a, int epi, int rows) {
+    static int enabled = -1;
+    if (enabled < 0) {
+        const char* e = getenv("DADMM_HYPER_KW");
+        enabled = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    if (!enabled || a.kwave < 1 || a.kwave > 32 || a.splits > 1) return false;
+    // (the inference GCN layer and the training forward's 200-deep one measured slower split: its
+    // epilogue is shorter than the chain it would overlap; profiles/r05/kwave_r05kw.txt)
+    if (epi == HYPER_EPI_GCN || (epi == HYPER_EPI_GCN_TRAIN && a.K < 256)) return false;
+    const int steps = a.K / 16;
+    if (steps < DADMM_HYPER_KW_MIN || hyper::use_dma(a.K, 1)) return false;
+    const long tiles = (long)((rows + 31) / 32) * ((a.N + hyper::TN - 1) / hyper::TN);
+    return tiles < 480;
+}
+
 hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st) {
-    const int units = (epi == HYPER_EPI_GCN || epi == HYPER_EPI_GCN_TRAIN || epi == HYPER_EPI_GCN_BWD) ? a.B : a.rows;
+    const bool gcn = epi == HYPER_EPI_GCN || epi == HYPER_EPI_GCN_TRAIN || epi == HYPER_EPI_GCN_BWD;
+    const int units = gcn ? a.B : a.rows;
     if (units <= 0 || a.N <= 0) return hipSuccess;
     if (a.K1 < a.K && (a.K1 & 15)) return hipErrorInvalidValue;
     hipError_t gerr = hipSuccess;
     if (epi == HYPER_EPI_GCN && try_gcn32(a, st, gerr)) return gerr;
-    int wr = 0;
-    if (epi == HYPER_EPI_BIAS && a.splits > 1) {
+    int wr = 0, ks = 1;
+    if (hyper_kwave(a, epi, gcn ? a.B * a.P : a.rows)) {   // 32-row tiles (whole samples), K split in two
+        ks = 2;
+        wr = 1;
+        a.gn = (a.N + hyper::TN - 1) / hyper::TN;
+        a.S_t = gcn ? 32 / a.P : 32;
+        a.gm = (units + a.S_t - 1) / a.S_t;
+    } else if (epi == HYPER_EPI_BIAS && a.splits > 1) {
         int sp = 0;
         wr = pick_split_tiles(a, a.K, sp);
         if (sp != a.splits) wr = pick_tiles(a, epi);   // caller's own split count: plain tiling
@@ -1223,11 +1294,11 @@ hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st) {
     if (a.splits < 1) a.splits = 1;
     const int grid = a.gm * a.gn * a.splits;
     switch (epi) {
-        case HYPER_EPI_BIAS: return hyper::launch_epi<HYPER_EPI_BIAS>(wr, grid, a, st);
-        case HYPER_EPI_GCN: return hyper::launch_epi<HYPER_EPI_GCN>(wr, grid, a, st);
-        case HYPER_EPI_HEAD: return hyper::launch_epi<HYPER_EPI_HEAD>(wr, grid, a, st);
-        case HYPER_EPI_GCN_TRAIN: return hyper::launch_epi<HYPER_EPI_GCN_TRAIN>(wr, grid, a, st);
-        case HYPER_EPI_GCN_BWD: return hyper::launch_epi<HYPER_EPI_GCN_BWD>(wr, grid, a, st);
+        case HYPER_EPI_BIAS: return hyper::launch_epi<HYPER_EPI_BIAS>(wr, ks, grid, a, st);
+        case HYPER_EPI_GCN: return hyper::launch_epi<HYPER_EPI_GCN>(wr, ks, grid, a, st);
+        case HYPER_EPI_HEAD: return hyper::launch_epi<HYPER_EPI_HEAD>(wr, ks, grid, a, st);
+        case HYPER_EPI_GCN_TRAIN: return hyper::launch_epi<HYPER_EPI_GCN_TRAIN>(wr, ks, grid, a, st);
+        case HYPER_EPI_GCN_BWD: return hyper::launch_epi<HYPER_EPI_GCN_BWD>(wr, ks, grid, a, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -396,7 +396,7 @@ static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* At
                 dZ = nz;
             } else {
                 // dX into the buffer dx held (gcn backward consumed it)
-                TRY(dadmm_hyper_linear(rows, N, Kin, dZ, N, N, nullptr, 0, g->conv_wt[i], nullptr, dx, Kin, stream));
+                TRY(dadmm::hyper_linear_gcn_dx(P, rows, N, Kin, dZ, N, g->conv_wt[i], nullptr, 0, dx, Kin, stream));
                 dZ = nullptr;
             }
         } else {
@@ -405,8 +405,8 @@ static int train_backward(const dadmm_hyper_net* net, int32_t B, const float* At
                 TRY(dadmm_hyper_wgrad(rows, N, 2 * n, dZ, N, AtAy, net->ld, n, Atb, net->ld, g->conv_w[0], nullptr,
                                       1, w.wscr, stream));
             // (acc_dA: dAtAy += ..., in the linear's epilogue instead of a separate add)
-            TRY(dadmm_hyper_linear_ex(rows, N, n, dZ, N, N, nullptr, 0, g->conv_wt[0], nullptr,
-                                      acc_dA ? dAtAy : nullptr, net->ld, dAtAy, net->ld, stream));
+            TRY(dadmm::hyper_linear_gcn_dx(P, rows, N, n, dZ, N, g->conv_wt[0], acc_dA ? dAtAy : nullptr, net->ld,
+                                           dAtAy, net->ld, stream));
         }
     }
     return DADMM_OK;

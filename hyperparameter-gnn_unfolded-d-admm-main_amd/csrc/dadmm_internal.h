@@ -252,6 +252,11 @@ struct HyperArgs {
     // gamma; part [3][B][N] the per-sample dgamma / dbeta / dbias sums; bn_eval: running statistics
     float* part;
     int bn_eval;
+    // GCN-class GEMMs (the GCN layers forward and backward, their input gradients): the launcher
+    // may split a small grid's K loop over two wave sets of each workgroup (linear_kernel KS = 2;
+    // hyper_kwave decides from the GEMM shape alone). 0 for the decoder's linears, whose chains
+    // dadmm_hyper_tail.hip restates.
+    int kwave;
 };
 
 // Counter-based dropout mask shared by the training forward and backward kernels (the backward
@@ -270,6 +275,11 @@ __host__ __device__ inline uint32_t drop_threshold(float p) {
     return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
 }
 hipError_t launch_hyper(HyperArgs a, int epi, hipStream_t st);
+// dadmm_hyper_linear_ex (no bias) as a GCN-class GEMM: a GCN layer's input gradient dX = dZ W on
+// its B samples of P rows, which may take the K split like the fused dadmm_hyper_linear_gcn_bwd
+// of the same shape (same bits either way); the C-ABI's linears never split (the decoder's)
+int hyper_linear_gcn_dx(int32_t P, int32_t rows, int32_t K, int32_t N, const float* x, int32_t ldx, const float* W,
+                        const float* addend, int32_t ld_add, float* y, int32_t ldy, void* stream);
 int hyper_linear_splits(int rows, int K, int N);
 struct RowNormArgs {
     const float* x;         // [nsum][rows][C] (row stride C, partial q at x + q * sum_stride)

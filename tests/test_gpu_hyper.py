@@ -85,7 +85,9 @@ def _ahat(nbr, P, dev):
                                                 # gcn32_kernel (32x32x2 MFMA, 256-row tiles): 400-wide
                                                 # layers of configs[4], a K tail (100 % 16), shared graph
                                                 (1024, 50, 400, 400, True), (1024, 50, 100, 200, True),
-                                                (2000, 16, 200, 200, False)])
+                                                (2000, 16, 200, 200, False),
+                                                # small grids (the inference layer never splits K)
+                                                (60, 5, 400, 400, True), (9, 16, 200, 400, False)])
 def test_gcn_layer_matches_torch(cuda, L, B, P, K, N, per_sample):
     from dadmm_hip.graph import ingest
     G = B if per_sample else 1

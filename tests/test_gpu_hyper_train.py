@@ -124,7 +124,10 @@ def _close64(got, want32, want64, name=""):
                                                           (16, 32, 8, "diff", True, 5),
                                                           (3, 100, 20, "diff", True, 70),
                                                           (5, 37, 16, "diff", True, 12),    # odd n
-                                                          (4, 2, 8, "same", False, 6)])     # 2n < 4
+                                                          (4, 2, 8, "same", False, 6),      # 2n < 4
+                                                          # h = 100: the 200/400-deep GEMMs split K
+                                                          # over two wave sets (linear_kernel KS = 2)
+                                                          (5, 64, 100, "diff", True, 12)])
 def test_train_hypernetwork_matches_torch_autograd(cuda, P, n, hidden, mode, per_sample, B):
     """n % 4 != 0: layer 1's input cat(AtAy, Atb) zero-padded to a multiple of 4 columns
     (hyper_ops.layer1_input; VERDICT r4 missing #2: such widths ran on torch before)."""
@@ -552,7 +555,8 @@ def test_model_eval_autograd_and_odd_n_use_hip(cuda):
 
 
 @pytest.mark.parametrize("knob", ["DADMM_GCNBWD_FUSE", "DADMM_HYPER_TAIL"])
-@pytest.mark.parametrize("P,n,hidden,B,per_sample", [(5, 64, 16, 40, False), (7, 32, 12, 33, True)])
+@pytest.mark.parametrize("P,n,hidden,B,per_sample", [(5, 64, 16, 40, False), (7, 32, 12, 33, True),
+                                                     (5, 64, 100, 40, True)])
 def test_fused_gcn_backward_bit_identical(cuda, monkeypatch, knob, P, n, hidden, B, per_sample):
     """Two fusions of the training hypernetwork against their separate launches, with dropout on:
     DADMM_GCNBWD_FUSE — GCN layers 4..1's block backward in the epilogue of the layer above's
