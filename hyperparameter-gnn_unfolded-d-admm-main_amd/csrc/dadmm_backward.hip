@@ -93,6 +93,11 @@ constexpr int BWD_QD = 5;
 #ifndef DADMM_BWD_PF
 #define DADMM_BWD_PF (DADMM_BWD_WAVES == 4 ? 2 : 0)
 #endif
+// DADMM_BWD_PK=1: the shared graph's consensus on row pairs with packed f32 instructions
+// (consensus_fma2: the same values, half the VALU issue)
+#ifndef DADMM_BWD_PK
+#define DADMM_BWD_PK 1
+#endif
 #if DADMM_BWD_ROT
 #define BWD_ROW(e, r) (r)
 #else
@@ -195,8 +200,26 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
     for (int q = 0; q < P; ++q)
 #pragma unroll
         for (int p = 0; p < P; ++p) mf[q][p] = (GRAPH == GRAPH_SHARED && ((msk[q] >> p) & 1u)) ? 1.0f : 0.0f;
+    [[maybe_unused]] f32x2_c mf2[P][P];
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int p = 0; p < P; ++p) mf2[q][p] = (f32x2_c){mf[q][p], mf[q][p]};
     auto cons = [&](const float (&x)[P][4], float (&o)[P][4], const uint32_t (&mk_)[P]) {
-        if constexpr (GRAPH == GRAPH_SHARED && DADMM_BWD_ROT) {
+        if constexpr (GRAPH == GRAPH_SHARED && DADMM_BWD_ROT && DADMM_BWD_PK) {
+#pragma unroll
+            for (int rp = 0; rp < 2; ++rp) {   // rows (2 rp, 2 rp + 1) packed
+                f32x2_c yy[P], dd[P];
+#pragma unroll
+                for (int p = 0; p < P; ++p) yy[p] = (f32x2_c){x[p][2 * rp], x[p][2 * rp + 1]};
+                consensus_fma2<P>(yy, dd, mf2);
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    o[p][2 * rp] = dd[p][0];
+                    o[p][2 * rp + 1] = dd[p][1];
+                }
+            }
+        } else if constexpr (GRAPH == GRAPH_SHARED && DADMM_BWD_ROT) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float yy[P][1], dd[P][1];

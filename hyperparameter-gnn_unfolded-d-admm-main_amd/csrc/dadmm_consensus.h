@@ -108,6 +108,49 @@ __device__ __forceinline__ void consensus_fma(const float (&yy)[P][1], float (&d
     }
 }
 
+// consensus_fma on two rows at once (v_pk_add_f32 / v_pk_fma_f32: each half rounded exactly as the
+// scalar instruction, so the result is consensus_fma's bit for bit, at half the VALU issue). The
+// multipliers mf2[a][b] = {mf, mf} are uniform (an SGPR pair per candidate pair).
+typedef float f32x2_c __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2_c pk_sub_c(f32x2_c a, f32x2_c b) {   // a - b == a + (-b) exactly
+    f32x2_c r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f32x2_c pk_fma_s(f32x2_c d, f32x2_c m, f32x2_c acc) {    // d m + acc
+    f32x2_c r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(d), "s"(m), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ f32x2_c pk_fma_sn(f32x2_c d, f32x2_c m, f32x2_c acc) {   // -d m + acc
+    f32x2_c r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(r) : "v"(d), "s"(m), "v"(acc));
+    return r;
+}
+template <int P>
+__device__ __forceinline__ void consensus_fma2(const f32x2_c (&yy)[P], f32x2_c (&dl)[P],
+                                               const f32x2_c (&mf)[P][P]) {
+    f32x2_c d[P][P];
+#pragma unroll
+    for (int a2 = 0; a2 < P; ++a2)
+#pragma unroll
+        for (int b2 = a2 + 1; b2 < P; ++b2) d[a2][b2] = pk_sub_c(yy[a2], yy[b2]);
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        f32x2_c acc = {0.0f, 0.0f};
+#pragma unroll
+        for (int q = 0; q < p; ++q) acc = pk_fma_sn(d[q][p], mf[q][p], acc);
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            if (q < p) acc = pk_fma_sn(d[q][p], mf[q][p], acc);
+            else if (q > p) acc = pk_fma_s(d[p][q], mf[p][q], acc);
+        }
+#pragma unroll
+        for (int q = p + 1; q < P; ++q) acc = pk_fma_s(d[p][q], mf[p][q], acc);
+        dl[p] = acc;
+    }
+}
+
 // Per-lane (per-sample graph) form: the conditional adds become selects; pair differences are
 // shared as above (the compiler CSEs yy[a] - yy[b] across the four uses).
 template <int P, int E>
