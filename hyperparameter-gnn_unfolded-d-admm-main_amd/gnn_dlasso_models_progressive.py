@@ -36,6 +36,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import dadmm_cpu
 from dadmm_hip import _lib
 from dadmm_hip import hyper_ops
 from dadmm_hip.autograd import tag_status
@@ -249,6 +250,15 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         a_hat = normalized_adjacency(graphs.nbr, self.P, adj=graphs.adj)
         if graphs.shared and graphs.adj is None:
             a_hat = a_hat[None]
+        if device.type == "cpu":
+            # CPU tensors (the reference's default device): its op sequence in torch eager ops,
+            # the hypernetwork as the torch composition (dadmm_cpu); CUDA tensors never get here
+            if inits is None:
+                y0, U0, d0 = (torch.randn((batch_size, self.P, self.n, 1), device=device) * 1e-2
+                              for _ in range(3))                                   # :142-146
+            else:
+                y0, U0, d0 = inits
+            return self._forward_cpu(bb, graphs, a_hat, y0, U0, d0, K)
         if inits is None:
             # torch.randn((B, P, n, 1)) * 1e-2 x 3 (:142-146), bit-identical, one launch
             y0, U0, d0 = draw_inits((batch_size, self.P, self.n), device)
@@ -307,6 +317,33 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
         Y = torch.stack(ys) if run.Y is None else run.Y
         Y = Y[..., :n].unsqueeze(-1)
         return tag_status(Y, self.last_status), (alpha_k, tau_k, rho_k, eta_k)
+
+    def _forward_cpu(self, bb, graphs, a_hat, y0, U0, d0, K):
+        """forward on CPU tensors (gnn_dlasso_models_progressive.py:148-240 in torch eager ops,
+        differentiable by torch autograd)."""
+        B, P, n = bb.shape[0], self.P, self.n
+        prep = dadmm_cpu.gnn_prepare(self.A, bb, graphs, B)
+        AtA, Atb = prep[0], prep[1]
+        y, U, d = (x.reshape(B, P, n, 1) for x in (y0, U0, d0))
+        self.last_backend = "cpu"
+        status = 0
+        Y = []
+        for k in range(K):
+            if bool(torch.isnan(y).any() or torch.isinf(y).any()):   # :150-152
+                status |= _lib.STATUS_Y_NONFINITE
+                y = torch.zeros_like(y)
+            if bool(torch.isnan(U).any() or torch.isinf(U).any()):   # :154-156
+                status |= _lib.STATUS_U_NONFINITE
+                U = torch.zeros_like(U)
+            AtAy = torch.matmul(AtA[None], y)                          # :158-162 (Gram form)
+            hyp = self.hypernetwork(AtAy[..., 0], Atb[..., 0], a_hat)   # :165-196
+            if self.on_hyp is not None:
+                self.on_hyp(AtAy[..., 0], Atb[..., 0], hyp)
+            y, U, d, st = dadmm_cpu.gnn_step(prep, y, U, d, AtAy, *hyp)
+            status |= st
+            Y.append(y)
+        self.last_status = torch.tensor([status], dtype=torch.int32)
+        return tag_status(torch.stack(Y), self.last_status), hyp
 
     def _forward_train_native(self, bb, graphs, a_hat, y0, U0, d0, K, H, grad):
         """The training forward as one GnnTrainFn node: K x (gram, hypernetwork, step), each

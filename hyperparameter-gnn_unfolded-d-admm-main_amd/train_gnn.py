@@ -99,7 +99,7 @@ def _host_graphs(P, prob, seeds):
 def _graphs(args, batch_seed, lo, hi, device):
     """This rank's graphs for samples lo..hi-1 of one batch, drawn per sample."""
     prob = max(args.graph_prob, 0.3)
-    if args.graphs == "host":
+    if args.graphs == "host" or device.type == "cpu":   # (on the CPU: networkx, as the reference)
         return ingest(_host_graphs(args.P, prob, [batch_seed * 65536 + s for s in range(lo, hi)]),
                       args.P, hi - lo, device)
     # device: one generate_er call per shard; sample s of the batch uses hash stream
@@ -138,11 +138,15 @@ def main(argv=None):
         raise SystemExit(f"--train_size ({args.train_size}) and --test_size ({args.test_size}) must "
                          f"be at least --batch_size ({args.batch_size})")
     rank, world, local = D.init_from_env()
-    if not (torch.cuda.is_available() and args.device.startswith("cuda")):
-        raise SystemExit("train_gnn.py runs the HIP forward: it needs a ROCm GPU (--device cuda:N)")
-    dev_idx = local % torch.cuda.device_count() if world > 1 else int(args.device.split(":")[1])
-    device = torch.device("cuda", dev_idx)
-    torch.cuda.set_device(device)
+    if torch.cuda.is_available() and args.device.startswith("cuda"):
+        dev_idx = local % torch.cuda.device_count() if world > 1 else int(args.device.split(":")[1])
+        device = torch.device("cuda", dev_idx)
+        torch.cuda.set_device(device)
+    elif args.device == "cpu":
+        # the reference's default device: DLASSO_GNNHyp3_Progressive runs its CPU path (dadmm_cpu)
+        device = torch.device("cpu")
+    else:
+        raise SystemExit(f"--device {args.device}: use cuda:N (a ROCm GPU) or cpu")
     seed = int(args.seed)
     torch.manual_seed(seed)
     gen = torch.Generator().manual_seed(seed)

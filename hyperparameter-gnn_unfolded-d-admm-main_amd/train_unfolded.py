@@ -100,15 +100,19 @@ def main(argv=None):
         dev_idx = local % torch.cuda.device_count() if world > 1 else int(args.device.split(":")[1])
         device = torch.device("cuda", dev_idx)
         torch.cuda.set_device(device)
+    elif args.device == "cpu":
+        # the reference's default device: DLASSO_unfolded runs its CPU path (dadmm_cpu)
+        device = torch.device("cpu")
     else:
-        raise SystemExit("train_unfolded.py runs the HIP forward: it needs a ROCm GPU (--device cuda:N)")
+        raise SystemExit(f"--device {args.device}: use cuda:N (a ROCm GPU) or cpu")
     seed = int(args.seed)
     torch.manual_seed(seed)
     gen = torch.Generator().manual_seed(seed)
 
     A = gnn_dlasso_utils.set_A(args).to(device)
     if args.init_draw == "local":
-        torch.cuda.manual_seed(seed * 1009 + rank)   # independent init noise per shard
+        if device.type == "cuda":
+            torch.cuda.manual_seed(seed * 1009 + rank)   # independent init noise per shard
     b_tr, x_tr = _dataset(A, args.train_size, args, gen)
     b_va, x_va = _dataset(A, args.test_size, args, gen)
     b_tr, x_tr, b_va, x_va = (t.to(device) for t in (b_tr, x_tr, b_va, x_va))

@@ -2,14 +2,16 @@
 
 Mirrors the reference's public interface (unfolded_DLASSO.py:9-168): constructor ``(A, args)``,
 ``forward(b, graph_list, K=None) -> (Y [K',B,P,n,1], hyp [H,4,1])`` with ``K' = min(K, self.K)``,
-state_dict ``{'seq_hyp.param': [K, P|1, 4]}``, and ``seq_hyp(k)``. The K-step recurrence runs in
-one fused HIP launch (``dadmm_hip``, C ABI ``include/dadmm.h``); there is no CPU path.
+state_dict ``{'seq_hyp.param': [K, P|1, 4]}``, and ``seq_hyp(k)``. On CUDA tensors the K-step
+recurrence runs in one fused HIP launch (``dadmm_hip``, C ABI ``include/dadmm.h``); CPU tensors
+(the reference's default device) run its op sequence in torch eager ops (``dadmm_cpu``).
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 
+import dadmm_cpu
 from dadmm_hip import _lib
 from dadmm_hip.autograd import check_status, dadmm_unfolded_apply, tag_status
 from dadmm_hip.ops import describe_status
@@ -99,6 +101,19 @@ class DLASSO_unfolded(nn.Module):
                     f"({batch_size}) at non-singleton dimension 0")
             bb = bb.expand(batch_size, -1, -1)
         graphs = ingest(graph_list, self.P, batch_size, device)
+
+        if device.type == "cpu":
+            # CPU tensors (the reference's default device): its op sequence in torch eager ops
+            # (dadmm_cpu); CUDA tensors never take this path
+            if inits is None:
+                y0, U0, d0 = (torch.randn((batch_size, self.P, self.n, 1), device=device) * 1e-2
+                              for _ in range(3))                            # :49-51, in order
+            else:
+                y0, U0, d0 = inits
+            table = self.seq_hyp.table(K)
+            Y, st = dadmm_cpu.unfolded_forward(self.A, bb, graphs, table, K, (y0, U0, d0))
+            self.last_status = torch.tensor([st], dtype=torch.int32)
+            return tag_status(Y.unsqueeze(-1), self.last_status), table[K - 1].unsqueeze(-1)
 
         if inits is None:
             # drawn by the forward's prologue launch: == torch.randn((B,P,n,1)) * 1e-2 x 3 value

@@ -113,11 +113,13 @@ def test_hypernetwork_matches_edge_list_restatement(mode):
         np.testing.assert_allclose(g[..., 0, 0].numpy(), w, rtol=1e-10, atol=1e-12)
 
 
-def test_forward_refuses_cpu_tensors():
+def test_forward_runs_cpu_tensors_on_the_cpu_path():
+    """CPU tensors (the reference's default device) run dadmm_cpu's torch ops; the HIP library
+    serves CUDA tensors only (tests/test_cpu_path.py checks the values)."""
     model = _model()
     b = torch.randn(3, 5, 8, 1)
-    with pytest.raises(RuntimeError):
-        model(b, [O.er_graph(5, 0.5, seed=1)] * 3)
+    Y, hyp = model(b, [O.er_graph(5, 0.5, seed=1)] * 3)
+    assert Y.device.type == "cpu" and model.last_backend == "cpu" and len(hyp) == 4
 
 
 def test_forward_needs_one_graph_per_sample():
