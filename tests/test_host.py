@@ -153,13 +153,21 @@ def test_module_state_dict_matches_reference_keys(mode, H):
     torch.testing.assert_close(model.AtA, torch.matmul(A.transpose(-1, -2), A))
 
 
-def test_module_refuses_cpu_tensors():
-    """No CPU fallback: the product path needs a ROCm device."""
+def test_module_dispatches_on_the_input_device(monkeypatch):
+    """CPU tensors run dadmm_cpu without touching the HIP library (here made unloadable); the HIP
+    entry points stay loud: they refuse CPU tensors and a missing library raises."""
     import unfolded_DLASSO
+    from dadmm_hip import PreparedOperator, _lib
+
+    def gone():
+        raise ImportError("libdadmm.so missing (test)")
+    monkeypatch.setattr(_lib, "load", gone)
     A = torch.randn(1, 3, 8, 16)
     model = unfolded_DLASSO.DLASSO_unfolded(A, _args(GHN_iter_num=3))
+    Y, hyp = model(torch.randn(4, 3, 8, 1), [nx.path_graph(3)] * 4)
+    assert Y.shape == (3, 4, 3, 16, 1) and Y.device.type == "cpu"
     with pytest.raises((RuntimeError, ImportError)):
-        model(torch.randn(4, 3, 8, 1), [nx.path_graph(3)] * 4)
+        PreparedOperator(A)          # the HIP path's first step: CPU tensor / no library -> raises
 
 
 def test_module_k_zero_raises():
