@@ -98,6 +98,13 @@ constexpr int BWD_QD = 5;
 #ifndef DADMM_BWD_PK
 #define DADMM_BWD_PK 1
 #endif
+// DADMM_BWD_DPP=1: the per-iteration dhyp wave sums on DPP moves (quad perms, half-row and row
+// mirrors: each lane ends with its 16-lane row's sum) and four readlanes, instead of six
+// ds_bpermute round trips per value (a fixed order either way: deterministic; the association
+// differs from the butterfly's, within f32 rounding)
+#ifndef DADMM_BWD_DPP
+#define DADMM_BWD_DPP 1
+#endif
 #if DADMM_BWD_ROT
 #define BWD_ROW(e, r) (r)
 #else
@@ -596,8 +603,12 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 float v = part[p][c];
+                if constexpr (DADMM_BWD_DPP) {
+                    v = wave_sum_dpp(v);
+                } else {
 #pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+                    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+                }
                 if (lane == 0) red[(w * P + p) * 4 + c] = v;
             }
         __syncthreads();

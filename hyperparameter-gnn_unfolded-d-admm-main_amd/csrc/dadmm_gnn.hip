@@ -64,6 +64,11 @@ constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
 #ifndef DADMM_GRAM_GD8
 #define DADMM_GRAM_GD8 1
 #endif
+// DADMM_SBW_DPP=1: the step adjoint's per-sample hyper-parameter wave sums on DPP moves and
+// readlanes (wave_sum_dpp) instead of six ds_bpermute round trips each
+#ifndef DADMM_SBW_DPP
+#define DADMM_SBW_DPP 1
+#endif
 #ifndef DADMM_GRAM_G2ALL
 #define DADMM_GRAM_G2ALL 1
 #endif
@@ -980,8 +985,12 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
     }
     __builtin_amdgcn_wave_barrier();
     auto accum = [&](int c, int p, float v) {   // wave-sum v into red[c][p or 0]
+        if constexpr (DADMM_SBW_DPP) {
+            v = wave_sum_dpp(v);
+        } else {
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        }
         if (lane == 0) red[c * H + (H == 1 ? 0 : p)] += v;
     };
     // (round 4) no-alias views of the streams, so that the unrolled agent loops below can put

@@ -6,6 +6,26 @@
 
 namespace dadmm {
 
+// Sum of v over the wave's 64 lanes, in a fixed order, on DPP moves (quad perms, half-row and row
+// mirrors: every lane ends with its 16-lane row's sum) and four readlanes: no LDS round trips (a
+// __shfl_xor butterfly is six ds_bpermute round trips). Deterministic; the association differs
+// from the butterfly's (f32 rounding). Uniform result.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov_f32(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v = v + dpp_mov_f32<0xB1>(v);    // quad_perm [1,0,3,2]
+    v = v + dpp_mov_f32<0x4E>(v);    // quad_perm [2,3,0,1]: every lane holds its quad's sum
+    v = v + dpp_mov_f32<0x141>(v);   // row_half_mirror: its 8-lane group's
+    v = v + dpp_mov_f32<0x140>(v);   // row_mirror: its 16-lane row's
+    const auto lane_v = [&](int l) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+    };
+    return (lane_v(0) + lane_v(16)) + (lane_v(32) + lane_v(48));
+}
+
+
 // sign(y) * t exactly as torch's eager ops give it (sign(+-0) = sign(NaN) = 0, so +0 there, else
 // +-t), without branches: the sign bit of y moved onto t, then one select. (The nested-ternary
 // form compiles to divergent branches, ~11 instructions per element in the middle of the MFMA
