@@ -62,10 +62,18 @@ __device__ __forceinline__ float visit_sum(const float* __restrict__ x, const in
     return acc;
 }
 
-// wave-sum of v into red[p][c] (lane 0 accumulates; one wave owns its red slice)
+// wave-sum of v into red[p][c] (lane 0 accumulates; one wave owns its red slice); on DPP moves
+// (wave_sum_dpp) unless built with -DDADMM_ADJ_DPP=0
+#ifndef DADMM_ADJ_DPP
+#define DADMM_ADJ_DPP 1
+#endif
 __device__ __forceinline__ void wave_accum(float* red, int p, int c, float v, int lane) {
+#if DADMM_ADJ_DPP
+    v = wave_sum_dpp(v);
+#else
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+#endif
     if (lane == 0) red[p * 4 + c] += v;
 }
 
@@ -402,8 +410,12 @@ __device__ __forceinline__ f32x4v visit_sum4(const float* __restrict__ x, const 
 // sum of v over this lane's 4 columns and its 16-lane group -> red[p][c] (lane 16 a adds)
 __device__ __forceinline__ void group_accum(float* red, int p, int c, f32x4v v, bool live, int lane) {
     float s = (v[0] + v[1]) + (v[2] + v[3]);
+#if DADMM_ADJ_DPP
+    s = row16_sum_dpp(s);
+#else
 #pragma unroll
     for (int off = 8; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+#endif
     if ((lane & 15) == 0 && live) red[p * 4 + c] += s;
 }
 

@@ -1060,8 +1060,7 @@ __global__ __launch_bounds__(THREADS) void rownorm_kernel(RowNormArgs a) {
         }
         s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    s = ln_row_sum(s);
     const float mean = s / (float)a.C;
     float q = 0.0f;
 #pragma unroll
@@ -1075,8 +1074,7 @@ __global__ __launch_bounds__(THREADS) void rownorm_kernel(RowNormArgs a) {
             }
         }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+    q = ln_row_sum(q);
     const float rstd = 1.0f / sqrtf(q / (float)a.C + a.eps);
     float* y = a.y + (size_t)row * a.C;
 #pragma unroll

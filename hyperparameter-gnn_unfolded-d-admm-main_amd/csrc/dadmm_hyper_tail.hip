@@ -127,8 +127,7 @@ __device__ void ln_rows(float* T, int ldt, int C, int r0, int rows_t, const floa
             }
             s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        s = ln_row_sum(s);
         const float mean = s / (float)C;
         float q = 0.0f;
 #pragma unroll
@@ -143,8 +142,7 @@ __device__ void ln_rows(float* T, int ldt, int C, int r0, int rows_t, const floa
                 }
             }
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+        q = ln_row_sum(q);
         const float rstd = 1.0f / sqrtf(q / (float)C + eps);
 #pragma unroll
         for (int u = 0; u < CHMAX; ++u) {
@@ -212,8 +210,7 @@ __device__ void ln_bwd_rows(float* G, int ldg, int C, int r0, int rows_t, int B,
             for (int e = 0; e < 4; ++e) v[u][e] = cok[u] ? xr[e] : 0.0f;
             s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        s = ln_row_sum(s);
         const float mean = s * invC;
         float q = 0.0f;
 #pragma unroll
@@ -226,8 +223,7 @@ __device__ void ln_bwd_rows(float* G, int ldg, int C, int r0, int rows_t, int B,
                 q = cok[u] ? q + dd : q;
             }
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+        q = ln_row_sum(q);
         const float rstd = 1.0f / sqrtf(q * invC + eps);
         float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
@@ -250,11 +246,8 @@ __device__ void ln_bwd_rows(float* G, int ldg, int C, int r0, int rows_t, int B,
                 g[u][e] = dxh;
             }
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            s1 += __shfl_xor(s1, o);
-            s2 += __shfl_xor(s2, o);
-        }
+        s1 = ln_row_sum(s1);
+        s2 = ln_row_sum(s2);
         const float m1 = s1 * invC, m2 = s2 * invC;
 #pragma unroll
         for (int u = 0; u < CHMAX; ++u) {

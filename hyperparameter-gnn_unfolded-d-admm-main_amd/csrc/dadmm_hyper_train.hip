@@ -196,8 +196,7 @@ __global__ __launch_bounds__(THREADS) void rownorm_bwd_kernel(RowNormBwdArgs a) 
             for (int e = 0; e < 4; ++e) v[u][e] = cok[u] ? xr[i][u][e] : 0.0f;
             s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        s = ln_row_sum(s);
         const float mean = s * invC;
         float q = 0.0f;
 #pragma unroll
@@ -209,8 +208,7 @@ __global__ __launch_bounds__(THREADS) void rownorm_bwd_kernel(RowNormBwdArgs a) 
                 q = cok[u] ? q + dd : q;
             }
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+        q = ln_row_sum(q);
         const float rstd = 1.0f / sqrtf(q * invC + a.eps);
         // xhat, dt (through the LeakyReLU), the affine partials, dxhat and its two row sums
         float s1 = 0.0f, s2 = 0.0f;
@@ -235,11 +233,8 @@ __global__ __launch_bounds__(THREADS) void rownorm_bwd_kernel(RowNormBwdArgs a) 
                 g[u][e] = dxh;
             }
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            s1 += __shfl_xor(s1, o);
-            s2 += __shfl_xor(s2, o);
-        }
+        s1 = ln_row_sum(s1);
+        s2 = ln_row_sum(s2);
         const float m1 = s1 * invC, m2 = s2 * invC;
         float* dx = a.dx + (size_t)row * C;
 #pragma unroll

@@ -24,6 +24,29 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
     };
     return (lane_v(0) + lane_v(16)) + (lane_v(32) + lane_v(48));
 }
+// Sum of v over each 16-lane row, in every lane of the row (the first four steps above).
+__device__ __forceinline__ float row16_sum_dpp(float v) {
+    v = v + dpp_mov_f32<0xB1>(v);
+    v = v + dpp_mov_f32<0x4E>(v);
+    v = v + dpp_mov_f32<0x141>(v);
+    return v + dpp_mov_f32<0x140>(v);
+}
+
+// The LayerNorm row sums (rownorm forward / backward and the hypernetwork tail kernel's copies of
+// them, which must reduce identically): wave_sum_dpp unless built with -DDADMM_LN_DPP=0 (the
+// __shfl_xor butterfly).
+#ifndef DADMM_LN_DPP
+#define DADMM_LN_DPP 1
+#endif
+__device__ __forceinline__ float ln_row_sum(float v) {
+#if DADMM_LN_DPP
+    return wave_sum_dpp(v);
+#else
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+#endif
+}
 
 
 // sign(y) * t exactly as torch's eager ops give it (sign(+-0) = sign(NaN) = 0, so +0 there, else
