@@ -41,6 +41,12 @@ constexpr int RING = 8;           // row steps (4 rows each) of operands in flig
 #ifndef DADMM_WGRAD2
 #define DADMM_WGRAD2 1            // 0: wgrad_kernel (32 x 32 tiles, 16x16x4 MFMA) for A/B builds
 #endif
+#ifndef DADMM_W2_FILL
+#define DADMM_W2_FILL 1           // wgrad2 row splits: one full round of workgroups (0: powers of two)
+#endif
+#ifndef DADMM_W2_SLOTS
+#define DADMM_W2_SLOTS 768        // wgrad2 workgroups resident at once (256 CUs x 3)
+#endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -580,6 +586,17 @@ int wgrad_splits(int R, int N, int K) {
         const long steps = ((long)R + 1) / 2;
         int s = 1;
         while (tiles * s * 2 <= 1024 && steps / (hgrad::W2_WAVES * s * 2) >= 64 && s < 64) s *= 2;
+        // A grid past one round of resident workgroups (256 CUs x 3: 80 VGPRs + 64 AGPRs hold 3
+        // waves per SIMD) ran its last 16-128 workgroups as a second round (784 for a 400 x 400
+        // weight, 896 for 400 x 200): such grids split to fill one round exactly instead, each
+        // wave walking >= 32 row pairs. (Filling the smaller grids too, 512 -> 768 workgroups for
+        // the 100 x 512 layer, measured slower: 87 vs 78 us.)
+        if (DADMM_W2_FILL && tiles * s > DADMM_W2_SLOTS) {
+            long f = DADMM_W2_SLOTS / tiles;
+            const long fmax = steps / (hgrad::W2_WAVES * 32);
+            f = f < fmax ? f : fmax;
+            return f > 1 ? (int)f : 1;
+        }
         return s;
     }
     const int tiles = ((N + hgrad::TN - 1) / hgrad::TN) * ((K + hgrad::TK - 1) / hgrad::TK);
