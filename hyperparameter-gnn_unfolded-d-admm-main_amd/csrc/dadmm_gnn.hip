@@ -72,6 +72,10 @@ constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
 #ifndef DADMM_GRAM_G2ALL
 #define DADMM_GRAM_G2ALL 1
 #endif
+// gram_kernel<true> (round 5) for grids of <= 2 items per CU at m_pad = 64, n_pad = 256
+#ifndef DADMM_GRAM_SMALL
+#define DADMM_GRAM_SMALL 1
+#endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -141,6 +145,12 @@ __global__ __launch_bounds__(THREADS) void check0_kernel(GnnArgs a, const float*
 // ---- gram: out = A^T (A x) per agent (mode 0), out = A^T b (mode 1), out += A^T (A x) (mode 2) --
 // item = (16-sample tile, agent p); x is y_k resolved through the guard flags (x_raw == nullptr)
 // or the raw operand x_raw (the adjoints' gradient operands).
+// SMALL (gram_small: a grid of at most two items per CU, m_pad = 64, n_pad = 256, mode != 1): the
+// same chains as the general form, with every operand load issued up front — the A rows, A^T rows
+// and (mode 2) out rows before the guard-flag walk that names x, then all 16 column steps of x —
+// so each wave waits on memory once before GEMM1 instead of once per ring refill and again for the
+// A^T rows after the barrier. Bit-identical (the chains and their order are unchanged).
+template <bool SMALL>
 __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const float* x_raw,
                                                        float* out, int mode) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -152,6 +162,85 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
     const int j = lane & 15, h = lane >> 4;
     const int s = tile * BT + j;
     const bool sv = s < B;
+
+    if constexpr (SMALL) {
+        // (host: m = 64 exactly, so every wave owns one live m-block and no load sits under a branch)
+        constexpr int T = 16, MB = 4;   // column steps of x (n_pad = 256), m-blocks (m_pad = 64)
+        // x's source first: the guard flag of iteration k - 1 and the table entry it names, issued
+        // before the operator loads so that their wait does not include them
+        const bool walk_x = x_raw == nullptr;
+        const bool prev = walk_x && k >= 1;
+        // the flag word through a descriptor whose range is empty when there is no k - 1 (reads 0,
+        // touches nothing); flags written by earlier launches are visible at this launch's start
+        const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<int32_t*>(a.flags), 0, prev ? 4 * (GNN_F_YNB(k - 1) + 1) : 0, 0x00020000);
+        const int f_raw = __builtin_amdgcn_raw_buffer_load_b32(rf, prev ? 4 * GNN_F_YNB(k - 1) : 0, 0, 0);
+        const float* y_prev = nullptr;
+        if (prev) y_prev = a.yptr[k];
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 ar[T], at_all[MB][4], oall[MB];
+        const float* arow = a.A + ((size_t)p * 64 + 16 * w + j) * 256 + 4 * h;
+#pragma unroll
+        for (int u = 0; u < T; ++u) ar[u] = *(const f32x4*)(arow + 16 * u);
+        // GEMM2's units: n-tiles w, w + 4, w + 8, w + 12 (one m-group)
+        const float* atb = a.At + ((size_t)p * 256 + j) * 64 + 4 * h;
+        const __amdgpu_buffer_rsrc_t ro =
+            __builtin_amdgcn_make_buffer_rsrc(out, 0, mode == 2 ? (int)((size_t)B * P * n * 4) : 0, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < MB; ++u) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) at_all[u][t] = *(const f32x4*)(atb + (size_t)16 * (w + WAVES * u) * 64 + 16 * t);
+            const int n0 = 16 * (w + WAVES * u) + 4 * h;
+            const uint32_t off = (sv && n0 < n) ? (uint32_t)((((size_t)s * P + p) * n + n0) * 4) : 0x80000000u;
+            oall[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ro, off, 0, 0));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bool zero = false;
+        const float* xs = !walk_x ? x_raw
+                        : (prev && __builtin_amdgcn_readfirstlane(f_raw) == 0) ? y_prev : y_source(a, k, zero);
+        {   // wave-uniform (scalar) pointer and guard: the descriptor below must live in SGPRs
+            const uint64_t xa = (uint64_t)xs;
+            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xa);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xa >> 32));
+            xs = (const float*)(((uint64_t)hi << 32) | lo);
+            zero = __builtin_amdgcn_readfirstlane((int)zero) != 0;
+        }
+        const uint32_t xbytes = zero ? 0u : (uint32_t)((size_t)B * P * n * 4);
+        const __amdgpu_buffer_rsrc_t rx =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), 0, (int)xbytes, 0x00020000);
+        const uint32_t xoff = sv ? (uint32_t)((((size_t)s * P + p) * n + 4 * h) * 4) : 0x80000000u;
+        f32x4 xr[T];
+#pragma unroll
+        for (int u = 0; u < T; ++u)
+            xr[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rx, 16 * u + 4 * h < n && sv ? xoff + 64u * u : 0x80000000u, 0, 0));
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int u = 0; u < T; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc = mfma4(ar[u][r], xr[u][r], acc);
+        *(f32x4*)(Rlds + j * RS + 16 * w + 4 * h) = acc;
+        __syncthreads();
+        f32x4 rv0[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) rv0[t] = *(const f32x4*)(Rlds + j * RS + 16 * t + 4 * h);
+#pragma unroll
+        for (int u = 0; u < MB; ++u) {
+            f32x4 g = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) g = mfma4(at_all[u][t][r], rv0[t][r], g);
+            const int n0 = 16 * (w + WAVES * u) + 4 * h;
+            if (sv && n0 < n) {
+                f32x4 v = mode == 2 ? oall[u] + g : g;
+                if (mode == 2 && a.acc_add != nullptr) v = v + *(const f32x4*)(a.acc_add + ((size_t)s * P + p) * n + n0);
+                *(f32x4*)(out + ((size_t)s * P + p) * n + n0) = v;
+            }
+        }
+        return;
+    }
 
 #if DADMM_GRAM_XLDS
     if (mode != 1 && MP <= 16 * WAVES * GQ_MAX) {
@@ -1279,12 +1368,17 @@ item_kernel:
     }
     const size_t lds = gnn_gram_lds(a.m_pad);
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)gnn::gram_kernel,
+        hipError_t e = hipFuncSetAttribute((const void*)gnn::gram_kernel<false>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
     const int items = ((a.B + BT - 1) / BT) * a.P;
-    hipLaunchKernelGGL(gnn::gram_kernel, dim3(items), dim3(gnn::THREADS), lds, st, a, k, x_raw, out,
+    if (DADMM_GRAM_SMALL && mode != 1 && a.m == 64 && a.m_pad == 64 && a.n_pad == 256 && items <= 512) {
+        hipLaunchKernelGGL(gnn::gram_kernel<true>, dim3(items), dim3(gnn::THREADS), lds, st, a, k, x_raw, out,
+                           mode);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(gnn::gram_kernel<false>, dim3(items), dim3(gnn::THREADS), lds, st, a, k, x_raw, out,
                        mode);
     return hipGetLastError();
 }

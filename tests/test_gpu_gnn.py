@@ -88,6 +88,8 @@ def test_recurrence_bit_exact_given_hypernetwork_outputs(cuda, mode, per_sample)
     # enough (agent, tile) work for the LDS-resident gram (gram_lds_kernel): three m-blocks (m = 40),
     # n_pad > n, a partial last 16-sample tile and several tiles per workgroup
     (16, 40, 200, 1990, 2),
+    # the small-grid gram (gram_kernel<true>: m = 64, n_pad = 256, <= 512 items), partial last tile
+    (5, 64, 256, 40, 3),
 ])
 def test_recurrence_bit_exact_larger_shapes(cuda, P, m, n, B, K):
     """The update kernel's column blocks / agent-row pairs and the gram kernel's operand ring and
@@ -239,7 +241,7 @@ def test_features_are_the_reference_gram_and_atb(cuda):
     np.testing.assert_allclose(Atb.cpu().numpy(), want_b, rtol=1e-4, atol=1e-4 * np.abs(want_b).max())
 
 
-@pytest.mark.parametrize("P,m,n,B", [(4, 24, 48, 10), (16, 32, 256, 96), (50, 32, 1024, 40)])
+@pytest.mark.parametrize("P,m,n,B", [(4, 24, 48, 10), (16, 32, 256, 96), (50, 32, 1024, 40), (5, 64, 256, 40)])
 def test_gram_acc_equals_gram_plus_add(cuda, P, m, n, B):
     """dadmm_gnn_gram_acc (out += A^T A x, the adjoint's one-launch accumulation) == out + the
     gram of x, bit for bit, on the item kernel and the LDS-resident gram; with an addend, the bits
@@ -338,12 +340,14 @@ def test_guard_on_nonfinite_y0_bit_exact(cuda):
     assert np.array_equal(Y[..., 0].cpu().numpy(), Yo)
 
 
-@pytest.mark.parametrize("k_bad", [1, 3])
-def test_guard_on_nonfinite_ynext_bit_exact(cuda, k_bad):
+@pytest.mark.parametrize("k_bad,shape", [(1, (4, 16, 32, 8, 5)), (3, (4, 16, 32, 8, 5)),
+                                         (1, (5, 64, 256, 24, 4))])
+def test_guard_on_nonfinite_ynext_bit_exact(cuda, k_bad, shape):
     """A NaN alpha from the hypernetwork at iteration k_bad makes y_next non-finite: the
     reference keeps y_k and appends it (gnn_dlasso_models_progressive.py:235-237), so Y[k_bad]
-    must hold y_k, also when k_bad < K - 1 (the slot is rewritten by the next iteration)."""
-    P, m, n, B, K = 4, 16, 32, 8, 5
+    must hold y_k, also when k_bad < K - 1 (the slot is rewritten by the next iteration). The
+    m = 64, n = 256 shape runs the small-grid gram, whose x source then takes the flag walk."""
+    P, m, n, B, K = shape
     model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", True)
     model.eval()
     model.hyper_backend = "torch"
