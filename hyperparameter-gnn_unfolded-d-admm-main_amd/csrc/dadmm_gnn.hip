@@ -72,6 +72,10 @@ constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
 #ifndef DADMM_GRAM_G2ALL
 #define DADMM_GRAM_G2ALL 1
 #endif
+// update_item: the guard flags and y_k's table entry loaded together (round 5)
+#ifndef DADMM_STEP_EARLY
+#define DADMM_STEP_EARLY 1
+#endif
 // gram_kernel<true> (round 5) for grids of <= 2 items per CU at m_pad = 64, n_pad = 256
 #ifndef DADMM_GRAM_SMALL
 #define DADMM_GRAM_SMALL 1
@@ -783,11 +787,23 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     const bool cv = c < n;
     const size_t base = (size_t)s * P * n + (cv ? c : 0);
     bool yzero = false;
+    // the guard words and the table entry y_k comes from in the common case, issued together
+    // (DADMM_STEP_EARLY; y_source's walk only when the k - 1 guard fired): one round trip before
+    // the visit lists instead of the walk's flag -> table -> flag chain
+#if DADMM_STEP_EARLY
+    const int f_prev = k > 0 ? __builtin_amdgcn_readfirstlane(flag_ld(a.flags + GNN_F_YNB(k - 1))) : 0;
+    const int f_u = __builtin_amdgcn_readfirstlane(flag_ld(a.flags + GNN_F_UBAD(k)));
+    float* const y_prev = a.yptr[k];
+    const float* __restrict__ ys = (k > 0 && f_prev == 0) ? y_prev : y_source(a, k, yzero);
+    const bool uzero = f_u != 0;
+    float* const fix = (FUSED && k > 0 && f_prev != 0) ? y_prev : nullptr;
+#else
     const float* __restrict__ ys = y_source(a, k, yzero);
     const bool uzero = flag_ld(a.flags + GNN_F_UBAD(k)) != 0;
     // the y_next guard of iteration k - 1 fired: Y[k-1] (= yptr[k], which holds the rejected
     // y_next) is rewritten with y_k
     float* const fix = (FUSED && k > 0 && flag_ld(a.flags + GNN_F_YNB(k - 1)) != 0) ? a.yptr[k] : nullptr;
+#endif
     float gclip, vclip;
     clips(a, k, gclip, vclip);
     float* yl = lds;                                  // [P][UCB] y_{k+1}
