@@ -44,6 +44,9 @@ constexpr int RING = 8;           // row steps (4 rows each) of operands in flig
 #ifndef DADMM_W2_FILL
 #define DADMM_W2_FILL 1           // wgrad2 row splits: one full round of workgroups (0: powers of two)
 #endif
+#ifndef DADMM_W2_SHORT
+#define DADMM_W2_SHORT 1          // wgrad2: short row walks on small grids split further
+#endif
 #ifndef DADMM_W2_SLOTS
 #define DADMM_W2_SLOTS 768        // wgrad2 workgroups resident at once (256 CUs x 3)
 #endif
@@ -496,7 +499,16 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(const float* __restrict
     if (idx >= count) return;
     float v = beta ? dst[idx] : 0.0f;
     float s = 0.0f;
-    for (int k = 0; k < splits; ++k) s += src[(size_t)k * count + idx];
+    // eight partials' loads in flight at a time, added in split order (the sum is unchanged)
+    int k = 0;
+    for (; k + 8 <= splits; k += 8) {
+        float p[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) p[u] = src[(size_t)(k + u) * count + idx];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += p[u];
+    }
+    for (; k < splits; ++k) s += src[(size_t)k * count + idx];
     dst[idx] = v + s;
 }
 
@@ -585,7 +597,25 @@ int wgrad_splits(int R, int N, int K) {
         const long tiles = (long)((N + hgrad::W2_T - 1) / hgrad::W2_T) * ((K + hgrad::W2_T - 1) / hgrad::W2_T);
         const long steps = ((long)R + 1) / 2;
         int s = 1;
-        while (tiles * s * 2 <= 1024 && steps / (hgrad::W2_WAVES * s * 2) >= 64 && s < 64) s *= 2;
+        bool short_walk = false;   // the doubling stopped on the walk length, not the grid size
+        while (tiles * s * 2 <= 1024 && s < 64) {
+            if (steps / (hgrad::W2_WAVES * s * 2) < 64) {
+                short_walk = true;
+                break;
+            }
+            s *= 2;
+        }
+        // Short walks on a small grid (the output head's and the last decoder layer's gradients
+        // over B K rows: 16 and 64 workgroups whose waves walked ~100 row pairs at ~0.25 us each,
+        // the ring's memory round trips exposed): split further, to >= 16 row pairs per wave
+        // (28.8 -> 15.7 and 25.6 -> 15.6 us at B = 256). Grids of 224-512 workgroups measured no
+        // faster or slower split.
+        if (DADMM_W2_SHORT && short_walk && tiles * s <= 128) {
+            long f = DADMM_W2_SLOTS / tiles;
+            const long fmax = steps / (hgrad::W2_WAVES * 16);
+            f = f < fmax ? f : fmax;
+            if (f > s) return (int)f;
+        }
         // A grid past one round of resident workgroups (256 CUs x 3: 80 VGPRs + 64 AGPRs hold 3
         // waves per SIMD) ran its last 16-128 workgroups as a second round (784 for a 400 x 400
         // weight, 896 for 400 x 200): such grids split to fill one round exactly instead, each

@@ -17,12 +17,20 @@ UNIFORM_FORM = False
 
 
 def _splits(R, N, K):
-    """wgrad_splits: powers of two, or (DADMM_W2_FILL) a grid past 768 workgroups refilled to one
-    round of 768, >= 32 row pairs per wave."""
+    """wgrad_splits: powers of two; (DADMM_W2_SHORT) a short walk on a small grid split to >= 16
+    row pairs per wave within 768 workgroups; (DADMM_W2_FILL) a grid past 768 refilled to 768,
+    >= 32 row pairs per wave."""
     tiles = ((N + W2_T - 1) // W2_T) * ((K + W2_T - 1) // W2_T)
-    steps, s = (R + 1) // 2, 1
-    while tiles * s * 2 <= 1024 and steps // (WAVES * s * 2) >= 64 and s < 64:
+    steps, s, short = (R + 1) // 2, 1, False
+    while tiles * s * 2 <= 1024 and s < 64:
+        if steps // (WAVES * s * 2) < 64:
+            short = True
+            break
         s *= 2
+    if short and tiles * s <= 128:   # DADMM_W2_SHORT: >= 16 row pairs per wave, one round
+        f = min(768 // tiles, steps // (WAVES * 16))
+        if f > s:
+            return f
     if tiles * s > 768:
         return max(1, min(768 // tiles, steps // (WAVES * 32)))
     return s
@@ -149,6 +157,6 @@ def _fast_cursor_ok(R, nb, splits, W=WAVES, ring=RING):
 @pytest.mark.parametrize("R,nb,splits", [(20480, 25, 16), (4096, 25, 64), (1280, 25, 16), (510, 4, 1),
                                          (1280, 1, 2), (20480, 25, 8), (300, 3, 4), (16, 3, 1), (74, 2, 3),
                                          (1280, 25, 15), (1280, 25, 27), (256, 25, 3), (256, 25, 25),
-                                         (20480, 25, 15), (1280, 25, 96)])
+                                         (20480, 25, 15), (1280, 25, 96), (256, 25, 50), (256, 25, 27)])
 def test_wgrad2_fast_cursor_sequence(R, nb, splits):
     assert _fast_cursor_ok(R, nb, splits)
