@@ -47,9 +47,6 @@ constexpr int RING = 8;           // row steps (4 rows each) of operands in flig
 #ifndef DADMM_W2_SHORT
 #define DADMM_W2_SHORT 1          // wgrad2: short row walks on small grids split further
 #endif
-#ifndef DADMM_W2_SLOTS
-#define DADMM_W2_SLOTS 768        // wgrad2 workgroups resident at once (256 CUs x 3)
-#endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -589,6 +586,15 @@ hipError_t launch_transpose(const float* in, int rows, int cols, float* out, hip
 
 namespace {
 int wgrad_waves(int tiles) { return tiles >= 256 ? 4 : tiles >= 128 ? 8 : 16; }
+// wgrad2 workgroups resident at once: 3 per CU (80 VGPRs + 64 AGPRs hold 3 waves per SIMD) x the
+// current device's CU count, queried per call (256 CUs on MI355X: 768)
+long w2_slots() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    return 3L * cus;
+}
 }
 
 int wgrad_splits(int R, int N, int K) {
@@ -610,19 +616,20 @@ int wgrad_splits(int R, int N, int K) {
         // the ring's memory round trips exposed): split further, to >= 16 row pairs per wave
         // (28.8 -> 15.7 and 25.6 -> 15.6 us at B = 256). Grids of 224-512 workgroups measured no
         // faster or slower split.
+        const long slots = w2_slots();
         if (DADMM_W2_SHORT && short_walk && tiles * s <= 128) {
-            long f = DADMM_W2_SLOTS / tiles;
+            long f = slots / tiles;
             const long fmax = steps / (hgrad::W2_WAVES * 16);
             f = f < fmax ? f : fmax;
             if (f > s) return (int)f;
         }
-        // A grid past one round of resident workgroups (256 CUs x 3: 80 VGPRs + 64 AGPRs hold 3
+        // A grid past one round of resident workgroups (w2_slots(): 3 per CU, 80 VGPRs + 64 AGPRs hold 3
         // waves per SIMD) ran its last 16-128 workgroups as a second round (784 for a 400 x 400
         // weight, 896 for 400 x 200): such grids split to fill one round exactly instead, each
         // wave walking >= 32 row pairs. (Filling the smaller grids too, 512 -> 768 workgroups for
         // the 100 x 512 layer, measured slower: 87 vs 78 us.)
-        if (DADMM_W2_FILL && tiles * s > DADMM_W2_SLOTS) {
-            long f = DADMM_W2_SLOTS / tiles;
+        if (DADMM_W2_FILL && tiles * s > slots) {
+            long f = slots / tiles;
             const long fmax = steps / (hgrad::W2_WAVES * 32);
             f = f < fmax ? f : fmax;
             return f > 1 ? (int)f : 1;

@@ -75,6 +75,17 @@ def tag_status(Y: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
     return Y
 
 
+def timed_out(Y: torch.Tensor) -> bool:
+    """True if ``Y`` (iterates, or the losses compute_loss made from them) came from a forward
+    whose guarded recomputation could not synchronise its grid (one host synchronisation; False
+    when the tensor carries no status). Multi-rank callers pass it through the collective that
+    follows (dist.global_losses(..., timed_out=...)) so every rank raises together."""
+    status = getattr(Y, "_dadmm_status", None)
+    if status is None:
+        return False
+    return bool(int(status.item()) & _lib.STATUS_BARRIER_TIMEOUT)
+
+
 def raise_if_timed_out(Y: torch.Tensor) -> None:
     """GuardTimeoutError if ``Y`` (iterates, or the losses compute_loss made from them) came from
     a forward whose guarded recomputation could not synchronise its grid (one host

@@ -47,16 +47,29 @@ def shard(t: torch.Tensor, rank: int = None, world_size: int = None):
     return t[lo:hi]
 
 
-def global_losses(loss_mean: torch.Tensor, loss_final: torch.Tensor, n_local: int):
+def global_losses(loss_mean: torch.Tensor, loss_final: torch.Tensor, n_local: int,
+                  timed_out: bool = None):
     """(loss_mean, loss_final) of the whole batch from this rank's shard losses: shard-size
     weighted mean, one all_reduce of 3 values. Returns detached 0-dim tensors (host-side logging
-    / scheduler use, like the reference's ``.item()`` sums, unfolded_train_new.py:82)."""
-    buf = torch.stack([loss_mean.detach().double() * n_local,
-                       loss_final.detach().double() * n_local,
-                       torch.tensor(float(n_local), dtype=torch.float64,
-                                    device=loss_mean.device)])
+    / scheduler use, like the reference's ``.item()`` sums, unfolded_train_new.py:82).
+
+    ``timed_out`` (this rank's forward had a guard-recomputation timeout, autograd.timed_out):
+    the flag rides in the same all_reduce, and EVERY rank raises GuardTimeoutError after the
+    collective when any rank set it (a rank raising before the collective would leave the others
+    blocked in it)."""
+    vals = [loss_mean.detach().double() * n_local, loss_final.detach().double() * n_local,
+            torch.tensor(float(n_local), dtype=torch.float64, device=loss_mean.device)]
+    if timed_out is not None:
+        vals.append(torch.tensor(1.0 if timed_out else 0.0, dtype=torch.float64,
+                                 device=loss_mean.device))
+    buf = torch.stack(vals)
     if world()[1] > 1:
         dist.all_reduce(buf)
+    if timed_out is not None and float(buf[3]) > 0:
+        from .autograd import GuardTimeoutError
+        raise GuardTimeoutError(
+            f"the guarded recomputation timed out on {int(float(buf[3]))} rank(s): "
+            "stepwise grid barrier timed out, Y is invalid (device shared with other work)")
     return buf[0] / buf[2], buf[1] / buf[2]
 
 

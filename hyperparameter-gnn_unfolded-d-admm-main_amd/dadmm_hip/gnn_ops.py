@@ -123,11 +123,14 @@ class GnnRun:
 
 def _stage_status(run: GnnRun):
     """After the forward's finish: the status word copied to pinned host memory behind an event,
-    so that the backward can read it without draining the stream (_check_guards)."""
+    so that the backward can read it without draining the stream (_check_guards). The copy and
+    the event go on run.dev's current stream (the one the forward ran on), whichever device is
+    current for the caller."""
     run.status_host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-    run.status_host.copy_(run.status, non_blocking=True)
-    run.status_event = torch.cuda.Event()
-    run.status_event.record()
+    with torch.cuda.device(run.dev):
+        run.status_host.copy_(run.status, non_blocking=True)
+        run.status_event = torch.cuda.Event()
+        run.status_event.record(torch.cuda.current_stream(run.dev))
 
 
 def _check_guards(run: GnnRun):

@@ -48,7 +48,7 @@ import configurations  # noqa: E402
 import gnn_dlasso_models_progressive  # noqa: E402
 import gnn_dlasso_utils  # noqa: E402
 from dadmm_hip import dist as D  # noqa: E402
-from dadmm_hip.autograd import raise_if_timed_out  # noqa: E402
+from dadmm_hip.autograd import timed_out  # noqa: E402
 from dadmm_hip.graph import generate_er, ingest  # noqa: E402
 
 MIN_ITERATIONS = 1        # gnn_dlasso_progressive.py:73
@@ -211,9 +211,10 @@ def main(argv=None):
                 loss_mean, loss_final = gnn_dlasso_utils.compute_loss(Y, x_va[sel])
                 # a timed-out guard recomputation makes the losses NaN: stop here with the
                 # error instead of feeding NaN to the scheduler and the checkpoint test (the
-                # float() below synchronises anyway)
-                raise_if_timed_out(loss_final)
-                gm, gf = D.global_losses(loss_mean, loss_final, hi - lo)
+                # float() below synchronises anyway); the flag rides in the loss all_reduce, so
+                # every rank raises together
+                gm, gf = D.global_losses(loss_mean, loss_final, hi - lo,
+                                         timed_out=timed_out(loss_final))
                 vm += float(gm)
                 vf += float(gf)
                 nb += 1

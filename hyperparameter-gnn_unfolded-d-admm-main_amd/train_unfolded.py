@@ -39,7 +39,7 @@ import configurations  # noqa: E402
 import gnn_dlasso_utils  # noqa: E402
 import unfolded_DLASSO  # noqa: E402
 from dadmm_hip import dist as D  # noqa: E402
-from dadmm_hip.autograd import raise_if_timed_out  # noqa: E402
+from dadmm_hip.autograd import timed_out  # noqa: E402
 
 
 def _dataset(A, size, args, gen):
@@ -68,7 +68,8 @@ def _inits(args, bs, lo, hi, device):
 def validate(model, b_va, x_va, graph, args, bs, gen, rank, world, device):
     """The epoch's validation loss (global over ranks) and the last batch's hyp. A timed-out
     guard recomputation (NaN losses, compute_loss) raises GuardTimeoutError here instead of
-    reaching the scheduler and the checkpoint test as NaN (the float() syncs anyway)."""
+    reaching the scheduler and the checkpoint test as NaN (the float() syncs anyway); the flag
+    goes through the loss all_reduce, so all ranks raise together."""
     model.eval()
     hyp = None
     with torch.no_grad():
@@ -78,8 +79,9 @@ def validate(model, b_va, x_va, graph, args, bs, gen, rank, world, device):
             sel = idx[lo:hi].to(device)
             Y, hyp = model(b_va[sel], [graph] * (hi - lo), inits=_inits(args, bs, lo, hi, device))
             loss_mean, loss_final = gnn_dlasso_utils.compute_loss(Y, x_va[sel])
-            raise_if_timed_out(loss_final)
-            tot += float(D.global_losses(loss_mean, loss_final, hi - lo)[1])
+            # the timeout flag rides in the loss all_reduce: every rank raises together
+            tot += float(D.global_losses(loss_mean, loss_final, hi - lo,
+                                         timed_out=timed_out(loss_final))[1])
             nb += 1
     return tot / max(nb, 1), hyp
 

@@ -143,3 +143,36 @@ def test_single_process_is_identity():
     assert torch.equal(p.grad, torch.full((3,), 2.0))
     gm, gf = D.global_losses(torch.tensor(0.5), torch.tensor(0.25), 5)
     assert float(gm) == 0.5 and float(gf) == 0.25
+
+
+def _timeout_worker(rank, world, port, out_path):
+    """Rank 1's forward timed out, rank 0's did not: both must raise after the collective."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    r, w, _ = D.init_from_env("gloo")
+    from dadmm_hip import _lib
+    from dadmm_hip.autograd import GuardTimeoutError, tag_status, timed_out
+    bits = _lib.STATUS_BARRIER_TIMEOUT if r == 1 else 0
+    lf = tag_status(torch.tensor(0.5), torch.tensor([bits], dtype=torch.int32))
+    raised = False
+    try:
+        D.global_losses(torch.tensor(0.5), lf, 3, timed_out=timed_out(lf))
+    except GuardTimeoutError:
+        raised = True
+    # both ranks reach this second collective only if neither was left blocked in the first
+    flags = [torch.zeros(1) for _ in range(w)]
+    torch.distributed.all_gather(flags, torch.tensor([1.0 if raised else 0.0]))
+    if r == 0:
+        np.save(out_path, torch.cat(flags).numpy())
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_timeout_flag_raises_on_every_rank(tmp_path):
+    """a guard-recomputation timeout on ONE rank must not leave the others
+    blocked in the loss all_reduce: the flag rides in that collective and every rank raises."""
+    out = str(tmp_path / "to.npy")
+    mp.start_processes(_timeout_worker, args=(2, _free_port(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    assert np.load(out).tolist() == [1.0, 1.0]
