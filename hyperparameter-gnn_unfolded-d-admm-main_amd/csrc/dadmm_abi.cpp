@@ -195,6 +195,110 @@ int dadmm_forward_record(const dadmm_dims* d, const void* op, const float* b, co
                         status, stream, true);
 }
 
+// ---- the column-split forward (dadmm_split.hip) ----------------------------------------------
+namespace {
+int device_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    return cus;
+}
+struct SplitPlan {
+    int nt = 0, slices = 0, groups = 0, tiles = 0;
+    size_t flag_bytes = 0, bytes = 0;
+};
+// groups = 0: the split path does not serve d (shape, or a batch that fills more than half the CUs)
+SplitPlan split_plan(const dadmm_dims* d) {
+    SplitPlan sp;
+    if (d == nullptr || d->B <= 0 || d->K <= 0 || d->P < 1 || d->P > 6 || d->m < 1 ||
+        d->m > dadmm::M_PAD || d->n < 1 || (d->n & 3) != 0 || d->hyp_rows < 1)
+        return sp;
+    if ((size_t)d->B * d->P * d->n * 4 >= ((size_t)1 << 31)) return sp;
+    const int nt = dadmm::fused_nt(d->n);
+    if (nt != 2 && nt != 4) return sp;
+    const int cus = device_cus();
+    const int tiles = (d->B + dadmm::BT - 1) / dadmm::BT;
+    if (2 * tiles > cus) return sp;
+    const int S = 64 * nt / dadmm::SPLIT_COLS;
+    int groups = cus / S;
+    groups = groups < tiles ? groups : tiles;
+    if (groups < 1) return sp;
+    sp.nt = nt;
+    sp.slices = S;
+    sp.groups = groups;
+    sp.tiles = tiles;
+    sp.flag_bytes = ((size_t)groups * d->P * 4 * S * 4 + 4 + 255) / 256 * 256;
+    sp.bytes = (size_t)groups * 2 * d->P * 4 * S * 1024;
+    return sp;
+}
+}  // namespace
+
+size_t dadmm_split_scratch_bytes(const dadmm_dims* d) {
+    if (d == nullptr || check_dims(d) != DADMM_OK) return 0;
+    return split_plan(d).bytes;
+}
+
+size_t dadmm_split_flag_bytes(const dadmm_dims* d) {
+    if (d == nullptr || check_dims(d) != DADMM_OK) return 0;
+    return split_plan(d).flag_bytes;
+}
+
+int dadmm_forward_split(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
+                        const uint32_t* nbr_order, const float* deg, const float* hyp,
+                        const float* y0, const float* U0, const float* d0, float* Y, float* U_out,
+                        int32_t* status, void* flags, void* scratch, void* stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (d->B == 0 || d->K == 0) return ok();
+    if (!op || !b || !nbr || !deg || !hyp || !y0 || !U0 || !d0 || !Y || !flags || !scratch)
+        return fail(DADMM_EINVAL, "a required pointer is NULL");
+    if (!aligned16(op) || !aligned16(Y) || !aligned16(y0) || !aligned16(U0) || !aligned16(d0) ||
+        !aligned16(flags) || !aligned16(scratch) || (U_out != nullptr && !aligned16(U_out)))
+        return fail(DADMM_EINVAL, "op, Y, y0, U0, d0, U_out, flags and scratch must be 16-byte aligned");
+    int graph = 0, nt = 0;
+    if ((rc = check_fused_shape(d, nbr_order, &graph, &nt)) != DADMM_OK) return rc;
+    const SplitPlan sp = split_plan(d);
+    if (sp.groups == 0)
+        return fail(DADMM_EUNSUPPORTED, "the column-split forward does not serve B=%d P=%d n=%d "
+                    "(n_pad 128 or 256, P <= 6, ceil(B/16) <= CUs/2)", d->B, d->P, d->n);
+    dadmm::split_fn_ptr fn = dadmm::find_split(d->P, nt, graph);
+    if (fn == nullptr)
+        return fail(DADMM_EUNSUPPORTED, "no split kernel for P=%d n_pad=%d", d->P, 64 * nt);
+    const int np = 64 * nt;
+    dadmm::SplitArgs sa;
+    dadmm::FusedArgs& a = sa.f;
+    a.A = (const float*)op;
+    a.At = a.A + (size_t)d->P * m_pad_of(d) * np;
+    a.b = b;
+    a.nbr = nbr;
+    a.nbr_order = nbr_order;
+    a.deg = deg;
+    a.hyp = hyp;
+    a.y0 = y0;
+    a.U0 = U0;
+    a.d0 = d0;
+    a.Y = Y;
+    a.U_out = U_out;
+    a.status = status;
+    a.Grec = nullptr;
+    a.Urec = nullptr;
+    a.B = d->B;
+    a.m = d->m;
+    a.n = d->n;
+    a.K = d->K;
+    a.hyp_rows = d->hyp_rows;
+    a.variant = d->variant;
+    sa.xflag = (uint32_t*)flags;
+    sa.xbuf = (float*)scratch;
+    sa.groups = sp.groups;
+    sa.tiles = sp.tiles;
+    sa.spin_ticks = 20000000ull;   // 0.2 s at the 100 MHz s_memrealtime clock
+    hipError_t e = fn(sa, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(DADMM_EHIP, "split launch: %s", hipGetErrorString(e));
+    return ok();
+}
+
 size_t dadmm_backward_scratch_bytes(const dadmm_dims* d) {
     if (check_dims(d) != DADMM_OK) return 0;
     const size_t nwg = ((size_t)d->B + dadmm::BT - 1) / dadmm::BT;

@@ -100,6 +100,20 @@ fused_fn_ptr find_fused_rec(int P, int nt, int graph);
 // hold (it serves n_pad = 256 with P = 4 or 5, shared or per-sample ascending graphs).
 fused_fn_ptr find_resident(int P, int nt, int graph);
 
+// ---- the column-split forward for small batches (dadmm_split.hip) ------------------------------
+constexpr int SPLIT_COLS = 64;   // columns of n_pad per slice (one workgroup each)
+struct SplitArgs {
+    FusedArgs f;         // as the fused kernel (U_out / status optional; no recording)
+    float* xbuf;         // [groups][2][P][4][S][256] GEMM1 partial tiles (no initialisation)
+    uint32_t* xflag;     // [groups][P][4][S] epoch words + 1 abort word: ZEROED before every launch
+    int groups;          // workgroup groups (S blocks each); grid = groups * S <= CUs
+    int tiles;           // ceil(B / BT) 16-sample tiles, walked g, g + groups, ...
+    uint64_t spin_ticks; // bound on one wait (s_memrealtime ticks, 100 MHz) before the abort
+};
+typedef hipError_t (*split_fn_ptr)(const SplitArgs&, hipStream_t);
+// P = 1..6, n_pad = 64 * nt with nt in {2, 4}; nullptr otherwise
+split_fn_ptr find_split(int P, int nt, int graph);
+
 // ---- adjoint (dadmm_backward.hip) ---------------------------------------------------------------
 struct BackwardArgs {
     const float* A;      // prepared operator [P][M_PAD][n_pad]

@@ -13,12 +13,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8
 STATUS_BARRIER_TIMEOUT = 0x100
-STATUS_RECOMPUTE = 16      # ungated fused kernel only: asymmetric shared adjacency
+STATUS_RECOMPUTE = 16      # ungated fused kernel: asymmetric shared adjacency; split: a wait timed out
 GATE_ON, FLAGS_ZEROED = 1, 2
 
 # every symbol include/dadmm.h declares
@@ -29,6 +29,9 @@ EXPORTED_SYMBOLS = (
     "dadmm_prepare_operator",
     "dadmm_forward",
     "dadmm_forward_record",
+    "dadmm_split_scratch_bytes",
+    "dadmm_split_flag_bytes",
+    "dadmm_forward_split",
     "dadmm_stepwise_scratch_bytes",
     "dadmm_forward_stepwise",
     "dadmm_backward_scratch_bytes",
@@ -170,6 +173,12 @@ def load() -> ctypes.CDLL:
     L.dadmm_prepare_operator.argtypes = [ctypes.POINTER(Dims), vp, vp, vp]
     L.dadmm_forward.restype = ctypes.c_int
     L.dadmm_forward.argtypes = [ctypes.POINTER(Dims)] + [vp] * 13
+    L.dadmm_split_scratch_bytes.restype = ctypes.c_size_t
+    L.dadmm_split_scratch_bytes.argtypes = [ctypes.POINTER(Dims)]
+    L.dadmm_split_flag_bytes.restype = ctypes.c_size_t
+    L.dadmm_split_flag_bytes.argtypes = [ctypes.POINTER(Dims)]
+    L.dadmm_forward_split.restype = ctypes.c_int
+    L.dadmm_forward_split.argtypes = [ctypes.POINTER(Dims)] + [vp] * 15
     L.dadmm_stepwise_scratch_bytes.restype = ctypes.c_size_t
     L.dadmm_stepwise_scratch_bytes.argtypes = [ctypes.POINTER(Dims)]
     L.dadmm_forward_stepwise.restype = ctypes.c_int

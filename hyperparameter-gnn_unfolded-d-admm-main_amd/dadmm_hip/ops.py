@@ -110,11 +110,12 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     """The K-step forward with the reference's NaN/Inf guards, enqueued on the current stream
     (no host synchronisation). Shapes: b [B,P,m], hyp [K,H,4], y0/U0/d0 [B,P,n].
 
-    path "auto": the fused kernel when the shape is compiled, otherwise the tiled kernel (one
-    launch per iteration); either is followed by the device-gated stepwise recomputation (runs only
-    if a guard event was flagged). Training (record) outside the fused shapes: the stepwise
-    kernels, or the streamed single launch where it applies (P <= 16, m <= 64). "fused" / "tiled" / "stepwise" force one path ("fused" / "tiled" alone do NOT apply
-    the guards: their status only flags them).
+    path "auto": the fused kernel when the shape is compiled (its column-split form,
+    dadmm_forward_split, for batches that fill at most half the CUs: GEMM1 in the split order,
+    ``split_cols``), otherwise the tiled kernel (one launch per iteration); either is followed by
+    the device-gated stepwise recomputation (runs only if a guard event was flagged). Training (record) outside the fused shapes: the stepwise
+    kernels, or the streamed single launch where it applies (P <= 16, m <= 64). "fused" / "split" / "tiled" / "stepwise" force one path ("fused" / "split" / "tiled"
+    alone do NOT apply the guards: their status only flags them).
 
     record: also store the trajectory the adjoint consumes (training; dadmm_forward_record).
 
@@ -127,7 +128,7 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     draw = y0 is None
     if draw != (U0 is None) or draw != (d0 is None):
         raise ValueError("pass all of y0, U0, d0 or none of them")
-    if path not in ("auto", "fused", "tiled", "stepwise"):
+    if path not in ("auto", "fused", "split", "tiled", "stepwise"):
         raise ValueError(f"unknown path {path!r}")
     B, P, m = b.shape
     if P != op.P or m != op.m:
@@ -146,17 +147,27 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
         Urec = torch.empty((K, B, P, ns), dtype=torch.float32, device=b.device)
     d = op.dims(B=B, K=K, variant=variant, hyp_rows=H, graph_shared=graphs.shared)
     L = _lib.load()
-    if path == "fused" and not graphs.fused_ok:
+    if path in ("fused", "split") and not graphs.fused_ok:
         raise ValueError("the fused kernel follows non-ascending adjacency orders only for "
                          "P <= 8; use path='auto' or 'stepwise'")
-    # one device allocation: [status word | 252 B pad | stepwise scratch (guard flags first)];
-    # the prologue zeroes the status word and the flags in the same launch as the draws
+    # small batches (the fused tiles would fill at most half the CUs): the column-split forward
+    split_b = 0
+    if path in ("auto", "split") and not record and graphs.fused_ok:
+        split_b = L.dadmm_split_scratch_bytes(ctypes.byref(d))
+    if path == "split" and split_b == 0:
+        raise ValueError(f"the column-split forward does not serve B={B} P={P} n={ns} "
+                         "(n_pad 128 or 256, P <= 6, m <= 64, ceil(B/16) <= CUs/2)")
+    flag_b = L.dadmm_split_flag_bytes(ctypes.byref(d)) if split_b else 0
+    # one device allocation: [status word | 252 B pad | split epoch words | stepwise scratch
+    # (guard flags first)]; the prologue zeroes the status word, the epoch words and the guard
+    # flags in the same launch as the draws
     gated = path in ("auto", "stepwise")
     nbytes = L.dadmm_stepwise_scratch_bytes(ctypes.byref(d)) if gated else 0
-    words = torch.empty(256 + max(nbytes, 256), dtype=torch.uint8, device=b.device)
+    words = torch.empty(256 + flag_b + max(nbytes, 256), dtype=torch.uint8, device=b.device)
     status = words[:4].view(torch.int32)
-    scratch = words[256:]
-    nzero = (256 + (_sw_flag_bytes(K) if gated else 0)) // 4
+    sflags = words[256:256 + flag_b]
+    scratch = words[256 + flag_b:]
+    nzero = (256 + flag_b + (_sw_flag_bytes(K) if gated else 0)) // 4
     if draw:
         y0, U0, d0 = draw_inits((B, P, op.n), b.device, ns, zero=words, nzero=nzero)
     else:
@@ -165,8 +176,14 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
                 0, 0, 0, 1, 1, 0.0, 0.0, None, None, None, _ptr(words), nzero, _stream(b.device)))
     with torch.cuda.device(b.device):
         stream = _stream(b.device)
-        fused = path in ("auto", "fused") and graphs.fused_ok
-        if fused:
+        fused = path in ("auto", "fused", "split") and graphs.fused_ok
+        if split_b:
+            xbuf = torch.empty(split_b, dtype=torch.uint8, device=b.device)
+            _lib.check("dadmm_forward_split", L.dadmm_forward_split(
+                ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.nbr), _ptr(graphs.order),
+                _ptr(graphs.deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U),
+                _ptr(status), _ptr(sflags), _ptr(xbuf), stream))
+        elif fused:
             if record:
                 rc = L.dadmm_forward_record(
                     ctypes.byref(d), _ptr(op.workspace), _ptr(b), _ptr(graphs.nbr),
@@ -220,6 +237,17 @@ def forward_raw(op: PreparedOperator, b: torch.Tensor, graphs: GraphBatch, hyp: 
     if record:
         return Y, U, status, traj
     return Y, U, status
+
+
+def split_cols(op: PreparedOperator, B: int, K: int, graphs: GraphBatch = None, hyp_rows: int = 1,
+               record: bool = False) -> int:
+    """The GEMM1 slice width forward_raw's "auto" path uses for this batch: 64 when it runs the
+    column-split forward (dadmm_forward_split), else 0 (the oracle's ``split_cols`` argument)."""
+    if record or (graphs is not None and not graphs.fused_ok):
+        return 0
+    shared = graphs.shared if graphs is not None else 1
+    d = op.dims(B=B, K=K, hyp_rows=hyp_rows, graph_shared=shared)
+    return 64 if _lib.load().dadmm_split_scratch_bytes(ctypes.byref(d)) else 0
 
 
 class Trajectory:

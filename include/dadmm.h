@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 17
+#define DADMM_ABI_VERSION 18
 
 enum {
     DADMM_OK = 0,
@@ -85,9 +85,10 @@ enum {
     DADMM_STATUS_GRAD_NAN = 4,       /* clamped gradient had NaN                     (:84)   */
     DADMM_STATUS_YNEXT_NAN = 8,      /* y_next had NaN/Inf                           (:102)  */
     DADMM_STATUS_RECOMPUTE = 16,     /* dadmm_forward only: the shared adjacency is not
-                                      * symmetric, so the fused consensus cannot follow it; the
-                                      * gated stepwise run recomputes the batch (never set after
-                                      * a gated run)                                          */
+                                      * symmetric, so the fused consensus cannot follow it;
+                                      * dadmm_forward_split: a wait between slices timed out;
+                                      * the gated stepwise run recomputes the batch (never set
+                                      * after a gated run)                                    */
     DADMM_STATUS_BARRIER_TIMEOUT = 0x100 /* gated stepwise run could not synchronise its grid
                                           * (device shared with other work): Y is invalid    */
 };
@@ -131,6 +132,28 @@ int dadmm_forward(const dadmm_dims* d, const void* op, const float* b, const uin
                   const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
                   const float* U0, const float* d0, float* Y, float* U_out, int32_t* status,
                   void* stream);
+
+/* The same forward for SMALL batches, columns split over workgroups (csrc/dadmm_split.hip).
+ * Replaces: the same reference lines as dadmm_forward (unfolded_DLASSO.py:45, 53-109).
+ * dadmm_forward's 16-sample tiles fill ceil(B / 16) CUs; here each tile's n_pad columns are cut
+ * into slices of 64, one workgroup each, with the operator slice resident in LDS and the GEMM1
+ * partial sums A_p[:, slice] y_p[slice] exchanged between the slices every iteration. GEMM1 is
+ * then R = ((c_0 + c_1) + c_2) + ... (slice 0's chain from -b, the others from +0), an order of
+ * its own: bit-identical to the oracle's oracle_forward_f32_split(split_cols = 64), not to
+ * dadmm_forward. Shapes: dadmm_forward's with n_pad = 128 or 256; applies when the batch fills at
+ * most half of the device's CUs (ceil(B / 16) <= CUs / 2): dadmm_split_scratch_bytes is 0 otherwise.
+ * `scratch`: dadmm_split_scratch_bytes(d) bytes (the partial sums), 16-byte aligned, any content;
+ * `flags`: dadmm_split_flag_bytes(d) bytes (the epoch words), 16-byte aligned, ZERO at every call
+ * (the prologue's `zero` words can clear them). A wait between slices is bounded: if the workgroups are not
+ * co-resident (the device shared with other work) the launch sets DADMM_STATUS_RECOMPUTE and the
+ * gated dadmm_forward_stepwise enqueued after it recomputes the batch exactly. Same outputs and
+ * `status` contract as dadmm_forward (no recording). */
+size_t dadmm_split_scratch_bytes(const dadmm_dims* d);
+size_t dadmm_split_flag_bytes(const dadmm_dims* d);
+int dadmm_forward_split(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
+                        const uint32_t* nbr_order, const float* deg, const float* hyp,
+                        const float* y0, const float* U0, const float* d0, float* Y, float* U_out,
+                        int32_t* status, void* flags, void* scratch, void* stream);
 
 /* dadmm_forward that also records the trajectory the adjoint (dadmm_backward) consumes — the
  * training-mode forward (the drivers call loss.backward() through it: unfolded_train_new.py:74-80).

@@ -22,6 +22,10 @@
  *                      reduction index visits 0,4,8,12,1,5,9,13,2,6,10,14,3,7,11,15 inside every
  *                      16-block (blocks ascending); GEMM1 chains start at -b, GEMM2 chains at +0;
  *                      every other operation rounds on its own, as the torch eager ops do.
+ *  oracle_forward_f32_split  the same with GEMM1 in the order of the column-split forward
+ *                      (dadmm_split.hip, small batches): the n columns cut into slices of
+ *                      split_cols; slice s's chain (same visiting order) starts at -b for s = 0
+ *                      and at +0 otherwise, and R = ((c_0 + c_1) + c_2) + ... left to right.
  *                      Built with -ffp-contract=off; fmaf is the C99 correctly rounded fma.
  *
  * compute_delta (:127-140) is restated literally for both: for p in 0..P-1, for q in
@@ -88,7 +92,7 @@ static int forward_f32_impl(int B, int P, int m, int n, int K, int variant, int 
                             const int32_t* nbr_idx, const float* deg, const float* hyp,
                             const float* y0, const float* U0, const float* d0, float* Y,
                             float* U_out, int32_t* status, float* Grec, float* Urec,
-                            int gram_mode) {
+                            int gram_mode, int split_cols) {
     if (B < 0 || P < 1 || m < 1 || n < 1 || K < 0 || (H != 1 && H != P)) return -1;
     const size_t S = (size_t)B * P * n;
     float* y = (float*)malloc(S * sizeof(float));
@@ -133,6 +137,21 @@ static int forward_f32_impl(int B, int P, int m, int n, int K, int variant, int 
                  * (gram_mode: R = A_p y_p from +0, b enters through Atb below) */
                 for (int i = 0; i < m; ++i) {
                     float acc = gram_mode ? 0.0f : -bp[i];
+                    if (split_cols > 0) {
+                        /* column-split order: one chain per slice, slice 0's from -b, the others
+                         * from +0, summed left to right */
+                        float r = 0.0f;
+                        for (int c0 = 0; c0 < npad; c0 += split_cols) {
+                            float part = c0 == 0 ? acc : 0.0f;
+                            for (int idx = c0; idx < c0 + split_cols && idx < npad; ++idx) {
+                                const int c = perm16(idx);
+                                if (c < n) part = fmaf(Ap[(size_t)i * n + c], yp[c], part);
+                            }
+                            r = c0 == 0 ? part : r + part;
+                        }
+                        R[i] = r;
+                        continue;
+                    }
                     for (int idx = 0; idx < npad; ++idx) {
                         const int c = perm16(idx);
                         if (c < n) acc = fmaf(Ap[(size_t)i * n + c], yp[c], acc);
@@ -231,7 +250,18 @@ int oracle_forward_f32(int B, int P, int m, int n, int K, int variant, int hyp_m
                        const float* y0, const float* U0, const float* d0, float* Y, float* U_out,
                        int32_t* status) {
     return forward_f32_impl(B, P, m, n, K, variant, hyp_mode, H, A, b, nbr_ptr, nbr_idx, deg, hyp,
-                            y0, U0, d0, Y, U_out, status, NULL, NULL, 0);
+                            y0, U0, d0, Y, U_out, status, NULL, NULL, 0, 0);
+}
+
+/* oracle_forward_f32 with GEMM1 in the column-split order (split_cols: a multiple of 16). */
+int oracle_forward_f32_split(int B, int P, int m, int n, int K, int variant, int hyp_mode, int H,
+                             const float* A, const float* b, const int32_t* nbr_ptr,
+                             const int32_t* nbr_idx, const float* deg, const float* hyp,
+                             const float* y0, const float* U0, const float* d0, float* Y,
+                             float* U_out, int32_t* status, int split_cols) {
+    if (split_cols < 0 || (split_cols & 15)) return -1;
+    return forward_f32_impl(B, P, m, n, K, variant, hyp_mode, H, A, b, nbr_ptr, nbr_idx, deg, hyp,
+                            y0, U0, d0, Y, U_out, status, NULL, NULL, 0, split_cols);
 }
 
 /* oracle_forward_f32 that also records the adjoint's trajectory (Grec, Urec: [K][B][P][n]). */
@@ -241,7 +271,7 @@ int oracle_forward_f32_rec(int B, int P, int m, int n, int K, int variant, int h
                            const float* y0, const float* U0, const float* d0, float* Y,
                            float* U_out, int32_t* status, float* Grec, float* Urec) {
     return forward_f32_impl(B, P, m, n, K, variant, hyp_mode, H, A, b, nbr_ptr, nbr_idx, deg, hyp,
-                            y0, U0, d0, Y, U_out, status, Grec, Urec, 0);
+                            y0, U0, d0, Y, U_out, status, Grec, Urec, 0, 0);
 }
 
 /* The GNN model's recurrence in the order of the per-iteration HIP path (dadmm_gnn.hip): gradient
@@ -253,7 +283,7 @@ int oracle_forward_f32_gram(int B, int P, int m, int n, int K, int variant, int 
                             const float* y0, const float* U0, const float* d0, float* Y,
                             float* U_out, int32_t* status) {
     return forward_f32_impl(B, P, m, n, K, variant, hyp_mode, H, A, b, nbr_ptr, nbr_idx, deg, hyp,
-                            y0, U0, d0, Y, U_out, status, NULL, NULL, 1);
+                            y0, U0, d0, Y, U_out, status, NULL, NULL, 1, 0);
 }
 
 /* ------------------------------------------------------------------------------------------ */

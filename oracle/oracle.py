@@ -48,6 +48,7 @@ def lib() -> ctypes.CDLL:
             f.argtypes = [i, i, i, i, i, i, i, i] + [fp] * 12
         L.oracle_forward_f32_rec.restype = ctypes.c_int
         L.oracle_forward_f32_rec.argtypes = [i, i, i, i, i, i, i, i] + [fp] * 14
+        L.oracle_forward_f32_split.argtypes = [i, i, i, i, i, i, i, i] + [fp] * 12 + [i]
         L.oracle_abi_version.restype = ctypes.c_int
         L.oracle_set_threads.restype = ctypes.c_int
         L.oracle_set_threads.argtypes = [i]
@@ -104,7 +105,7 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
-def _run(fn, out_dt, A, b, graph_list, hyp, y0, U0, d0, variant, hyp_mode, rec=None):
+def _run(fn, out_dt, A, b, graph_list, hyp, y0, U0, d0, variant, hyp_mode, rec=None, tail=()):
     A = _c(A, np.float32).reshape(A.shape[-3:]) if A.ndim == 4 else _c(A, np.float32)
     P, m, n = A.shape
     B = y0.shape[0]
@@ -128,18 +129,24 @@ def _run(fn, out_dt, A, b, graph_list, hyp, y0, U0, d0, variant, hyp_mode, rec=N
         rec[1] = np.empty((K, B, P, n), out_dt)
         extra = (_ptr(rec[0]), _ptr(rec[1]))
     rc = fn(B, P, m, n, K, variant, hyp_mode, H, _ptr(A), _ptr(b), _ptr(nbr_ptr), _ptr(nbr_idx),
-            _ptr(deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U), _ptr(st), *extra)
+            _ptr(deg), _ptr(hyp), _ptr(y0), _ptr(U0), _ptr(d0), _ptr(Y), _ptr(U), _ptr(st), *extra,
+            *tail)
     if rc != 0:
         raise RuntimeError(f"oracle returned {rc}")
     return Y, U, int(st[0])
 
 
-def forward_f32(A, b, graph_list, hyp, y0, U0, d0, variant=0, hyp_mode=0):
+def forward_f32(A, b, graph_list, hyp, y0, U0, d0, variant=0, hyp_mode=0, split_cols=0):
     """Order-matched fp32 restatement (bit-exact target of the HIP kernel).
 
     ``graph_list``: B networkx graphs, or a (nbr_ptr, nbr_idx, deg) CSR tuple (graph_arrays).
+    ``split_cols`` > 0: GEMM1 in the column-split order of the small-batch forward
+    (dadmm_split.hip; the split the library chose is ``dadmm_hip.ops.split_cols``).
 
     Returns (Y [K,B,P,n] float32, U_K [B,P,n] float32, guard status bits)."""
+    if split_cols:
+        return _run(lib().oracle_forward_f32_split, np.float32, A, b, graph_list, hyp, y0, U0, d0,
+                    variant, hyp_mode, tail=(int(split_cols),))
     return _run(lib().oracle_forward_f32, np.float32, A, b, graph_list, hyp, y0, U0, d0, variant,
                 hyp_mode)
 

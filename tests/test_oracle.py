@@ -369,3 +369,27 @@ def test_adjoint_sensitivity_fp32_vs_fp64_trajectory():
     Y32, _, _, G32, U32 = O.forward_f32_rec(A, b, graphs, hyp, y0, U0, d0)
     d32 = O.backward_np64(A, graphs, hyp, y0, d0, Y32, G32, U32, gY)
     assert np.abs(d32 - d64).max() <= 0.1 * np.abs(d64).max()
+
+
+def test_split_order_restatement():
+    """oracle_forward_f32_split (the column-split forward's GEMM1 order, dadmm_split.hip): one
+    slice covering every column is the unsplit chain exactly; 64-column slices give a different
+    fp32 evaluation of the same recurrence (not bit-equal at a 256-column shape), as close to the
+    fp64 restatement as the unsplit order is."""
+    P, m, n, B, K = 3, 16, 200, 4, 6
+    A, b, _ = O.make_problem(P, m, n, B, seed=5)
+    G = O.er_graph(P, 0.6, seed=2)
+    rng = np.random.default_rng(0)
+    y0, U0, d0 = (1e-2 * rng.standard_normal((3, B, P, n))).astype(np.float32)
+    hyp = O.hyp_table(0.3 * rng.standard_normal((K, P, 4)), [0.1, 0.99, 0.99, 0.99])
+    Y, U, _ = O.forward_f32(A, b, [G] * B, hyp, y0, U0, d0)
+    Y1, U1, _ = O.forward_f32(A, b, [G] * B, hyp, y0, U0, d0, split_cols=256)
+    assert np.array_equal(Y, Y1) and np.array_equal(U, U1)
+    Ys, _, _ = O.forward_f32(A, b, [G] * B, hyp, y0, U0, d0, split_cols=64)
+    assert not np.array_equal(Y, Ys)
+    Y64, _, _ = O.forward_f64(A, b, [G] * B, hyp, y0, U0, d0)
+    e_split = float(((Ys[-1] - Y64[-1]) ** 2).mean())
+    e_fused = float(((Y[-1] - Y64[-1]) ** 2).mean())
+    assert e_split <= 1e-8 and e_fused <= 1e-8, (e_split, e_fused)
+    with pytest.raises(RuntimeError):
+        O.forward_f32(A, b, [G] * B, hyp, y0, U0, d0, split_cols=40)   # not a multiple of 16
