@@ -80,17 +80,22 @@ __device__ __forceinline__ float mclamp(float x, float lo, float hi) {
 }
 __device__ __forceinline__ bool finitef(float x) { return __builtin_isfinite(x); }
 
-// Wait until the epoch words of every other slice of one (agent, m-block) reach `epoch`: lanes
-// 0..S-1 but `self` poll one word each (sc1 loads), lane S the launch-wide abort word. False when the launch is
-// aborted (by this wave's deadline or another's). Wave-uniform.
-template <int S>
-__device__ __forceinline__ bool wait_slices(const uint32_t* words, uint32_t epoch, uint32_t* abortw,
-                                            uint64_t spin_ticks, int lane, int self) {
+// Wait until the epoch words of every other slice of the wave's TH (agent, m-block) tiles reach
+// `epoch`: lane t * S + s polls word s of tile t (sc1 loads; tile t's S words at words[t]), lanes
+// of the wave's own slice skip, lane TH * S polls the launch-wide abort word. False when the
+// launch is aborted (by this wave's deadline or another's). Wave-uniform.
+template <int S, int TH>
+__device__ __forceinline__ bool wait_tiles(const uint32_t* const (&words)[TH > 0 ? TH : 1], uint32_t epoch,
+                                           uint32_t* abortw, uint64_t spin_ticks, int lane, int self) {
+    const uint32_t* mine = nullptr;
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+        if (lane >= t * S && lane < (t + 1) * S && lane - t * S != self) mine = words[t] + (lane - t * S);
     uint64_t t_end = 0;
     for (int spin = 0;; ++spin) {
         uint32_t v = epoch, ab = 0;
-        if (lane < S && lane != self) v = __hip_atomic_load((gu32*)(words + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else if (lane == S) ab = __hip_atomic_load((gu32*)abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (mine != nullptr) v = __hip_atomic_load((gu32*)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (lane == TH * S) ab = __hip_atomic_load((gu32*)abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (__ballot(v < epoch) == 0) return true;
         if (__ballot(ab != 0) != 0) return false;
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -243,8 +248,40 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
                 vclip = 100.0f;                                  // :224, :232
             }
 
-            // ---- dual update deferred from iteration k-1 (:95-99): delta_k = 2 L y_k for the
-            //      wave's 4 rows (all P agents of the row are in Ylds), U_k = clamp(U + delta eta) --
+            // ---- GEMM1 partials c_s = A_p[:, slice] y_p[slice] (+ -b in slice 0), published one
+            //      chain at a time: stored write-through (sc1); chain i-1's epoch word after chain
+            //      i's store (every VMEM op but that store has completed: vmcnt counts in order) --
+            f32x4 part[THA];
+#pragma unroll
+            for (int i = 0; i < TH; ++i) {
+                const int p = HALF + 2 * i;
+                f32x4 acc = bseed[i];
+#pragma unroll
+                for (int t = 0; t < NS / 16; ++t) {
+                    const f32x4 av = *(const f32x4*)(Alds + (p * M_PAD + 16 * mb + j) * AST + 16 * t + 4 * h);
+                    const f32x4 bv = *(const f32x4*)(Ylds + (p * BT + j) * YS + 16 * t + 4 * h);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc = mfma4(av[r], bv[r], acc);
+                }
+                part[i] = acc;
+                bstore4<16>(acc, rX, xtile_off(slot, p, slice));
+                if (i > 0) {
+                    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                    if (lane == 0)
+                        __hip_atomic_store((gu32*)(flag_at(HALF + 2 * (i - 1)) + slice), epoch,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (TH > 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0)
+                    __hip_atomic_store((gu32*)(flag_at(HALF + 2 * (TH - 1)) + slice), epoch,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+
+            // ---- dual update deferred from iteration k-1 (:95-99), under the exchange: delta_k =
+            //      2 L y_k for the wave's 4 rows (all P agents of a row are in Ylds), U_k = clamp(U
+            //      + delta eta); needed only by this iteration's primal updates -------------------
             if (k > 0) {
                 float yy[P][4], dd[P][4];
 #pragma unroll
@@ -266,47 +303,28 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
                 }
             }
 
-            // ---- GEMM1 partials c_s = A_p[:, slice] y_p[slice] (+ -b in slice 0), published
-            //      one chain at a time: the epoch word of chain i - 1 after chain i's store ------
-            f32x4 part[THA];
+            // ---- R_p = ((c_0 + c_1) + c_2) + ... for the wave's (agent, m-block) tiles -> Rlds:
+            //      one poll over all of them, then every remote partial load in flight at once
+            //      (a per-agent pipeline with LDS arrival counters under GEMM2 measured slower:
+            //      206 vs 198 us per forward at configs[1]) ----------------------
+            {
+                const uint32_t* words[THA];
 #pragma unroll
-            for (int i = 0; i < TH; ++i) {
-                const int p = HALF + 2 * i;
-                f32x4 acc = bseed[i];
-#pragma unroll
-                for (int t = 0; t < NS / 16; ++t) {
-                    const f32x4 av = *(const f32x4*)(Alds + (p * M_PAD + 16 * mb + j) * AST + 16 * t + 4 * h);
-                    const f32x4 bv = *(const f32x4*)(Ylds + (p * BT + j) * YS + 16 * t + 4 * h);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc = mfma4(av[r], bv[r], acc);
-                }
-                part[i] = acc;
-                bstore4<16>(acc, rX, xtile_off(slot, p, slice));
-                if (i > 0) {
-                    // every VMEM op but this store has completed (in order): chain i-1's tile
-                    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-                    if (lane == 0)
-                        __hip_atomic_store((gu32*)(flag_at(HALF + 2 * (i - 1)) + slice), epoch,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
+                for (int i = 0; i < TH; ++i) words[i] = flag_at(HALF + 2 * i);
+                if (!aborted) aborted = !wait_tiles<S, TH>(words, epoch, abortw, sa.spin_ticks, lane, slice);
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0 && TH > 0)
-                __hip_atomic_store((gu32*)(flag_at(HALF + 2 * (TH - 1)) + slice), epoch,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-
-            // ---- R_p = ((c_0 + c_1) + c_2) + ... for the wave's (agent, m-block) tiles -> Rlds --
+            f32x4 c[THA][S];
 #pragma unroll
-            for (int i = 0; i < TH; ++i) {
-                const int p = HALF + 2 * i;
-                if (!aborted) aborted = !wait_slices<S>(flag_at(p), epoch, abortw, sa.spin_ticks, lane, slice);
-                f32x4 c[S];
+            for (int i = 0; i < TH; ++i)
 #pragma unroll
                 for (int s2 = 0; s2 < S; ++s2)
-                    c[s2] = s2 == slice ? part[i] : bload4<16>(rX, xtile_off(slot, p, s2));
-                f32x4 rsum = c[0];
+                    c[i][s2] = s2 == slice ? part[i] : bload4<16>(rX, xtile_off(slot, HALF + 2 * i, s2));
 #pragma unroll
-                for (int s2 = 1; s2 < S; ++s2) rsum = rsum + c[s2];
+            for (int i = 0; i < TH; ++i) {
+                const int p = HALF + 2 * i;
+                f32x4 rsum = c[i][0];
+#pragma unroll
+                for (int s2 = 1; s2 < S; ++s2) rsum = rsum + c[i][s2];
                 *(f32x4*)(Rlds + (p * BT + j) * RS + 16 * mb + 4 * h) = rsum;
             }
             __syncthreads();
@@ -323,10 +341,8 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
                 for (int t = 0; t < M_PAD / 16; ++t) {
                     const f32x4 rv = *(const f32x4*)(Rlds + (p * BT + j) * RS + 16 * t + 4 * h);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float av = Alds[(p * M_PAD + 16 * t + 4 * h + r) * AST + 16 * nt + j];
-                        gp = mfma4(av, rv[r], gp);
-                    }
+                    for (int r = 0; r < 4; ++r)
+                        gp = mfma4(Alds[(p * M_PAD + 16 * t + 4 * h + r) * AST + 16 * nt + j], rv[r], gp);
                 }
                 float* yrow = Ylds + (p * BT + j) * YS + 16 * nt + 4 * h;
                 const f32x4 yk = *(const f32x4*)yrow;
