@@ -35,15 +35,37 @@ def _t(x, dev):
     return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
 
 
+# GEMM1 order of the last _run_hip: the column-split forward (small batches at n_pad 128 / 256,
+# dadmm_split.hip) sums 64-column partial chains; a guard that fired sends the batch through the
+# stepwise recomputation (the fused order)
+_LAST = {"split": 0}
+
+
 def _run_hip(dev, A, b, graphs_list, hyp, y0, U0, d0, variant=0, path="auto"):
     from dadmm_hip import PreparedOperator, forward_raw, ingest
+    from dadmm_hip.ops import split_cols
     B = y0.shape[0]
     op = PreparedOperator(_t(A, dev))
     g = ingest(graphs_list, A.shape[0], B, dev)
     Y, U, st = forward_raw(op, _t(b, dev), g, _t(hyp, dev), _t(y0, dev), _t(U0, dev),
                            _t(d0, dev), variant=variant, want_U=True, path=path)
     torch.cuda.synchronize()
-    return Y.cpu().numpy(), U.cpu().numpy(), int(st.item()), g.shared
+    st = int(st.item())
+    sc = split_cols(op, B, hyp.shape[0], g, hyp_rows=hyp.shape[1]) if path == "auto" else 0
+    if sc:
+        # the split launch alone (ungated): any bit it raises sends the auto path's batch
+        # through the stepwise recomputation, whose order is the fused one
+        _, _, st_split = forward_raw(op, _t(b, dev), g, _t(hyp, dev), _t(y0, dev), _t(U0, dev),
+                                     _t(d0, dev), variant=variant, path="split")
+        if int(st_split.item()) != 0:
+            sc = 0
+    _LAST["split"] = sc
+    return Y.cpu().numpy(), U.cpu().numpy(), st, g.shared
+
+
+def _expected(*args, **kw):
+    """oracle.forward_f32 in the order the last _run_hip evaluated (split or fused)."""
+    return O.forward_f32(*args, split_cols=_LAST["split"], **kw)
 
 
 def test_mfma_f32_is_a_k_ordered_fma_chain(cuda):
@@ -88,7 +110,7 @@ def test_headline_shape_bit_exact(cuda, hyp_kind):
     hyp = O.hyp_table(param, MAXP)
     Y, U, st, shared = _run_hip(cuda, A, b, [G] * B, hyp, y0, U0, d0)
     assert shared and st == 0
-    Yo, Uo, sto = O.forward_f32(A, b, [G] * B, hyp, y0, U0, d0)
+    Yo, Uo, sto = _expected(A, b, [G] * B, hyp, y0, U0, d0)
     assert sto == 0
     assert np.array_equal(Y, Yo), f"max |diff| {np.abs(Y - Yo).max()} at {np.argwhere(Y != Yo)[:3]}"
     assert np.array_equal(U, Uo)
@@ -113,7 +135,7 @@ def test_headline_shape_vs_fp64(cuda):
         y0, U0, d0 = (1e-2 * rng.standard_normal((3, B, P, n))).astype(np.float32)
         Y, _, st, _ = _run_hip(cuda, A, b, [G] * B, hyp, y0, U0, d0)
         Y64, _, _ = O.forward_f64(A, b, [G] * B, hyp, y0, U0, d0)
-        Y32, _, _ = O.forward_f32(A, b, [G] * B, hyp, y0, U0, d0)
+        Y32, _, _ = _expected(A, b, [G] * B, hyp, y0, U0, d0)
         mse = float(((Y[-1] - Y64[-1]) ** 2).mean())
         assert mse == float(((Y32[-1] - Y64[-1]) ** 2).mean())
         mses.append(mse)
@@ -171,7 +193,7 @@ def test_shapes_bit_exact(cuda, P, m, n, B, K, prob, per_sample, path, request):
     rng = np.random.default_rng(K)
     hyp = O.hyp_table((0.5 * rng.standard_normal((K, P, 4))).astype(np.float32), MAXP)
     Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0, path=path)
-    Yo, Uo, _ = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
+    Yo, Uo, _ = _expected(A, b, graphs, hyp, y0, U0, d0)
     assert st == 0
     assert np.array_equal(Y, Yo), f"max |diff| {np.abs(Y - Yo).max()}"
     assert np.array_equal(U, Uo)
@@ -230,7 +252,7 @@ def test_same_mode_and_gnn_variant(cuda, path):
     hyp = O.hyp_table((rng.standard_normal((K, 1, 4))).astype(np.float32), [0.3, 0.99, 0.99, 0.99])
     for variant in (0, 1):
         Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0, variant=variant, path=path)
-        Yo, Uo, _ = O.forward_f32(A, b, graphs, hyp, y0, U0, d0, variant=variant)
+        Yo, Uo, _ = _expected(A, b, graphs, hyp, y0, U0, d0, variant=variant)
         assert np.array_equal(Y, Yo), (variant, np.abs(Y - Yo).max())
         assert np.array_equal(U, Uo)
 
@@ -290,7 +312,7 @@ def test_guards_bit_exact(cuda, path):
     G = O.er_graph(P, 0.6, seed=2)
     for name, A, b, hyp, y0, U0, d0 in _guard_cases(P, m, n, B, K, seed=11):
         Y, U, st, _ = _run_hip(cuda, A, b, [G] * B, hyp, y0, U0, d0, path=path)
-        Yo, Uo, sto = O.forward_f32(A, b, [G] * B, hyp, y0, U0, d0)
+        Yo, Uo, sto = _expected(A, b, [G] * B, hyp, y0, U0, d0)
         assert st == sto, (name, st, sto)
         np.testing.assert_array_equal(Y, Yo, err_msg=name)
         np.testing.assert_array_equal(U, Uo, err_msg=name)
@@ -317,7 +339,7 @@ def test_guards_bit_exact_per_sample_graphs_large_batch(cuda):
     graphs = [O.connected_er_graph(P, 0.5, seed=300 + s) for s in range(B)]
     for name, A, b, hyp, y0, U0, d0 in _guard_cases(P, m, n, B, K, seed=5)[:3]:
         Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0)
-        Yo, Uo, sto = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
+        Yo, Uo, sto = _expected(A, b, graphs, hyp, y0, U0, d0)
         assert st == sto, (name, st, sto)
         np.testing.assert_array_equal(Y, Yo, err_msg=name)
         np.testing.assert_array_equal(U, Uo, err_msg=name)
@@ -345,7 +367,9 @@ def test_module_forward_matches_oracle(cuda):
         Y, hyp = model(bt, [G] * B, inits=tuple(_t(v, cuda) for v in (y0, U0, d0)))
         table = model.hyp_table(K).cpu().numpy()
     assert Y.shape == (K, B, P, n, 1) and hyp.shape == (P, 4, 1)
-    Yo, _, _ = O.forward_f32(A, b, [G] * B, table, y0, U0, d0)
+    from dadmm_hip.ops import split_cols
+    Yo, _, _ = O.forward_f32(A, b, [G] * B, table, y0, U0, d0,
+                             split_cols=split_cols(model.operator(), B, K))
     assert np.array_equal(Y[..., 0].cpu().numpy(), Yo)
     # K override: min(K, self.K) layers, equal to the prefix of the full run
     with torch.no_grad():
@@ -370,7 +394,9 @@ def test_module_odd_n_is_zero_padded(cuda):
         Y, _ = model(torch.from_numpy(b).to(cuda)[..., None], [G] * B,
                      inits=tuple(_t(v, cuda) for v in (y0, U0, d0)))
         table = model.hyp_table(K).cpu().numpy()
-    Yo, _, _ = O.forward_f32(A, b, [G] * B, table, y0, U0, d0)
+    from dadmm_hip.ops import split_cols
+    Yo, _, _ = O.forward_f32(A, b, [G] * B, table, y0, U0, d0,
+                             split_cols=split_cols(model.operator(), B, K))
     assert np.array_equal(Y[..., 0].cpu().numpy(), Yo)
 
 
@@ -388,8 +414,10 @@ def test_repeat_runs_identical(cuda):
 @pytest.mark.parametrize("path", sorted(__import__("glob").glob(os.path.join(GOLD, "golden_*.npz"))),
                          ids=lambda p: os.path.basename(p))
 def test_goldens_bit_exact(cuda, path):
-    """The kernel against the committed golden vectors (graphs given as CSR in adjacency
-    order, so non-ascending adjacency lists take the ordered-consensus kernel)."""
+    """The fused kernel against the committed golden vectors (graphs given as CSR in adjacency
+    order, so non-ascending adjacency lists take the ordered-consensus kernel). The goldens hold
+    the fused order: path "fused" (the auto path takes the column-split forward at these batch
+    sizes, tests/test_gpu_split.py)."""
     from dadmm_hip import PreparedOperator, forward_raw, from_csr
     g = np.load(path)
     P = g["A"].shape[0]
@@ -397,7 +425,7 @@ def test_goldens_bit_exact(cuda, path):
     gb = from_csr(g["nbr_ptr"], g["nbr_idx"], g["deg"], P, cuda)
     Y, U, st = forward_raw(op, _t(g["b"], cuda), gb, _t(g["hyp"], cuda), _t(g["y0"], cuda),
                            _t(g["U0"], cuda), _t(g["d0"], cuda), variant=int(g["variant"]),
-                           want_U=True)
+                           want_U=True, path="fused")
     assert int(st.item()) == 0
     np.testing.assert_array_equal(Y.cpu().numpy(), g["Y32"])
     np.testing.assert_array_equal(U.cpu().numpy(), g["U32"])
@@ -422,7 +450,7 @@ def test_non_ascending_adjacency_bit_exact(cuda):
     y0, U0, d0 = _inits(B, P, n, seed=5)
     hyp = O.hyp_table((rng.standard_normal((K, P, 4))).astype(np.float32), MAXP)
     Y, U, st, _ = _run_hip(cuda, A, b, graphs, hyp, y0, U0, d0)
-    Yo, Uo, _ = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
+    Yo, Uo, _ = _expected(A, b, graphs, hyp, y0, U0, d0)
     assert np.array_equal(Y, Yo) and np.array_equal(U, Uo)
 
 

@@ -74,7 +74,9 @@ def test_forward_on_device_graphs_bit_exact(cuda, P, n, m, B, K, path):
     t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(cuda)   # noqa: E731
     op = PreparedOperator(t(A))
     Y, U, st = forward_raw(op, t(b), gb, t(hyp), t(y0), t(U0), t(d0), want_U=True, path=path)
-    Yo, Uo, sto = O.forward_f32(A, b, graphs, hyp, y0, U0, d0)
+    from dadmm_hip.ops import split_cols
+    sc = split_cols(op, B, K, gb, hyp_rows=P) if path == "auto" else 0   # dadmm_split.hip order
+    Yo, Uo, sto = O.forward_f32(A, b, graphs, hyp, y0, U0, d0, split_cols=sc)
     assert int(st.item()) == sto == 0
     assert np.array_equal(Y.cpu().numpy(), Yo)
     assert np.array_equal(U.cpu().numpy(), Uo)
