@@ -113,14 +113,6 @@ int check_fused_shape(const dadmm_dims* d, const uint32_t* nbr_order, int* graph
     return DADMM_OK;
 }
 
-// The row-divided fused kernel (dadmm_fused.hip) is the default: at the headline shape the
-// agent-resident one (dadmm_resident.hip) measured 0.60-0.67 vs 0.53-0.61 ms per launch on the
-// same boxes (profiles/r05/resident_ablations_r05.txt). DADMM_FUSED_DIVISION=agents selects it.
-bool agent_division() {
-    const char* e = getenv("DADMM_FUSED_DIVISION");
-    return e != nullptr && strcmp(e, "agents") == 0;
-}
-
 int forward_impl(const dadmm_dims* d, const void* op, const float* b, const uint64_t* nbr,
                  const uint32_t* nbr_order, const float* deg, const float* hyp, const float* y0,
                  const float* U0, const float* d0, float* Y, float* Grec, float* Urec,
@@ -138,12 +130,7 @@ int forward_impl(const dadmm_dims* d, const void* op, const float* b, const uint
         return fail(DADMM_EINVAL, "Y, y0, U0, d0 and U_out must be 16-byte aligned");
     int graph = 0, nt = 0;
     if ((rc = check_fused_shape(d, nbr_order, &graph, &nt)) != DADMM_OK) return rc;
-    // inference: DADMM_FUSED_DIVISION=agents selects the agent-resident kernel where it holds the
-    // shape (A/B timing; both kernels are bit-identical)
-    dadmm::fused_fn_ptr fn = nullptr;
-    if (!rec && agent_division()) fn = dadmm::find_resident(d->P, nt, graph);
-    if (fn == nullptr)
-        fn = rec ? dadmm::find_fused_rec(d->P, nt, graph) : dadmm::find_fused(d->P, nt, graph);
+    dadmm::fused_fn_ptr fn = rec ? dadmm::find_fused_rec(d->P, nt, graph) : dadmm::find_fused(d->P, nt, graph);
     if (fn == nullptr)
         return fail(DADMM_EUNSUPPORTED, "no fused kernel for P=%d n=%d (n_pad=%d)", d->P, d->n,
                     64 * nt);

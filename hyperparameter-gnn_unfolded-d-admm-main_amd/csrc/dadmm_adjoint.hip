@@ -29,13 +29,7 @@ namespace adj {
 constexpr int THREADS = 256;   // 4 waves, one (sample, 64-column) item each
 constexpr int WAVES = 4;
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-// DADMM_ADJ_V4=1: the 16-byte-lane form of the register-resident update (adj_update_v4)
-#ifndef DADMM_ADJ_V4
-#define DADMM_ADJ_V4 1
-#endif
-#ifndef DADMM_ADJ_PF
-#define DADMM_ADJ_PF 1
-#endif
+// the register-resident update runs in the 16-byte-lane form (adj_update_v4)
 
 __device__ __forceinline__ float tclamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 __device__ __forceinline__ bool inside(float x, float lo, float hi) { return x >= lo && x <= hi; }
@@ -62,18 +56,10 @@ __device__ __forceinline__ float visit_sum(const float* __restrict__ x, const in
     return acc;
 }
 
-// wave-sum of v into red[p][c] (lane 0 accumulates; one wave owns its red slice); on DPP moves
-// (wave_sum_dpp) unless built with -DDADMM_ADJ_DPP=0
-#ifndef DADMM_ADJ_DPP
-#define DADMM_ADJ_DPP 1
-#endif
+// wave-sum of v into red[p][c] (lane 0 accumulates; one wave owns its red slice) on DPP moves
+// (wave_sum_dpp)
 __device__ __forceinline__ void wave_accum(float* red, int p, int c, float v, int lane) {
-#if DADMM_ADJ_DPP
     v = wave_sum_dpp(v);
-#else
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-#endif
     if (lane == 0) red[p * 4 + c] += v;
 }
 
@@ -236,163 +222,12 @@ __global__ __launch_bounds__(64 * W) void adj_update_kernel(AdjArgs a, int k, in
     }
 }
 
-// The same iteration with y_bar and U_bar held in registers between the two phases (P <= PM):
-// the first phase's y_bar + gY[k] and U_bar' never go to HBM, so each element of y_bar / U_bar is
-// read once and written once per iteration (1.47 instead of 2.0 GB per iteration at configs[2]).
-// Every value and operation order is the generic kernel's.
-template <int PM>
-__global__ __launch_bounds__(THREADS) void adj_update_reg(AdjArgs a, int k, int items) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int P = a.P, n = a.n, K = a.K, H = a.hyp_rows;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float* xs = lds + w * (2 * P * 64);
-    float* ds = xs + P * 64;
-    float* red = lds + WAVES * 2 * P * 64;
-    float* rw = red + w * P * 4;
-    int32_t* vpl = (int32_t*)(red + WAVES * P * 4) + w * (P + 1 + (2 * P * P + 3) / 4);
-    uint8_t* vql = (uint8_t*)(vpl + P + 1);
-    for (int i = lane; i < P * 4; i += 64) rw[i] = 0.0f;
-    const int item = blockIdx.x * WAVES + w;
-    const size_t S = (size_t)a.B * P * n;
-    if (item < items) {
-        const int nch = (n + 63) / 64;
-        const int s = item / nch, c = (item % nch) * 64 + lane;
-        const bool cv = c < n;
-        const size_t base = (size_t)s * P * n + (cv ? c : 0);
-        const int g0 = a.graph_shared ? 0 : s * P;
-        {
-            const int v0 = a.vptr[g0], ve = a.vptr[g0 + P];
-            for (int i = lane; i <= P; i += 64) vpl[i] = a.vptr[g0 + i] - v0;
-            for (int i = lane; i < ve - v0; i += 64) vql[i] = a.vq[v0 + i];
-        }
-        float gclip, vclip;
-        clips(a.variant, k, gclip, vclip);
-        auto hyp = [&](int kk, int p, int comp) {
-            return a.hyp[((size_t)kk * H + (H == 1 ? 0 : p)) * 4 + comp];
-        };
-        const float* __restrict__ y1 = a.Y + (size_t)k * S;
-        const float* __restrict__ yk = k > 0 ? a.Y + (size_t)(k - 1) * S : a.y0;
-        const float* __restrict__ gYk = a.gY + (size_t)k * S;
-        const float* __restrict__ Urk = a.Urec + (size_t)k * S;
-        const float* __restrict__ Grk = a.Grec + (size_t)k * S;
-        float* __restrict__ ybs = a.yb;
-        float* __restrict__ Ubs = a.Ub;
-        float* __restrict__ Gbs = a.Gb;
-        for (int p = 0; p < P; ++p) xs[p * 64 + lane] = cv ? y1[base + (size_t)p * n] : 0.0f;
-        __builtin_amdgcn_wave_barrier();
-        float ybr[PM], ubr[PM];
-        constexpr int GP = 4;
-#pragma unroll
-        for (int p0 = 0; p0 < PM; p0 += GP) {
-            if (p0 >= P) break;
-            float d1[GP], gy[GP], ur[GP], gb[GP];
-#pragma unroll
-            for (int i = 0; i < GP; ++i) d1[i] = p0 + i < P ? visit_sum(xs, vpl, vql, p0 + i, lane) : 0.0f;
-#pragma unroll
-            for (int i = 0; i < GP; ++i) {
-                const int p = p0 + i;
-                gy[i] = ur[i] = gb[i] = ybr[p] = ubr[p] = 0.0f;
-                if (cv && p < P) {
-                    const size_t off = base + (size_t)p * n;
-                    gy[i] = gYk[off];
-                    ur[i] = Urk[off];
-                    ubr[p] = Ubs[off];
-                    gb[i] = Gbs[off];
-                    ybr[p] = ybs[off];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < GP; ++i) {
-                const int p = p0 + i;
-                if (p >= P) break;
-                const bool md = a.variant == 0 || inside(d1[i], -20.0f, 20.0f);   // GNN clamp :229
-                const float dcl = a.variant == 0 ? d1[i] : tclamp(d1[i], -20.0f, 20.0f);
-                float pe = 0.0f, db = 0.0f;
-                if (cv) {
-                    const float et = hyp(k, p, 3);
-                    const float rh1 = k + 1 < K ? hyp(k + 1, p, 2) : 0.0f;
-                    ybr[p] = ybr[p] + gy[i];                                      // + gY[k]
-                    const float wv = ur[i] + dcl * et;
-                    const float wb = inside(wv, -vclip, vclip) ? ubr[p] : 0.0f;
-                    pe = wb * dcl;
-                    db = md ? gb[i] * rh1 + wb * et : 0.0f;
-                    ubr[p] = wb;
-                }
-                ds[p * 64 + lane] = db;
-                wave_accum(rw, p, 3, pe, lane);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        for (int p = 0; p < P; ++p) xs[p * 64 + lane] = cv ? yk[base + (size_t)p * n] : 0.0f;
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int p0 = 0; p0 < PM; p0 += GP) {
-            if (p0 >= P) break;
-            float tv[GP], dk[GP], gr[GP];
-#pragma unroll
-            for (int i = 0; i < GP; ++i) {
-                const int p = p0 + i;
-                tv[i] = dk[i] = 0.0f;
-                if (p < P) {
-                    tv[i] = visit_sum(ds, vpl, vql, p, lane);
-                    if (k > 0) {
-                        dk[i] = visit_sum(xs, vpl, vql, p, lane);
-                        if (a.variant != 0) dk[i] = tclamp(dk[i], -20.0f, 20.0f);
-                    }
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < GP; ++i) {
-                const int p = p0 + i;
-                gr[i] = 0.0f;
-                if (cv && p < P) {
-                    const size_t off = base + (size_t)p * n;
-                    if (k == 0) dk[i] = a.d0[off];
-                    gr[i] = Grk[off];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < GP; ++i) {
-                const int p = p0 + i;
-                if (p >= P) break;
-                float pa = 0.0f, pt = 0.0f, pr = 0.0f;
-                if (cv) {
-                    const size_t off = base + (size_t)p * n;
-                    const float al = hyp(k, p, 0);
-                    const float y = xs[p * 64 + lane];
-                    const float g = tclamp(gr[i], -gclip, gclip);
-                    const float z = y - al * g;
-                    const float ybv = ybr[p] + tv[i];
-                    const float zb = inside(z, -vclip, vclip) ? ybv : 0.0f;
-                    pa = -zb * g;
-                    const float grb = inside(gr[i], -gclip, gclip) ? -al * zb : 0.0f;
-                    pt = grb * sign_times(y, 1.0f);
-                    pr = grb * dk[i];
-                    const float dg = a.deg[g0 + p];
-                    Ubs[off] = ubr[p] + grb * dg;
-                    ybs[off] = zb;
-                    Gbs[off] = grb;
-                }
-                wave_accum(rw, p, 0, pa, lane);
-                wave_accum(rw, p, 1, pt, lane);
-                wave_accum(rw, p, 2, pr, lane);
-            }
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < P * 4; i += THREADS) {
-        float v = 0.0f;
-#pragma unroll
-        for (int ww = 0; ww < WAVES; ++ww) v += red[ww * P * 4 + i];
-        a.partial[((size_t)blockIdx.x * K + k) * P * 4 + i] = v;
-    }
-}
-
-// The register-resident iteration with 16-byte lanes (P <= PM, DADMM_ADJ_V4): lane l owns agent
+// The register-resident iteration with 16-byte lanes (P <= PM): y_bar and U_bar stay in
+// registers between the two phases (each element read and written once per iteration); lane l owns agent
 // p0 + l / 16 of the current group of four and columns 4 (l % 16) .. + 3 of the item's 64, so one
 // wave instruction moves four agents' 256-byte rows (1 KB) instead of one agent's 256 bytes, and
 // the LDS rows are read as b128 (a 16-lane group spans 16 distinct 16-byte bank slots). Every
-// element's value and operation order is adj_update_reg's; only the dhyp partial sums are
+// element's value and operation order is the generic kernel's; only the dhyp partial sums are
 // associated differently (each lane's 4 columns, then a 16-lane shuffle tree per agent).
 __device__ __forceinline__ f32x4v visit_sum4(const float* __restrict__ x, const int32_t* __restrict__ vp,
                                              const uint8_t* __restrict__ vq, int p, int cq) {
@@ -410,12 +245,7 @@ __device__ __forceinline__ f32x4v visit_sum4(const float* __restrict__ x, const 
 // sum of v over this lane's 4 columns and its 16-lane group -> red[p][c] (lane 16 a adds)
 __device__ __forceinline__ void group_accum(float* red, int p, int c, f32x4v v, bool live, int lane) {
     float s = (v[0] + v[1]) + (v[2] + v[3]);
-#if DADMM_ADJ_DPP
     s = row16_sum_dpp(s);
-#else
-#pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-#endif
     if ((lane & 15) == 0 && live) red[p * 4 + c] += s;
 }
 
@@ -471,16 +301,15 @@ __global__ __launch_bounds__(THREADS) void adj_update_v4(AdjArgs a, int k, int i
             const int p = 4 * g + ag;
             if (4 * g < P && p < P) *(f32x4v*)(xs + p * 64 + 4 * cq) = ld(y1, p);
         }
-        // DADMM_ADJ_PF: the second phase's operands (y_k rows, Grec[k]) issued now, so that phase
+        // the second phase's operands (y_k rows, Grec[k]) issued now, so that phase
         // does not start with another HBM round trip
         f32x4v ykr[NG], grr[NG];
-        if (DADMM_ADJ_PF) {
 #pragma unroll
-            for (int g = 0; g < NG; ++g) {
-                ykr[g] = ld(yk, 4 * g + ag);
-                grr[g] = ld(Grk, 4 * g + ag);
-            }
+        for (int g = 0; g < NG; ++g) {
+            ykr[g] = ld(yk, 4 * g + ag);
+            grr[g] = ld(Grk, 4 * g + ag);
         }
+    
         __builtin_amdgcn_wave_barrier();
         f32x4v ybr[NG], ubr[NG];
         // dual-update adjoint of iteration k (:95-99): the group's loads in flight together, then
@@ -517,7 +346,7 @@ __global__ __launch_bounds__(THREADS) void adj_update_v4(AdjArgs a, int k, int i
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
             const int p = 4 * g + ag;
-            if (4 * g < P && p < P) *(f32x4v*)(xs + p * 64 + 4 * cq) = DADMM_ADJ_PF ? ykr[g] : ld(yk, p);
+            if (4 * g < P && p < P) *(f32x4v*)(xs + p * 64 + 4 * cq) = ykr[g];
         }
         __builtin_amdgcn_wave_barrier();
         // y_bar += 2 L d_bar; primal-update and gradient-clamp adjoint (:73-93)
@@ -527,7 +356,7 @@ __global__ __launch_bounds__(THREADS) void adj_update_v4(AdjArgs a, int k, int i
             const int p = 4 * g + ag;
             const bool pv = p < P;
             const int pc = pv ? p : 0;
-            const f32x4v gr = DADMM_ADJ_PF ? grr[g] : ld(Grk, p);
+            const f32x4v gr = grr[g];
             f32x4v dk = k == 0 ? ld(a.d0, p) : z4;
             const f32x4v tv = pv ? visit_sum4(ds, vpl, vql, p, cq) : z4;
             if (k > 0 && pv) {
@@ -603,8 +432,8 @@ hipError_t launch_adjoint(const AdjArgs& a, float* dhyp, hipStream_t st) {
     if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
     // y_bar / U_bar register-resident between the phases for P <= 16, the generic kernel above
     const int W = adjoint_waves(a.P);
-    auto kern = a.P <= 8 ? (DADMM_ADJ_V4 ? adj::adj_update_v4<8> : adj::adj_update_reg<8>)
-              : a.P <= 16 ? (DADMM_ADJ_V4 ? adj::adj_update_v4<16> : adj::adj_update_reg<16>)
+    auto kern = a.P <= 8 ? adj::adj_update_v4<8>
+              : a.P <= 16 ? adj::adj_update_v4<16>
               : W == 4 ? adj::adj_update_kernel<4> : W == 2 ? adj::adj_update_kernel<2> : adj::adj_update_kernel<1>;
     if (lds > 64 * 1024 &&
         (e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) !=

@@ -60,56 +60,23 @@ __device__ __forceinline__ uint32_t fresh_s(uint32_t x) {
     return x;
 }
 
-// Waves per workgroup: 8 (two per SIMD, 256 registers each) or 4 (one per SIMD, 512 registers:
-// twice the rows per wave, room to keep more of the five trajectory streams in flight). 4 with
-// the pipelined prefetch (PF 2) is the default: 1.22 vs 1.27-1.28 ms at H (profiles/r05/adjoint_variants_r05j.txt)
-#ifndef DADMM_BWD_WAVES
-#define DADMM_BWD_WAVES 4
-#endif
-constexpr int WAVES = DADMM_BWD_WAVES;
-static_assert(WAVES == 8 || WAVES == 4, "adjoint workgroup: 4 or 8 waves");
-// GEMM2's A^T operand through a per-wave LDS ring filled by LDS-DMA, as in the forward
-// (dadmm_fused.hip): BWD_QD quarter-chains of 1 KB per wave, BWD_QD - 1 in flight. The 4-wave form
-// reads it straight from L2 instead (its loads sit in the 512-register budget): 1.19-1.21 vs
-// 1.22-1.23 ms at H (profiles/r05/adjoint_variants_r05p.txt)
-#ifndef DADMM_BWD_AT_DMA
-#define DADMM_BWD_AT_DMA (DADMM_BWD_WAVES == 4 ? 0 : 1)
-#endif
-constexpr int BWD_QD = 5;
-// DADMM_BWD_ROT=1: the elementwise phase walks the wave's T2 row tiles in a runtime loop and
-// rotates the carried state (y_bar, U_bar) so that the current tile's rows are always columns
-// 0..3 of the register arrays (static indices), and the shared graph's consensus is the forward's
-// branch-free consensus_fma (0/1 edge multipliers in SGPRs: exactly the forward's delta, so the
-// re-evaluated masks are the forward's). The unrolled tile loop let the compiler interleave the
-// two tiles' temporaries: 256 VGPRs + 231 spilled at H; this form: 13 spilled.
-#ifndef DADMM_BWD_ROT
-#define DADMM_BWD_ROT 1
-#endif
-// DADMM_BWD_PF=1 (4-wave form): all five streams of a tile (Y[k], Urec, gY, Y[k-1] or d0,
-// Grec) are loaded at the top of the tile, one memory round trip instead of four dependent ones.
-// DADMM_BWD_PF=2: software-pipelined — the streams of the NEXT tile (after a wave's last tile:
-// the first tile of iteration k - 1) are issued at the top of the current one, so the last
-// tile's prefetch lands under the GEMM phases
-#ifndef DADMM_BWD_PF
-#define DADMM_BWD_PF (DADMM_BWD_WAVES == 4 ? 2 : 0)
-#endif
-// DADMM_BWD_PK=1: the shared graph's consensus on row pairs with packed f32 instructions
-// (consensus_fma2: the same values, half the VALU issue)
-#ifndef DADMM_BWD_PK
-#define DADMM_BWD_PK 1
-#endif
-// DADMM_BWD_DPP=1: the per-iteration dhyp wave sums on DPP moves (quad perms, half-row and row
-// mirrors: each lane ends with its 16-lane row's sum) and four readlanes, instead of six
-// ds_bpermute round trips per value (a fixed order either way: deterministic; the association
-// differs from the butterfly's, within f32 rounding)
-#ifndef DADMM_BWD_DPP
-#define DADMM_BWD_DPP 1
-#endif
-#if DADMM_BWD_ROT
+// Decisions measured at H (round 6 removed the A/B switches):
+//   * 4 waves per workgroup (one per SIMD, 512 registers: twice the rows per wave, room for more of
+//     the five trajectory streams in flight): 1.22 vs 1.27-1.28 ms with 8 (adjoint_variants_r05j);
+//   * GEMM2's A^T straight from L2 (the loads sit in the 512-register budget) instead of the
+//     forward's LDS-DMA ring: 1.19-1.21 vs 1.22-1.23 ms (adjoint_variants_r05p);
+//   * the elementwise phase walks the wave's T2 row tiles in a runtime loop and rotates the carried
+//     state (y_bar, U_bar) so that the current tile's rows are always columns 0..3 of the register
+//     arrays (static indices); the unrolled tile loop interleaved the two tiles' temporaries
+//     (256 VGPRs + 231 spilled at H, this form 13);
+//   * all five streams of a tile (Y[k], Urec, gY, Y[k-1] or d0, Grec) software-pipelined: the NEXT
+//     tile's streams (after a wave's last tile: the first tile of iteration k - 1) issued at the
+//     top of the current one, so the last tile's prefetch lands under the GEMM phases;
+//   * the shared graph's consensus on row pairs with packed f32 instructions (consensus_fma2: the
+//     same values as the forward's consensus_fma, so the re-evaluated masks are the forward's);
+//   * the per-iteration dhyp wave sums on DPP moves (wave_sum_dpp): a fixed order, deterministic.
+constexpr int WAVES = 4;
 #define BWD_ROW(e, r) (r)
-#else
-#define BWD_ROW(e, r) (e)
-#endif
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n folded at compile time
     switch (n) {
@@ -153,7 +120,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
     float* __restrict__ Glds = lds;                 // [P][BT][YS]  gr_bar (GEMM B operand)
     float* __restrict__ Rlds = lds + P * BT * YS;   // [P][BT][RS]  A gr_bar
     float* __restrict__ red = Rlds + P * BT * RS;   // [WAVES][P][4] partial sums
-    float* __restrict__ Qlds = red + WAVES * P * 4;  // [WAVES][BWD_QD][256] A^T ring (DMA)
 
     const int lane = threadIdx.x & 63;
     const int j = lane & 15;
@@ -213,7 +179,7 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 #pragma unroll
         for (int p = 0; p < P; ++p) mf2[q][p] = (f32x2_c){mf[q][p], mf[q][p]};
     auto cons = [&](const float (&x)[P][4], float (&o)[P][4], const uint32_t (&mk_)[P]) {
-        if constexpr (GRAPH == GRAPH_SHARED && DADMM_BWD_ROT && DADMM_BWD_PK) {
+        if constexpr (GRAPH == GRAPH_SHARED) {
 #pragma unroll
             for (int rp = 0; rp < 2; ++rp) {   // rows (2 rp, 2 rp + 1) packed
                 f32x2_c yy[P], dd[P];
@@ -226,7 +192,7 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                     o[p][2 * rp + 1] = dd[p][1];
                 }
             }
-        } else if constexpr (GRAPH == GRAPH_SHARED && DADMM_BWD_ROT) {
+        } else if constexpr (GRAPH == GRAPH_SHARED) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float yy[P][1], dd[P][1];
@@ -247,15 +213,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
     const uint32_t voffA = (uint32_t)(((16 * mb + j) * NP + 4 * h) * 4);
     const uint32_t voffAt = (uint32_t)((j * MP + 4 * h) * 4);
     const float* brow = Glds + j * YS + 4 * h;
-    // quarter q = 4 (p T2 + tt) + t: A^T_p rows of n-tile w T2 + tt, m-block t -> slot q % BWD_QD
-    auto dma_quarter = [&](int q) {
-        const int c = q >> 2, t = q & 3;
-        const int p = c / T2, tt = c % T2;
-        const uint32_t vAt = voffAt + (uint32_t)(16 * (w * T2 + tt) * MP * 4);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rAt, (lds_void*)(Qlds + (w * BWD_QD + q % BWD_QD) * 256), 16,
-                                                 vAt + 64 * t, (uint32_t)(p * NP * MP * 4), 0, 0);
-    };
-#if DADMM_BWD_PF == 2
     // the five streams of (iteration kk, tile tt_) into one set of registers; every load is
     // unconditional (branch-free: a load under a branch makes the compiler drain the queue)
     f32x4 cy1[P], cu[P], cg[P], cyk[P], cgr[P];
@@ -280,7 +237,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
         issue1(3, K - 1, 0, cyk);
         issue1(4, K - 1, 0, cgr);
     }
-#endif
     __syncthreads();
 
     for (int k = K - 1; k >= 0; --k) {
@@ -320,11 +276,7 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
             [[maybe_unused]] const rsrc_t ruk = make_rsrc(a.Urec + (size_t)k * S, state_bytes);
             [[maybe_unused]] const rsrc_t rgy = make_rsrc(a.gY + (size_t)k * S, state_bytes);
             [[maybe_unused]] const rsrc_t rd0 = make_rsrc(a.d0, state_bytes);
-#if DADMM_BWD_ROT
 #pragma unroll 1
-#else
-#pragma unroll
-#endif
             for (int tt = 0; tt < T2; ++tt) {
                 const int n0 = (w * T2 + tt) * 16 + 4 * h;
                 const bool ok = n0 < n;
@@ -333,7 +285,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                 const uint32_t vrow = ok ? (uint32_t)((s * P * n + n0) * 4) : 0x80000000u;
                 // live ranges kept short (register budget): [P][4] temporaries t1, t2
                 float t1[P][4], t2[P][4];
-#if DADMM_BWD_PF == 2
                 // this tile's streams were issued a tile (or the GEMM phases) ago; each stream of
                 // the next tile (after the last tile: iteration k - 1's first) is issued into the
                 // same registers right after this tile's last read of it
@@ -346,21 +297,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 #define pgr cgr
 #define BWD_LD(pre, rs) (pre[p])
 #define BWD_NEXT(c, arr) issue1(c, nk, ntt, arr)
-#elif DADMM_BWD_PF
-                f32x4 py1[P], pu[P], pg[P], pyk[P], pgr[P];
-#pragma unroll
-                for (int p = 0; p < P; ++p) {
-                    const uint32_t so = (uint32_t)(p * n * 4);
-                    py1[p] = bload4(ry1, vrow, so);
-                    pu[p] = bload4(ruk, vrow, so);
-                    pg[p] = bload4(rgy, vrow, so);
-                    pyk[p] = k > 0 ? bload4(ryk, vrow, so) : bload4(rd0, vrow, so);
-                    pgr[p] = bload4(rgr, vrow, so);
-                }
-#define BWD_LD(pre, rs) (pre[p])
-#else
-#define BWD_LD(pre, rs) bload4(rs, vrow, (uint32_t)(p * n * 4))
-#endif
                 // t2 = delta_{k+1} formed from y_{k+1} exactly as the forward did
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
@@ -368,9 +304,7 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 #pragma unroll
                     for (int r = 0; r < 4; ++r) t1[p][r] = v[r];
                 }
-#if DADMM_BWD_PF == 2
                 BWD_NEXT(0, cy1);
-#endif
                 cons(t1, t2, mk);
                 const uint32_t md1 = clamp_delta(t2, a.variant);
                 fence();
@@ -392,10 +326,8 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                         Ub[p][BWD_ROW(e, r)] = wb;
                     }
                 }
-#if DADMM_BWD_PF == 2
                 BWD_NEXT(1, cu);
                 BWD_NEXT(2, cg);
-#endif
                 cons(t1, t2, mk);   // t2 = 2 L d_bar
 #pragma unroll
                 for (int p = 0; p < P; ++p)
@@ -403,7 +335,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                     for (int r = 0; r < 4; ++r) yb[p][BWD_ROW(4 * tt + r, r)] += t2[p][r];
                 fence();
                 // t1 = y_k; t2 = delta_k (k > 0: formed from y_k as the forward did; k = 0: d0)
-#if DADMM_BWD_PF
                 if (k > 0) {
 #pragma unroll
                     for (int p = 0; p < P; ++p)
@@ -422,28 +353,7 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                         }
                     }
                 }
-#if DADMM_BWD_PF == 2
                 BWD_NEXT(3, cyk);
-#endif
-#else
-#pragma unroll
-                for (int p = 0; p < P; ++p) {
-                    const f32x4 v = bload4(ryk, vrow, (uint32_t)(p * n * 4));
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) t1[p][r] = v[r];
-                }
-                if (k > 0) {
-                    cons(t1, t2, mk);
-                    clamp_delta(t2, a.variant);
-                } else {
-#pragma unroll
-                    for (int p = 0; p < P; ++p) {
-                        const f32x4 v = bload4(rd0, vrow, (uint32_t)(p * n * 4));
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) t2[p][r] = v[r];
-                    }
-                }
-#endif
                 fence();
                 // primal update + gradient clamp adjoint (:73-93)
 #pragma unroll
@@ -469,7 +379,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                     }
                     *(f32x4*)(Glds + (p * BT + j) * YS + n0) = gbv;
                 }
-#if DADMM_BWD_PF == 2
                 BWD_NEXT(4, cgr);
 #undef py1
 #undef pu
@@ -477,8 +386,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 #undef pyk
 #undef pgr
 #undef BWD_NEXT
-#endif
-#if DADMM_BWD_ROT
                 // rotate: the next tile's carried state moves to rows 0..3 (T2 rotations: identity)
 #pragma unroll
                 for (int p = 0; p < P; ++p)
@@ -493,7 +400,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
                         yb[p][4 * (T2 - 1) + r] = y0v;
                         Ub[p][4 * (T2 - 1) + r] = u0v;
                     }
-#endif
             }
         }
         __syncthreads();
@@ -522,12 +428,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 #pragma unroll
                     for (int r = 0; r < 4; ++r) acc[i] = mfma4(av[t & 1][i][r], bv[r], acc[i]);
                 }
-                if constexpr (DADMM_BWD_AT_DMA) {
-                    if (t == NB - 1 && has_tiles) {   // GEMM2's first quarters, across the barrier
-#pragma unroll
-                        for (int q = 0; q + 1 < BWD_QD && q < P * T2 * 4; ++q) dma_quarter(q);
-                    }
-                }
             }
 #pragma unroll
             for (int i = 0; i < TH; ++i)
@@ -537,34 +437,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 
         // ---- GEMM2: y_bar_p += A_p^T R_p on this wave's n-tiles, as (agent, tile) chains of 16
         //      MFMAs; the A^T rows of the next chain load under the current one ----------------
-#if DADMM_BWD_AT_DMA
-        if (has_tiles) {
-            constexpr int NS = P * T2;
-            constexpr int NQ = NS * 4;
-            const int lane = threadIdx.x & 63;
-#pragma unroll
-            for (int c = 0; c < NS; ++c) {
-                const int p = c / T2, tt = c % T2;
-                f32x4 rv[MP / 16];
-#pragma unroll
-                for (int t = 0; t < MP / 16; ++t)
-                    rv[t] = *(const f32x4*)(Rlds + (p * BT + j) * RS + 4 * h + 16 * t);
-                f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-                for (int t = 0; t < MP / 16; ++t) {
-                    const int q = c * 4 + t;
-                    if (q + BWD_QD - 1 < NQ) dma_quarter(q + BWD_QD - 1);
-                    // no other VMEM op is issued in this loop: the younger ops are the later DMAs
-                    wait_vm(NQ - 1 - q < BWD_QD - 1 ? NQ - 1 - q : BWD_QD - 1);
-                    const f32x4 av = *(const f32x4*)(Qlds + (w * BWD_QD + q % BWD_QD) * 256 + lane * 4);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) gc = mfma4(av[r], rv[t][r], gc);
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) yb[p][4 * tt + r] += gc[r];
-            }
-        }
-#else
         if (has_tiles) {
             constexpr int NS = P * T2;
             f32x4 tring[2][MP / 16];
@@ -595,7 +467,6 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
             }
         }
 
-#endif
 
         // ---- dhyp partial sums of iteration k: lane -> wave -> workgroup --------------------
 #pragma unroll
@@ -603,12 +474,8 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 float v = part[p][c];
-                if constexpr (DADMM_BWD_DPP) {
-                    v = wave_sum_dpp(v);
-                } else {
-#pragma unroll
-                    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-                }
+                v = wave_sum_dpp(v);
+            
                 if (lane == 0) red[(w * P + p) * 4 + c] = v;
             }
         __syncthreads();
@@ -624,16 +491,12 @@ __device__ __forceinline__ void body(const BackwardArgs& a, float* __restrict__ 
 }
 
 template <int P, int NT, int GRAPH>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVES == 4 ? 1 : 2, WAVES == 4 ? 1 : 2)))
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void backward_kernel(BackwardArgs a) {
     constexpr int NP = NT * 64;
-    __shared__ __attribute__((aligned(16))) float lds[P * BT * ((NP + 4) + (M_PAD + 4)) + WAVES * P * 4 +
-                                                      (DADMM_BWD_AT_DMA ? WAVES * BWD_QD * 256 : 0)];
+    __shared__ __attribute__((aligned(16))) float lds[P * BT * ((NP + 4) + (M_PAD + 4)) + WAVES * P * 4];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (WAVES == 4 || w < 4)
-        body<P, NT, GRAPH, 0>(a, lds, w);
-    else
-        body<P, NT, GRAPH, 1>(a, lds, w);
+    body<P, NT, GRAPH, 0>(a, lds, w);
 }
 
 // dhyp[k][hh][c] = sum over workgroups (and over agents for H = 1) of partial[wg][k][p][c]; one
@@ -689,9 +552,6 @@ backward_fn_ptr pick_nt(int nt, int graph) {
 }  // namespace bwd
 
 backward_fn_ptr find_backward(int P, int nt, int graph) {
-#ifdef DADMM_ONLY_H   // compile-time experiments: instantiate the headline shape only
-    return (P == 5 && nt == 4 && graph == GRAPH_SHARED) ? &bwd::launch<5, 4, GRAPH_SHARED> : nullptr;
-#else
     switch (P) {
         case 1: return bwd::pick_nt<1>(nt, graph);
         case 2: return bwd::pick_nt<2>(nt, graph);
@@ -701,7 +561,6 @@ backward_fn_ptr find_backward(int P, int nt, int graph) {
         case 6: return bwd::pick_nt<6>(nt, graph);
         default: return nullptr;
     }
-#endif
 }
 
 hipError_t launch_backward_reduce(const float* partial, float* dhyp, int nwg, int K, int P, int H,

@@ -36,53 +36,20 @@
 #ifndef DADMM_FUSED_REC
 #define DADMM_FUSED_REC 0
 #endif
-// GEMM2's A^T operand through a per-wave LDS ring filled by LDS-DMA (buffer_load ... lds):
-// DADMM_AT_QD quarter-chains (16 n-rows x 16 m, 1 KB per wave) deep, no VGPRs in flight
-#ifndef DADMM_AT_DMA
-#define DADMM_AT_DMA 1
-#endif
-#ifndef DADMM_A_RING
-#define DADMM_A_RING 3
-#endif
-// GEMM2 as paired chains: each agent's T2 n-tiles run as T2 interleaved accumulator chains that
-// share the R_p operand (independent MFMAs back to back instead of one dependent chain), with
-// the agent's primal update under the next agent's MFMAs
-#ifndef DADMM_G2_PAIR
-#define DADMM_G2_PAIR 1
-#endif
-#ifndef DADMM_AT_QD
-#define DADMM_AT_QD (DADMM_G2_PAIR ? 6 : 5)
-#endif
-// DADMM_AT_DMA = 0 with DADMM_G2_PAIR: GEMM2's A^T through a register ring of DADMM_AT_RS steps
-// (one step = the T2 fragments of (agent, m-block)), the first steps issued under GEMM1
-#ifndef DADMM_AT_RS
-#define DADMM_AT_RS 3
-#endif
-// Per-agent-group synchronisation instead of the two workgroup barriers per iteration (8-wave
-// workgroups, DMA paired GEMM2): LDS arrival counters let a half of the waves run GEMM2 of the
-// agents whose R is complete while the other half still runs GEMM1 (see fused_body)
-#ifndef DADMM_AGENT_SYNC
-#define DADMM_AGENT_SYNC 0
-#endif
-// LDS row padding (floats) of the y tile Ylds and the R tile Rlds. The tiles are read with
-// ds_read_b128 (GEMM1's B operand, GEMM2's R operand, the primal update): a 16-lane b128 group
-// {j = 0-3, 12-15 at h} + {j = 4-11 at h + 1} hits distinct 16-B bank slots iff the row stride is
-// 8 mod 64 floats (slot = (2 j + h) mod 16); +4 (slot = j + h) puts two lanes of every group on
-// one slot (2-way: 8 LDS cycles per read instead of 4). Measured at H (three interleaved rounds,
-// bit-identical): +8 / +8 0.589-0.648 ms vs +4 / +4 0.604-0.606 ms (profiles/r04/variants_r04c.txt)
-#ifndef DADMM_YS_PAD
-#define DADMM_YS_PAD 8
-#endif
-#ifndef DADMM_RS_PAD
-#define DADMM_RS_PAD 8
-#endif
-// DADMM_DUAL_B128=1: the deferred dual update reads the lane's 4 rows of a chunk of every agent as
-// one ds_read_b128 each (conflict-free with DADMM_YS_PAD 8) and updates the 4 rows back to back,
-// instead of 4 ds_read_b32 per agent (a b32 read of the same row position r by 32 lanes of
-// 16-B aligned rows touches at most 8 of the 32 banks: 4-way conflicts for any row stride)
-#ifndef DADMM_DUAL_B128
-#define DADMM_DUAL_B128 0
-#endif
+// Decisions measured at the headline shape (the A/B switches were removed in
+// round 6 once their experiments closed):
+//   * GEMM2's A^T operand through a per-wave LDS ring filled by LDS-DMA (buffer_load ... lds), six
+//     quarter-chains (16 n-rows x 16 m, 1 KB per wave) deep, no VGPRs in flight (a 2-4 step
+//     register ring, a 5-deep ring and inline-asm DMAs were no faster);
+//   * GEMM2 as paired chains: an agent's T2 n-tiles run as T2 interleaved accumulator chains that
+//     share the R_p operand, the agent's primal update under the next agent's MFMAs;
+//   * GEMM1's A operand through a 3-step register ring (4 steps: no faster);
+//   * LDS rows of Ylds / Rlds padded by 8 floats: a 16-lane ds_read_b128 group {j = 0-3, 12-15
+//     at h} + {j = 4-11 at h + 1} hits distinct 16-B bank slots iff the row stride is 8 mod 64
+//     floats (+8: 0.589-0.648 ms vs +4: 0.604-0.606 ms, profiles/r04/variants_r04c.txt);
+//   * two workgroup barriers per iteration (per-agent-group LDS arrival counters: no faster), the
+//     second half of the waves at raised priority, the deferred dual update's reads as
+//     ds_read_b32 (b128 chunks removed the remaining bank conflicts but spilled: slower).
 
 namespace dadmm {
 
@@ -129,11 +96,8 @@ __device__ __forceinline__ void bstore4(f32x4 v, rsrc_t r, uint32_t voff, uint32
 // The iterate stream Y (K*B*P*n*4 bytes, 524 MB at the headline shape) is written once and never
 // re-read by the kernel; its cache policy decides whether it evicts the operator A / A^T that
 // every workgroup re-reads from L2 each iteration. aux: 16 = sc1, 2 = nt.
-#ifndef DADMM_Y_AUX
-#define DADMM_Y_AUX 16
-#endif
 __device__ __forceinline__ void bstore4_stream(f32x4 v, rsrc_t r, uint32_t voff) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, voff, 0, DADMM_Y_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, voff, 0, 16);
 }
 
 // torch.clamp(x, lo, hi) == min(max(x, lo), hi) for every non-NaN x. A NaN never needs to be
@@ -154,17 +118,6 @@ __device__ __forceinline__ float mclamp(float x, float lo, float hi) {
 // memory queue (no vmcnt wait at the top of an iteration)
 typedef const __attribute__((address_space(4))) float cfloat;
 __device__ __forceinline__ bool finitef(float x) { return __builtin_isfinite(x); }
-// Ablation knobs (timing builds only, never shipped): replace operand loads by register values.
-#ifdef DADMM_ABL_A_CONST
-#define ABL_A(x) ((f32x4){__builtin_bit_cast(float, voffA), 0.001f, 0.002f, 0.003f})
-#else
-#define ABL_A(x) (x)
-#endif
-#ifdef DADMM_ABL_AT_CONST
-#define ABL_AT(x) ((f32x4){__builtin_bit_cast(float, voffAt), 0.001f, 0.002f, 0.003f})
-#else
-#define ABL_AT(x) (x)
-#endif
 
 // A per-iteration opaque copy of a loop-invariant offset: keeps `base + constant` inside the loop
 // so instruction selection folds the constant into the load's immediate offset instead of LICM
@@ -179,25 +132,6 @@ __device__ __forceinline__ uint32_t fresh_s(uint32_t x) {   // same, for a wave-
     return x;
 }
 
-// Diagnostic build only (-DDADMM_STAMPS, scripts/stamps.py): per-phase cycle sums per wave.
-#ifdef DADMM_STAMPS
-__device__ unsigned long long* g_stamps;
-__device__ __forceinline__ unsigned long long stamp() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define STAMP_DECL unsigned long long st_acc[5] = {0, 0, 0, 0, 0}, st_prev = stamp();
-#define STAMP(i) do { const unsigned long long t_ = stamp(); st_acc[i] += t_ - st_prev; st_prev = t_; } while (0)
-#define STAMP_FLUSH(w) do { if ((threadIdx.x & 63) == 0 && g_stamps != nullptr) for (int i_ = 0; i_ < 5; ++i_) \
-    g_stamps[((size_t)blockIdx.x * 8 + (w)) * 8 + i_] = st_acc[i_]; } while (0)
-#else
-#define STAMP_DECL
-#define STAMP(i) do {} while (0)
-#define STAMP_FLUSH(w) do {} while (0)
-#endif
 
 // The paired-chain GEMM2's A^T ring, simulated at compile time: quarter q = (4 p + t) T2 + tt is
 // A^T_p rows of n-tile tt, m-block t. PRE quarters are issued before the phase (under GEMM1's
@@ -206,9 +140,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 // then waits for its T2 quarters; after the MFMAs of agent p >= 1 the primal update of agent
 // p - 1 issues T2 * SPQ stores. younger[q] = the VMEM ops issued after quarter q's DMA and
 // before its wait, i.e. the exact s_waitcnt vmcnt(younger[q]) that guarantees it has landed.
-// FLUSH (agent sync): the stores of position FLUSH - 1 are issued before position FLUSH's steps
-// instead of after them (-1: none).
-template <int P, int T2, int QD, int SPQ, int FLUSH = -1>
+template <int P, int T2, int QD, int SPQ>
 struct G2Plan {
     static constexpr int NQ = P * 4 * T2;
     static constexpr int PRE = QD < NQ ? QD : NQ;
@@ -218,50 +150,16 @@ struct G2Plan {
         int op = 0, issued = 0;
         for (; issued < PRE; ++issued) pos[issued] = op++;
         for (int p = 0; p < P; ++p) {
-            if (p == FLUSH && p > 0) op += T2 * SPQ;
             for (int t = 0; t < 4; ++t) {
                 const int q0 = (4 * p + t) * T2;
                 const int lim = q0 + QD - 1 < NQ - 1 ? q0 + QD - 1 : NQ - 1;
                 for (; issued <= lim; ++issued) pos[issued] = op++;
                 for (int tt = 0; tt < T2; ++tt) younger[q0 + tt] = op - 1 - pos[q0 + tt];
             }
-            if (p > 0 && p != FLUSH) op += T2 * SPQ;
+            if (p > 0) op += T2 * SPQ;
         }
     }
 };
-
-// LDS arrival counters of the agent-group synchronisation (one lane adds; the spin reads with
-// s_sleep). The adder first waits for its own LDS writes (lgkmcnt(0)); LDS is coherent in the CU.
-__device__ __forceinline__ void lds_signal(uint32_t* c, int lane) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_wait(uint32_t* c, uint32_t target) {
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-        __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
-}
-
-// DADMM_DMA_ASM=1: the A^T ring's LDS-DMA issued from inline asm. With the builtin the compiler
-// treats every later LDS read as a possible alias of an outstanding copy and adds its own
-// vmcnt waits before them (on top of the plan's exact waits); from inline asm the copies are
-// invisible to it and only the plan's waits (wait_vm(younger[q])) order them. Bit-identical, but
-// measured no faster here (0.599-0.613 vs 0.586-0.599 ms at H, profiles/r03/fused_dma_asm_r03.jsonl;
-// the streamed kernel needed it, dadmm_stream.hip), so off.
-#ifndef DADMM_DMA_ASM
-#define DADMM_DMA_ASM 0
-#endif
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4_t rsrc_words4(const void* base, uint32_t bytes) {
-    const uint64_t b = (uint64_t)base;
-    return (i32x4_t){(int)(uint32_t)b, (int)(uint32_t)(b >> 32) & 0xffff, (int)bytes, 0x00020000};
-}
-__device__ __forceinline__ void dma_lds16(uint32_t lds_addr, uint32_t voff, uint32_t soff, i32x4_t rsrc) {
-    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-                 :
-                 : "s"(lds_addr), "v"(voff), "s"(rsrc), "s"(soff)
-                 : "memory", "m0");
-}
 
 // Compiler-only memory barrier: bounds how far the scheduler hoists operand loads.
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
@@ -286,28 +184,17 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     constexpr int E = T2 * 4;                        // state elements per lane per agent
     constexpr int TH = (P - HALF + AS - 1) / AS;     // GEMM1 tiles of this wave: agents HALF + AS*i
     constexpr int THA = TH > 0 ? TH : 1;             // array extent (P = 1 leaves half 1 idle)
-    constexpr int YS = NP + DADMM_YS_PAD;            // LDS row strides (floats): the padding
-    constexpr int RS = MP + DADMM_RS_PAD;            //   breaks the power-of-two bank period
+    constexpr int YS = NP + 8;            // LDS row strides (floats): the padding
+    constexpr int RS = MP + 8;            //   breaks the power-of-two bank period
     // GEMM1 A-operand ring depth: one step in flight under the MFMAs of the current step. A
     // deeper ring for the small-state instantiations perturbs the register allocation of the
     // large ones compiled in the same module (MI355X_MICROARCH §5.4 rule 19): measured 65 VGPR
     // spills for P=5, n=256 with a conditional depth, 3 with a uniform depth of 2.
-    constexpr int RING = DADMM_A_RING;
+    constexpr int RING = 3;
     float* __restrict__ Ylds = lds;                  // [P][BT][YS]   y_k, n contiguous
     float* __restrict__ Rlds = lds + P * BT * YS;    // [P][BT][RS]   A y - b, m contiguous
-    float* __restrict__ Blds = Rlds + P * BT * RS;   // [P][BT][RS]   -b (not with DADMM_AT_DMA)
-    constexpr int QD = DADMM_AT_QD;
-    float* __restrict__ Qlds = Rlds + P * BT * RS;   // [WAVES][QD][256] A^T ring (DADMM_AT_DMA)
-
-    // agent-group sync (DADMM_AGENT_SYNC): Rrdy[h] counts the waves of half h that have stored
-    // their R tiles (4 per iteration), Ydone[h] the waves that have finished the primal updates
-    // of half h's agents (every wave with GEMM2 tiles, once per iteration). GEMM2 visits the
-    // agents of half 1 first (p odd), then half 0.
-    constexpr bool SYNC = DADMM_AGENT_SYNC && DADMM_AT_DMA && DADMM_G2_PAIR && WAVES == 8 && P > 1;
-    uint32_t* const cnt = (uint32_t*)(DADMM_AT_DMA ? Qlds + WAVES * QD * 256 : Blds + P * BT * RS);
-    constexpr int NODD = P / 2;                      // agents 1, 3, ...: the first GEMM2 positions
-    auto agent_at = [](int i) { return SYNC ? (i < NODD ? 2 * i + 1 : 2 * (i - NODD)) : i; };
-    constexpr int TILE_WAVES = (NB + T2 - 1) / T2;    // waves with GEMM2 tiles (has_tiles)
+    constexpr int QD = 6;                            // A^T ring depth (quarter-chains per wave)
+    float* __restrict__ Qlds = Rlds + P * BT * RS;   // [WAVES][QD][256] A^T ring
 
     const int lane = threadIdx.x & 63;
     const int j = lane & 15;             // sample within the tile (MFMA column)
@@ -322,9 +209,6 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     const uint32_t state_bytes = (uint32_t)((size_t)B * P * n * 4);
     const rsrc_t rA = make_rsrc(a.A, (uint32_t)(P * MP * NP * 4));
     const rsrc_t rAt = make_rsrc(a.At, (uint32_t)(P * MP * NP * 4));
-#if DADMM_DMA_ASM
-    const i32x4_t rAtw = rsrc_words4(a.At, (uint32_t)(P * MP * NP * 4));
-#endif
 
     // ---- graph data --------------------------------------------------------------------------
     uint32_t msk[P], ord[P];
@@ -380,8 +264,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
         }
     }
     // -b for this wave's GEMM1 tiles (agent HALF + AS*i, rows m = 16*mb + 4h + r) seeds every
-    // iteration's GEMM1 chains: in LDS next to R, or (DADMM_AT_DMA: that LDS holds the A^T ring)
-    // in registers
+    // iteration's GEMM1 chains, held in registers (the LDS next to R holds the A^T ring)
     f32x4 bseed[THA];
 #pragma unroll
     for (int i = 0; i < TH; ++i) {
@@ -392,8 +275,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
             const int mi = 16 * mb + 4 * h + r;
             v[r] = (sv && mi < m) ? -a.b[((size_t)s * P + p) * m + mi] : 0.0f;
         }
-        if constexpr (DADMM_AT_DMA) bseed[i] = v;
-        else *(f32x4*)(Blds + (p * BT + j) * RS + 16 * mb + 4 * h) = v;
+        bseed[i] = v;
     }
 
     // Reference guards at the top of an iteration (unfolded_DLASSO.py:55-61) can only fire at
@@ -450,32 +332,11 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     // ring slot q % QD of this wave (lane-linear: lane l's 16 bytes at l * 16, which is exactly the
     // MFMA A-operand fragment lane l reads back)
     auto dma_quarter = [&](const uint32_t (&vAt)[T2], int q) {
-#if DADMM_G2_PAIR
-        const int tt = q % T2, t = (q / T2) & 3, p = agent_at(q / (4 * T2));   // see G2Plan
-#else
-        const int c = q >> 2, t = q & 3;
-        const int p = c / T2, tt = c % T2;
-#endif
-#if DADMM_DMA_ASM
-        dma_lds16((uint32_t)(uintptr_t)(lds_void*)(Qlds + (w * QD + q % QD) * 256), vAt[tt] + 64 * t,
-                  (uint32_t)(p * NP * MP * 4), rAtw);
-#else
+        const int tt = q % T2, t = (q / T2) & 3, p = q / (4 * T2);   // see G2Plan
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rAt, (lds_void*)(Qlds + (w * QD + q % QD) * 256), 16,
                                                  vAt[tt] + 64 * t, (uint32_t)(p * NP * MP * 4), 0, 0);
-#endif
     };
 
-#if !DADMM_AT_DMA && DADMM_G2_PAIR
-    // GEMM2 A^T register ring: slot st % DADMM_AT_RS holds step st = 4 p + t, the A^T_p rows of the
-    // wave's T2 n-tiles at m-block t
-    f32x4 tring2[DADMM_AT_RS][T2];
-    auto load_at_step = [&](f32x4 (&slot)[T2], const uint32_t (&vAt)[T2], int st) {
-        const int p = st / 4, t = st % 4;
-#pragma unroll
-        for (int tt = 0; tt < T2; ++tt)
-            slot[tt] = ABL_AT(bload4(rAt, vAt[tt] + 64 * t, (uint32_t)(p * NP * MP * 4)));
-    };
-#endif
     // GEMM1 A-operand ring: slot t % RING holds A rows of step t (16 columns) for the TH tiles.
     // The first step of every iteration is issued before the previous iteration's last Y stores,
     // so it is not queued behind them (vmcnt counts loads and stores in order).
@@ -486,19 +347,12 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     auto load_a = [&](f32x4 (&slot)[THA], int t) {
 #pragma unroll
         for (int i = 0; i < TH; ++i)
-            slot[i] = ABL_A(bload4(rA, vA + 64 * t, (uint32_t)((HALF + AS * i) * MP * NP * 4)));
+            slot[i] = bload4(rA, vA + 64 * t, (uint32_t)((HALF + AS * i) * MP * NP * 4));
     };
 #pragma unroll
     for (int t = 0; t + 1 < RING; ++t) load_a(aring[t], t);
-#ifndef DADMM_HALF_PRIO
-#define DADMM_HALF_PRIO 1
-#endif
-    if (HALF == 1 && DADMM_HALF_PRIO) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half loses arbitration
-    if constexpr (SYNC) {
-        if (w == 0 && lane < 4) cnt[lane] = 0u;
-    }
+    if (HALF == 1) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half loses arbitration
     __syncthreads();
-    STAMP_DECL
 
     // dual update deferred from the previous iteration: delta_k = 2 L y_k for row e (all agents,
     // lane-local), GNN delta clamp, U_k = clamp(U_{k-1} + delta_k * eta_{k-1}) (:95-99)
@@ -530,10 +384,6 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
     };
 
     for (int k = 0; k < a.K; ++k) {
-        if constexpr (SYNC) {
-            // y_k of this half's agents complete in Ylds (every tile wave's primal updates)
-            if (k > 0) lds_wait(cnt + 2 + HALF, (uint32_t)(TILE_WAVES * k));
-        }
         vA = fresh(voffA);
         // shared graph: re-launder the (uniform) masks so the neighbour tests are evaluated in the
         // loop (s_bitcmp + branch) instead of being hoisted as P*P 64-bit condition registers
@@ -569,8 +419,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
             f32x4 acc[THA];
 #pragma unroll
             for (int i = 0; i < TH; ++i)
-                acc[i] = DADMM_AT_DMA ? bseed[i]
-                                      : *(const f32x4*)(Blds + ((HALF + AS * i) * BT + j) * RS + 16 * mb + 4 * h);
+                acc[i] = bseed[i];
             f32x4 bring[2][THA];
 #pragma unroll
             for (int i = 0; i < TH; ++i)
@@ -591,52 +440,21 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
                     for (int i = 0; i < TH; ++i) acc[i] = mfma4(av[i][r], bv[i][r], acc[i]);
-                if constexpr (DADMM_AT_DMA) {
-                    // GEMM2's first quarters, in flight across the barrier
-                    if (t == NB - 1 && has_tiles) {
-#pragma unroll
-                        for (int q = 0; q + 1 - DADMM_G2_PAIR < QD && q < P * T2 * 4; ++q) dma_quarter(vAt, q);
-                    }
-                }
-#if !DADMM_AT_DMA && DADMM_G2_PAIR
-                // GEMM2's first A^T steps, in flight across the barrier
+                // GEMM2's first quarters, in flight across the barrier
                 if (t == NB - 1 && has_tiles) {
 #pragma unroll
-                    for (int st = 0; st + 1 < DADMM_AT_RS && st < 4 * P; ++st) load_at_step(tring2[st], vAt, st);
+                    for (int q = 0; q < QD && q < P * T2 * 4; ++q) dma_quarter(vAt, q);
                 }
-#endif
-#if DADMM_DUAL_B128
-                // chunks tt with tt * NB / T2 == t: the 4 rows of every agent in one b128 read each
-#pragma unroll
-                for (int tt = 0; tt < T2; ++tt) {
-                    if ((tt * NB) / T2 == t && has_tiles) {
-                        f32x4 yc[P];
-#pragma unroll
-                        for (int p = 0; p < P; ++p) yc[p] = *(const f32x4*)ylds_at(p, 4 * tt);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            float yr[P];
-#pragma unroll
-                            for (int p = 0; p < P; ++p) yr[p] = yc[p][r];
-                            dual_update_row(4 * tt + r, mk, deferred, yr);
-                        }
-                    }
-                }
-#else
                 // rows e with e * NB / E == t
 #pragma unroll
                 for (int e = 0; e < E; ++e)
                     if ((e * NB) / E == t && has_tiles) dual_update_row(e, mk, deferred);
-#endif
             }
 #pragma unroll
             for (int i = 0; i < TH; ++i)
                 *(f32x4*)(Rlds + ((HALF + AS * i) * BT + j) * RS + 16 * mb + 4 * h) = acc[i];
         }
-        STAMP(0);
-        if constexpr (SYNC) lds_signal(cnt + HALF, lane);   // this wave's R tiles are in Rlds
-        else __syncthreads();
-        STAMP(1);
+        __syncthreads();
 
         // ---- GEMM2 (G_p = A_p^T R_p) as a sequence of (agent, n-tile) chains of 16 MFMAs; the
         //      A^T rows of the next chain load one chain ahead, and each chain's gradient
@@ -647,20 +465,9 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
             const rsrc_t rG = make_rsrc(REC ? a.Grec + (size_t)k * B * P * n : a.Y, REC ? state_bytes : 0u);
             const rsrc_t rUr = make_rsrc(REC ? a.Urec + (size_t)k * B * P * n : a.Y, REC ? state_bytes : 0u);
             [[maybe_unused]] constexpr int NS = P * T2;      // chains: s = p*T2 + tt
-#if !DADMM_AT_DMA && !DADMM_G2_PAIR
-            f32x4 tring[2][MP / 16];
-#endif
             [[maybe_unused]] f32x4 g[2];
             f32x4 rv[MP / 16];
             bool bad_g = false;
-#if !DADMM_AT_DMA && !DADMM_G2_PAIR
-            auto load_at = [&](f32x4 (&slot)[MP / 16], int s2) {
-                const int p = s2 / T2, tt = s2 % T2;
-#pragma unroll
-                for (int t = 0; t < MP / 16; ++t)
-                    slot[t] = ABL_AT(bload4(rAt, vAt[tt] + 64 * t, (uint32_t)(p * NP * MP * 4)));
-            };
-#endif
             // primal update of (agent p, tile tt) from its G (:73-93); iterate to LDS and Y[k]
             auto primal_update = [&](int s2, const f32x4& gp) {
                 const int p = s2 / T2, tt = s2 % T2;
@@ -691,34 +498,21 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                     yn[r] = v;
                 }
                 *(f32x4*)(Ylds + (p * BT + j) * YS + n0) = yn;
-#ifndef DADMM_ABL_NO_STORE
                 // Y[k][s][p][n0..n0+3]; rows past n go to an offset the range check drops
                 bstore4_stream(yn, rY, n0 < n ? voffY + (uint32_t)((p * n + nb * 16) * 4) : 0x80000000u);
-#endif
                 if constexpr (REC) {
                     const uint32_t o = n0 < n ? voffY + (uint32_t)((p * n + nb * 16) * 4) : 0x80000000u;
                     bstore4_stream(grv, rG, o);
                     bstore4_stream(urv, rUr, o);
                 }
             };
-#if DADMM_AT_DMA && DADMM_G2_PAIR
             // stores of one primal update (Y[k], and Grec / Urec when recording)
             constexpr int SPQ = REC ? 3 : 1;
-            constexpr int FL = SYNC ? NODD : -1;
-            constexpr G2Plan<P, T2, QD, SPQ, FL> plan{};
+            constexpr G2Plan<P, T2, QD, SPQ> plan{};
             f32x4 gp[2][T2];
 #pragma unroll
             for (int i = 0; i < P; ++i) {
-                const int p = agent_at(i);
-                if constexpr (SYNC) {
-                    if (i == NODD) {
-                        // the odd agents' last primal update, then release them to GEMM1(k+1)
-#pragma unroll
-                        for (int tt = 0; tt < T2; ++tt) primal_update(agent_at(i - 1) * T2 + tt, gp[(i - 1) & 1][tt]);
-                        lds_signal(cnt + 2 + 1, lane);
-                    }
-                    if (i == 0 || i == NODD) lds_wait(cnt + (i == 0 ? 1 : 0), (uint32_t)(4 * (k + 1)));
-                }
+                const int p = i;
                 compiler_fence();
 #pragma unroll
                 for (int t = 0; t < MP / 16; ++t)
@@ -738,7 +532,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
 #pragma unroll
                     for (int tt = 0; tt < T2; ++tt) {
                         wait_vm(plan.younger[q0 + tt]);
-                        av[tt] = ABL_AT(*(const f32x4*)(Qlds + (w * QD + (q0 + tt) % QD) * 256 + lane * 4));
+                        av[tt] = *(const f32x4*)(Qlds + (w * QD + (q0 + tt) % QD) * 256 + lane * 4);
                     }
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
@@ -752,117 +546,13 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
                     // to count them), before the last agent's Y stores
                     for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
                 }
-                if (i > 0 && i != FL) {
+                if (i > 0) {
 #pragma unroll
-                    for (int tt = 0; tt < T2; ++tt) primal_update(agent_at(i - 1) * T2 + tt, gp[(i - 1) & 1][tt]);
-                }
-            }
-#pragma unroll
-            for (int tt = 0; tt < T2; ++tt) primal_update(agent_at(P - 1) * T2 + tt, gp[(P - 1) & 1][tt]);
-            if constexpr (SYNC) lds_signal(cnt + 2 + 0, lane);   // the even agents' y_{k+1}
-#elif DADMM_G2_PAIR
-            // paired chains, A^T from the register ring (compiler-counted vmcnt waits)
-            constexpr int NST = 4 * P;
-            f32x4 gp[2][T2];
-#pragma unroll
-            for (int p = 0; p < P; ++p) {
-                compiler_fence();
-#pragma unroll
-                for (int t = 0; t < MP / 16; ++t)
-                    rv[t] = *(const f32x4*)(Rlds + (p * BT + j) * RS + 4 * h + 16 * t);
-                f32x4 gc[T2];
-#pragma unroll
-                for (int tt = 0; tt < T2; ++tt) gc[tt] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-                for (int t = 0; t < MP / 16; ++t) {
-                    const int st = 4 * p + t;
-                    if (st + DADMM_AT_RS - 1 < NST)
-                        load_at_step(tring2[(st + DADMM_AT_RS - 1) % DADMM_AT_RS], vAt, st + DADMM_AT_RS - 1);
-                    const f32x4(&av)[T2] = tring2[st % DADMM_AT_RS];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-#pragma unroll
-                        for (int tt = 0; tt < T2; ++tt) gc[tt] = mfma4(av[tt][r], rv[t][r], gc[tt]);
-                }
-#pragma unroll
-                for (int tt = 0; tt < T2; ++tt) gp[p & 1][tt] = gc[tt];
-                if (p + 1 == P && k + 1 < a.K) {
-                    for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
-                }
-                if (p > 0) {
-#pragma unroll
-                    for (int tt = 0; tt < T2; ++tt) primal_update((p - 1) * T2 + tt, gp[(p - 1) & 1][tt]);
+                    for (int tt = 0; tt < T2; ++tt) primal_update((i - 1) * T2 + tt, gp[(i - 1) & 1][tt]);
                 }
             }
 #pragma unroll
             for (int tt = 0; tt < T2; ++tt) primal_update((P - 1) * T2 + tt, gp[(P - 1) & 1][tt]);
-#elif DADMM_AT_DMA
-            constexpr int NQ = NS * 4;
-            // stores of one primal update (Y[k], and Grec / Urec when recording)
-            constexpr int SPQ = REC ? 3 : 1;
-#pragma unroll
-            for (int s2 = 0; s2 < NS; ++s2) {
-                compiler_fence();
-                if (s2 % T2 == 0) {
-                    const int p = s2 / T2;
-#pragma unroll
-                    for (int t = 0; t < MP / 16; ++t)
-                        rv[t] = *(const f32x4*)(Rlds + (p * BT + j) * RS + 4 * h + 16 * t);
-                }
-                f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-                for (int t = 0; t < MP / 16; ++t) {
-                    const int q = s2 * 4 + t;
-                    if (q + QD - 1 < NQ) dma_quarter(vAt, q + QD - 1);
-                    // quarter q has landed once no more than the VMEM ops issued after its DMA
-                    // are in flight: the later DMAs, and the primal updates' stores issued after
-                    // quarters u in [q - QD + 1, q - 1] with u = 3 mod 4, u >= 7 (chain >= 1)
-                    int younger = NQ - 1 - q < QD - 1 ? NQ - 1 - q : QD - 1;
-#pragma unroll
-                    for (int u = q - QD + 1; u < q; ++u)
-                        if (u >= 7 && (u & 3) == 3) younger += SPQ;
-                    wait_vm(younger);
-                    const f32x4 av = ABL_AT(*(const f32x4*)(Qlds + (w * QD + q % QD) * 256 + lane * 4));
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) gc = mfma4(av[r], rv[t][r], gc);
-                }
-                g[s2 & 1] = gc;
-                if (s2 + 1 == NS && k + 1 < a.K) {
-                    // next iteration's first GEMM1 steps, after every ring wait (so no wait has
-                    // to count them), before the last chain's Y stores
-                    for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
-                }
-                if (s2 > 0) primal_update(s2 - 1, g[(s2 - 1) & 1]);
-            }
-#else
-            load_at(tring[0], 0);
-#pragma unroll
-            for (int s2 = 0; s2 < NS; ++s2) {
-                if (s2 + 1 < NS) {
-                    load_at(tring[(s2 + 1) & 1], s2 + 1);
-                } else if (k + 1 < a.K) {
-                    // next iteration's first GEMM1 steps: before the last chains' Y stores
-                    for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
-                }
-                compiler_fence();
-                if (s2 % T2 == 0) {
-                    const int p = s2 / T2;
-#pragma unroll
-                    for (int t = 0; t < MP / 16; ++t)
-                        rv[t] = *(const f32x4*)(Rlds + (p * BT + j) * RS + 4 * h + 16 * t);
-                }
-                f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-                for (int t = 0; t < MP / 16; ++t)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) gc = mfma4(tring[s2 & 1][t][r], rv[t][r], gc);
-                g[s2 & 1] = gc;
-                if (s2 > 0) primal_update(s2 - 1, g[(s2 - 1) & 1]);
-            }
-#endif
-#if !DADMM_G2_PAIR
-            primal_update(NS - 1, g[(NS - 1) & 1]);
-#endif
             status |= bad_g ? 4u : 0u;
         } else if (k + 1 < a.K) {
             for (int t0 = 0; t0 + 1 < RING; ++t0) load_a(aring[t0], t0);
@@ -870,12 +560,8 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
 #pragma unroll
         for (int p = 0; p < P; ++p) et_prev[p] = et[p];
         vclip_prev = vclip;
-        STAMP(2);
-        STAMP(3);
-        if constexpr (!SYNC) __syncthreads();
-        STAMP(4);
+        __syncthreads();
     }
-    STAMP_FLUSH(w);
 
     if (a.U_out != nullptr && has_tiles) {
         // the dual update of the last iteration (deferred like the others)
@@ -911,27 +597,14 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, float* __restrict
 template <int P, int NT, int GRAPH, int WV, bool REC>
 __global__ __launch_bounds__(WV * 64) void fused_forward_kernel(FusedArgs a) {
     constexpr int NP = NT * 64;
-    __shared__ __attribute__((aligned(16))) float lds[(DADMM_AT_DMA
-        ? P * BT * ((NP + DADMM_YS_PAD) + (M_PAD + DADMM_RS_PAD)) + WV * DADMM_AT_QD * 256
-        : P * BT * ((NP + DADMM_YS_PAD) + 2 * (M_PAD + DADMM_RS_PAD))) + 4];   // + the agent-sync counters
+    // Ylds + Rlds + the waves' A^T rings
+    __shared__ __attribute__((aligned(16))) float lds[P * BT * ((NP + 8) + (M_PAD + 8)) + WV * 6 * 256];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave id, in an SGPR
-    if constexpr (WV == 4) {
-        fused_body<P, NT, GRAPH, 4, 0, REC>(a, lds, w);
-    } else if constexpr (WV == 16) {   // 4 waves per SIMD (timing experiments)
-        if (w < 4)
-            fused_body<P, NT, GRAPH, 16, 0, REC>(a, lds, w);
-        else if (w < 8)
-            fused_body<P, NT, GRAPH, 16, 1, REC>(a, lds, w);
-        else if (w < 12)
-            fused_body<P, NT, GRAPH, 16, 2, REC>(a, lds, w);
-        else
-            fused_body<P, NT, GRAPH, 16, 3, REC>(a, lds, w);
-    } else {
-        if (w < 4)
-            fused_body<P, NT, GRAPH, 8, 0, REC>(a, lds, w);
-        else
-            fused_body<P, NT, GRAPH, 8, 1, REC>(a, lds, w);
-    }
+    static_assert(WV == 8, "8 waves per workgroup (2 per SIMD; 4 and 16 measured slower, DESIGN.md §4.1)");
+    if (w < 4)
+        fused_body<P, NT, GRAPH, 8, 0, REC>(a, lds, w);
+    else
+        fused_body<P, NT, GRAPH, 8, 1, REC>(a, lds, w);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -965,11 +638,6 @@ static fused_fn_ptr pick_nt(int nt, int graph) {
     return nullptr;
 }
 
-#if defined(DADMM_STAMPS) && !DADMM_FUSED_REC
-extern "C" int dadmm_debug_set_stamps(void* buf) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -3;
-}
-#endif
 
 // This file is compiled twice (csrc/Makefile): DADMM_FUSED_REC = 0 defines find_fused (inference),
 // DADMM_FUSED_REC = 1 defines find_fused_rec (training: also records Grec / Urec).
@@ -978,9 +646,6 @@ fused_fn_ptr find_fused_rec(int P, int nt, int graph) {
 #else
 fused_fn_ptr find_fused(int P, int nt, int graph) {
 #endif
-#ifdef DADMM_ONLY_H   // compile-time experiments: instantiate the headline shape only
-    return (P == 5 && nt == 4 && graph == GRAPH_SHARED) ? &launch_fused<5, 4, GRAPH_SHARED> : nullptr;
-#else
     switch (P) {
         case 1: return pick_nt<1>(nt, graph);
         case 2: return pick_nt<2>(nt, graph);
@@ -990,7 +655,6 @@ fused_fn_ptr find_fused(int P, int nt, int graph) {
         case 6: return pick_nt<6>(nt, graph);
         default: return nullptr;
     }
-#endif
 }
 
 }  // namespace dadmm

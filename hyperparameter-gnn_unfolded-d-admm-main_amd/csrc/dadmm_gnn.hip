@@ -42,44 +42,14 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int THREADS = 256;   // 4 waves
 constexpr int WAVES = 4;
-// gram_kernel's GEMM1 with x staged through LDS once per workgroup (m_pad <= 16 WAVES GQ_MAX):
-// bit-identical, but measured slower (configs[2] adjoint 17.8 vs 14.8 ms, configs[4] shard forward
-// 102.8 vs 97.3 ms, profiles/r04/variants_r04c.txt: the chunk barriers serialise the waves), so off
-#ifndef DADMM_GRAM_XLDS
-#define DADMM_GRAM_XLDS 0
-#endif
-constexpr int GQ_MAX = 2;      // m-blocks per wave in that form
-// gram as one wave per (16-sample tile, agent) item, R in registers (gram_w1_kernel; m <= 128):
-// bit-identical, measured no faster (configs[2] adjoint 14.5-14.6 vs 14.5-14.9 ms, configs[4]
-// shard forward 97.1-97.6 vs 96.8-97.3 ms, profiles/r04/variants_r04d.txt), so off
-#ifndef DADMM_GRAM_W1
-#define DADMM_GRAM_W1 0
-#endif
-// gram_kernel mode 2: the out rows prefetched one GEMM2 unit ahead
-#ifndef DADMM_GRAM_OPF
-#define DADMM_GRAM_OPF 1
-#endif
-// gram_kernel (round 5): GEMM1's ring 8 deep where the column steps divide, and a wave's whole
-// GEMM2 (<= 4 units) loaded at once
-#ifndef DADMM_GRAM_GD8
-#define DADMM_GRAM_GD8 1
-#endif
-// DADMM_SBW_DPP=1: the step adjoint's per-sample hyper-parameter wave sums on DPP moves and
-// readlanes (wave_sum_dpp) instead of six ds_bpermute round trips each
-#ifndef DADMM_SBW_DPP
-#define DADMM_SBW_DPP 1
-#endif
-#ifndef DADMM_GRAM_G2ALL
-#define DADMM_GRAM_G2ALL 1
-#endif
-// update_item: the guard flags and y_k's table entry loaded together (round 5)
-#ifndef DADMM_STEP_EARLY
-#define DADMM_STEP_EARLY 1
-#endif
-// gram_kernel<true> (round 5) for grids of <= 2 items per CU at m_pad = 64, n_pad = 256
-#ifndef DADMM_GRAM_SMALL
-#define DADMM_GRAM_SMALL 1
-#endif
+// Decisions (variants measured and dropped; git history holds them, DESIGN.md §4 the numbers):
+// gram_kernel's GEMM1 with x staged through LDS (slower: the chunk barriers serialise the waves,
+// profiles/r04/variants_r04c.txt) and a one-wave-per-item gram with R in registers (no faster,
+// variants_r04d.txt) are gone. Kept: gram_kernel mode 2 prefetches the out rows one GEMM2 unit
+// ahead; GEMM1's ring is 8 deep where the column steps divide and a wave's whole GEMM2 (<= 4
+// units) is loaded at once (round 5); the step adjoint's per-sample hyper-parameter sums run on
+// DPP moves and readlanes (wave_sum_dpp); update_item loads the guard flags and y_k's table entry
+// together; gram_kernel<true> serves grids of <= 2 items per CU at m_pad = 64, n_pad = 256.
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -246,76 +216,6 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
         return;
     }
 
-#if DADMM_GRAM_XLDS
-    if (mode != 1 && MP <= 16 * WAVES * GQ_MAX) {
-        // GEMM1 with the x operand staged once per workgroup: 64-column chunks of the 16 samples'
-        // rows (4 KB) are loaded by all four waves together — lane l of wave w fetches 16 bytes of
-        // sample 4 w + l / 16, i.e. four full 256-byte row segments per wave instruction — and
-        // written to a double-buffered LDS chunk with the column quad XOR-swizzled by the sample
-        // (row sl, quad q at slot sl * 16 + (q ^ sl)), so the MFMA B-operand reads (lane (j, h),
-        // quad 4 t + h of sample j) hit 16 distinct 16-byte bank slots per b128 group. Every
-        // wave then reads x from LDS instead of loading the full x itself (the m-blocks of one
-        // (tile, agent) item share it), and an idle wave (m < 64) still helps load. The MFMA
-        // order is the loop below's (one chain per m-block, columns ascending): unchanged.
-        bool zero = false;
-        const float* xs = x_raw != nullptr ? x_raw : y_source(a, k, zero);
-        float* Xlds = lds + BT * RS;                  // [2][16][64] chunk double buffer
-        const int NC = NP / 64;
-        const uint32_t xbytes = zero ? 0u : (uint32_t)((size_t)B * P * n * 4);
-        const __amdgpu_buffer_rsrc_t rx =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), 0, (int)xbytes, 0x00020000);
-        const int sl = 4 * w + (lane >> 4);           // sample row this lane loads
-        const int qx = (lane & 15) ^ sl;              // its column quad (swizzled slot lane & 15)
-        const int sg = tile * BT + sl;
-        auto ldx = [&](int c) -> f32x4 {
-            const int col = 64 * c + 4 * qx;
-            const uint32_t off = (sg < B && col < n) ? (uint32_t)((((size_t)sg * P + p) * n + col) * 4)
-                                                     : 0x80000000u;
-            return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
-        };
-        const int nq = (MP / 16 - w + WAVES - 1) / WAVES;   // this wave's m-blocks (<= GQ_MAX)
-        const int mlim = (m + 15) / 16;
-        f32x4 acc[GQ_MAX], ar[2][GQ_MAX][4];
-        const float* arow[GQ_MAX];
-#pragma unroll
-        for (int g = 0; g < GQ_MAX; ++g) {
-            acc[g] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-            arow[g] = a.A + ((size_t)p * MP + 16 * (w + WAVES * g) + j) * NP + 4 * h;
-        }
-        auto lda = [&](f32x4 (&dst)[GQ_MAX][4], int c) {
-#pragma unroll
-            for (int g = 0; g < GQ_MAX; ++g)
-                if (g < nq && w + WAVES * g < mlim) {
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) dst[g][t] = *(const f32x4*)(arow[g] + 64 * c + 16 * t);
-                }
-        };
-        f32x4 xr[2];
-        xr[0] = ldx(0);
-        if (NC > 1) xr[1] = ldx(1);
-        lda(ar[0], 0);
-        for (int c = 0; c < NC; ++c) {
-            float* slot = Xlds + (c & 1) * (BT * 64);
-            *(f32x4*)(slot + (sl * 16 + (lane & 15)) * 4) = xr[c & 1];
-            __syncthreads();
-            if (c + 2 < NC) xr[c & 1] = ldx(c + 2);
-            if (c + 1 < NC) lda(ar[(c + 1) & 1], c + 1);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const f32x4 bv = *(const f32x4*)(slot + (j * 16 + ((4 * t + h) ^ j)) * 4);
-#pragma unroll
-                for (int g = 0; g < GQ_MAX; ++g)
-                    if (g < nq && w + WAVES * g < mlim) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) acc[g] = mfma4(ar[c & 1][g][t][r], bv[r], acc[g]);
-                    }
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < GQ_MAX; ++g)
-            if (g < nq) *(f32x4*)(Rlds + j * RS + 16 * (w + WAVES * g) + 4 * h) = acc[g];
-    } else
-#endif
     if (mode != 1) {
         bool zero = false;
         const float* xs = x_raw != nullptr ? x_raw : y_source(a, k, zero);
@@ -359,7 +259,7 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
                         }
                     }
                 };
-                if (DADMM_GRAM_GD8 && T % 8 == 0)
+                if (T % 8 == 0)
                     gemm1(std::integral_constant<int, 8>{});
                 else
                     gemm1(std::integral_constant<int, 4>{});
@@ -397,7 +297,7 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
             if (4 * mg + t < mbk) dst[t] = *(const f32x4*)(atb + (size_t)16 * nb * MP + 64 * mg + 16 * t);
     };
     const int units = (NP / 16 - w + WAVES - 1) / WAVES * MG;
-    if (DADMM_GRAM_G2ALL && MG == 1 && units <= 4) {
+    if (MG == 1 && units <= 4) {
         // (round 5) every unit's A^T rows (and mode 2's out rows) loaded at once: one memory wait
         // for the wave's whole GEMM2 instead of one per unit; the chains are the loop's below
         f32x4 at_all[4][4], oall[4];
@@ -435,7 +335,7 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
     // mode 2 (out += ...): the out rows of the unit that completes a tile are loaded one unit
     // ahead (a load issued just before its add left the HBM latency exposed once per tile)
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        out, 0, (mode == 2 && DADMM_GRAM_OPF) ? (int)((size_t)B * P * n * 4) : 0, 0x00020000);
+        out, 0, (mode == 2) ? (int)((size_t)B * P * n * 4) : 0, 0x00020000);
     auto ldo = [&](int u) -> f32x4 {
         const int nb = w + WAVES * (u / MG), mg = u % MG, n0 = 16 * nb + 4 * h;
         const uint32_t off = (mg == MG - 1 && sv && n0 < n) ? (uint32_t)((((size_t)s * P + p) * n + n0) * 4)
@@ -443,11 +343,11 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
         return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ro, off, 0, 0));
     };
     f32x4 ocur = {0.0f, 0.0f, 0.0f, 0.0f}, onxt = ocur;
-    if (DADMM_GRAM_OPF && mode == 2 && units > 0) ocur = ldo(0);
+    if (mode == 2 && units > 0) ocur = ldo(0);
     for (int u = 0; u < units; ++u) {
         const int nb = w + WAVES * (u / MG), mg = u % MG;
         if (u + 1 < units) load_at(at_nxt, u + 1);
-        if (DADMM_GRAM_OPF && mode == 2 && u + 1 < units) onxt = ldo(u + 1);
+        if (mode == 2 && u + 1 < units) onxt = ldo(u + 1);
         if (mg == 0) {
             gc = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -470,7 +370,7 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
         const int n0 = 16 * nb + 4 * h;
         if (mg == MG - 1 && sv && n0 < n) {
             f32x4* o = (f32x4*)(out + ((size_t)s * P + p) * n + n0);
-            f32x4 v = mode == 2 ? (DADMM_GRAM_OPF ? ocur : *o) + gc : gc;
+            f32x4 v = mode == 2 ? ocur + gc : gc;
             if (mode == 2 && a.acc_add != nullptr) v = v + *(const f32x4*)(a.acc_add + ((size_t)s * P + p) * n + n0);
             *o = v;
         }
@@ -480,127 +380,18 @@ __global__ __launch_bounds__(THREADS) void gram_kernel(GnnArgs a, int k, const f
     }
 }
 
-// ---- gram, one wave per item (DADMM_GRAM_W1): the same chains as gram_kernel with the whole item
-// in one wave. GEMM1 keeps every m-block's accumulator (MQ of them) in registers, so each x
-// column block is loaded once per item (gram_kernel's four waves each load all of x for their own
-// m-block) and no R tile goes through LDS: the MFMA accumulator layout (rows 4 h + r of m-block g,
-// sample j) is exactly GEMM2's B-operand layout. No LDS, no barriers: four independent items per
-// 256-thread workgroup. Chains and their order are gram_kernel's (bit-identical).
-template <int MQ>
-__global__ __launch_bounds__(THREADS) void gram_w1_kernel(GnnArgs a, int k, const float* x_raw, float* out,
-                                                          int mode) {
-    const int P = a.P, n = a.n, m = a.m, B = a.B, NP = a.n_pad, MP = a.m_pad;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int item = blockIdx.x * WAVES + w;
-    const int tiles = (B + BT - 1) / BT;
-    if (item >= tiles * P) return;                 // whole waves only; no barrier below
-    const int tile = item / P, p = item % P;
-    const int j = lane & 15, h = lane >> 4;
-    const int s = tile * BT + j;
-    const bool sv = s < B;
-    const int mbk = (m + 15) / 16;                 // m-blocks holding rows (<= MQ)
-    f32x4 R[MQ];
-#pragma unroll
-    for (int g = 0; g < MQ; ++g) R[g] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-    if (mode != 1) {
-        bool zero = false;
-        const float* xs = x_raw != nullptr ? x_raw : y_source(a, k, zero);
-        const uint32_t xbytes = zero ? 0u : (uint32_t)((size_t)B * P * n * 4);
-        const __amdgpu_buffer_rsrc_t rx =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), 0, (int)xbytes, 0x00020000);
-        const uint32_t xoff = sv ? (uint32_t)((((size_t)s * P + p) * n + 4 * h) * 4) : 0x80000000u;
-        auto ldx = [&](int t) -> f32x4 {
-            return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                rx, 16 * t + 4 * h < n && sv ? xoff + 64u * t : 0x80000000u, 0, 0));
-        };
-        const float* arow = a.A + ((size_t)p * MP + j) * NP + 4 * h;   // + 16 g NP (m-block g)
-        constexpr int GD = MQ <= 2 ? 4 : 2;        // k-steps in flight (register budget)
-        const int T = NP / 16;
-        f32x4 ar[GD][MQ], xr[GD];
-        auto lda = [&](f32x4 (&dst)[MQ], int t) {
-#pragma unroll
-            for (int g = 0; g < MQ; ++g)
-                if (g < mbk) dst[g] = *(const f32x4*)(arow + (size_t)16 * g * NP + 16 * t);
-        };
-#pragma unroll
-        for (int u = 0; u < GD; ++u) {
-            if (u < T) {
-                lda(ar[u], u);
-                xr[u] = ldx(u);
-            }
-        }
-        for (int t0 = 0; t0 < T; t0 += GD) {
-#pragma unroll
-            for (int u = 0; u < GD; ++u) {
-                const int t = t0 + u;
-                if (t < T) {
-#pragma unroll
-                    for (int g = 0; g < MQ; ++g)
-                        if (g < mbk) {
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) R[g] = mfma4(ar[u][g][r], xr[u][r], R[g]);
-                        }
-                    if (t + GD < T) {
-                        lda(ar[u], t + GD);
-                        xr[u] = ldx(t + GD);
-                    }
-                }
-            }
-        }
-    } else {
-#pragma unroll
-        for (int g = 0; g < MQ; ++g)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int mi = 16 * g + 4 * h + r;
-                R[g][r] = (sv && mi < m) ? a.b[((size_t)s * P + p) * m + mi] : 0.0f;
-            }
-    }
-    // GEMM2: out = A_p^T R over the n-tiles, one chain per tile over the m-blocks ascending; the A^T
-    // rows of tile nb + 1 load under tile nb's MFMAs
-    const float* atb = a.At + ((size_t)p * NP + j) * MP + 4 * h;
-    const int NT16 = NP / 16;
-    f32x4 at[2][MQ];
-    auto ldt = [&](f32x4 (&dst)[MQ], int nb) {
-#pragma unroll
-        for (int g = 0; g < MQ; ++g)
-            if (g < mbk) dst[g] = *(const f32x4*)(atb + (size_t)16 * nb * MP + 16 * g);
-    };
-    ldt(at[0], 0);
-    for (int nb = 0; nb < NT16; ++nb) {
-        if (nb + 1 < NT16) ldt(at[(nb + 1) & 1], nb + 1);
-        f32x4 gc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int g = 0; g < MQ; ++g)
-            if (g < mbk) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) gc = mfma4(at[nb & 1][g][r], R[g][r], gc);
-            }
-        const int n0 = 16 * nb + 4 * h;
-        if (sv && n0 < n) {
-            f32x4* o = (f32x4*)(out + ((size_t)s * P + p) * n + n0);
-            f32x4 v = mode == 2 ? *o + gc : gc;
-            if (mode == 2 && a.acc_add != nullptr) v = v + *(const f32x4*)(a.acc_add + ((size_t)s * P + p) * n + n0);
-            *o = v;
-        }
-    }
-}
-
 // ---- gram with the agent's operator resident in LDS (round 4, the default where it fits) ---------
 // gram_kernel re-reads A_p and A_p^T from L2 for every (16-sample tile, agent) item and runs one
 // dependent MFMA chain per wave (PMC at configs[2]: MFMA busy 0.25, waves half the time stalled on
 // issue). Here a workgroup owns ONE agent and a run of tiles: A_p's rows (16 MQ x n_pad) are copied
 // into LDS once (row stride n_pad + 4 floats: the GEMM2 fragment gathers, rows 4 h + r apart, land
-// in 64 distinct banks) and every wave runs whole items as gram_w1_kernel does — GEMM1 with the MQ
+// in 64 distinct banks) and every wave runs whole items — GEMM1 with the MQ
 // m-block chains interleaved and R kept in registers (the accumulator layout is GEMM2's B operand),
 // GEMM2 with two n-tiles' chains interleaved — reading both operand fragments from LDS; only the x
 // and out streams touch HBM (x through a GX-deep register ring, mode 2's out rows two n-tile pairs
 // ahead). 16 waves (four per SIMD) hide the stream latency. Chains and their order are
 // gram_kernel's: GEMM1 from +0 over the columns in 16-blocks (0,4,8,12,1,... inside), GEMM2 from +0
 // over the m-blocks ascending — bit-identical output.
-#ifndef DADMM_GRAM_LDS
-#define DADMM_GRAM_LDS 1
-#endif
 constexpr int GL_WAVES = 16;
 __host__ __device__ constexpr size_t gram_lds_bytes(int mq, int n_pad) { return 4 * (size_t)16 * mq * (n_pad + 4); }
 
@@ -746,37 +537,23 @@ __global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int 
 constexpr int UP_CH = 4;
 // columns per item: 128 (a wave instruction covers 2 agent rows) or 64 (4 rows; half the LDS per
 // workgroup, so more workgroups fit per CU at large P)
-#ifndef DADMM_STEP_UCB
-#define DADMM_STEP_UCB 128
-#endif
-constexpr int UCB = DADMM_STEP_UCB;
+constexpr int UCB = 128;
 constexpr int RPI = 256 / UCB;    // agent rows per wave instruction (UCB / 4 lanes per row)
 static_assert(UCB == 64 || UCB == 128, "UCB");
-// DADMM_STEP_KEEPU=1: the step keeps phase 1's U rows in registers for phase 2 (one fewer HBM
-// stream) — 97 instead of 82 VGPRs, four instead of five waves per SIMD: 86.1-86.4 vs 84.7-85.0 ms
-// at the configs[4] shard forward (profiles/r04/variants_r04o_step_keepu.txt), so off
-#ifndef DADMM_STEP_NOBR
-#define DADMM_STEP_NOBR 1       // fused step pass: unconditional loads, results selected after
-#endif
-#ifndef DADMM_STEP_UPCH
-#define DADMM_STEP_UPCH 2       // row pairs in flight per wave in the fused step pass
-#endif
-#ifndef DADMM_STEP_KEEPU
-#define DADMM_STEP_KEEPU 0
-#endif
+// Keeping phase 1's U rows in registers for phase 2 (one fewer HBM stream) was measured and
+// dropped: 97 instead of 82 VGPRs, four instead of five waves per SIMD, 86.1-86.4 vs 84.7-85.0 ms
+// at the configs[4] shard forward (profiles/r04/variants_r04o_step_keepu.txt)
 // LDS bytes for one sample's visit lists: at most 2 P entries per agent (each incident edge is
 // visited from both of its ends; a self-loop twice), one byte each
 __host__ __device__ constexpr int update_visit_words(int P) { return (2 * P * P + 3) / 4; }
 __host__ __device__ constexpr size_t update_lds_bytes(int P) {
     return 4 * ((size_t)P * UCB + (size_t)(P + 1) + update_visit_words(P));
 }
-// KEEPU (fused pass, P <= 64): phase 1's U rows stay in registers for the dual update of phase 2
-// instead of being read from HBM a second time (one of the pass's nine 4-byte streams per element)
-template <bool FUSED, bool KEEPU = false>
+template <bool FUSED>
 __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, float* lds) {
     // row pairs in flight per wave: the fused pass streams 5 state tensors, so fewer pairs keep
     // its registers at 4+ waves per SIMD
-    constexpr int UP_CH = FUSED ? DADMM_STEP_UPCH : gnn::UP_CH;
+    constexpr int UP_CH = FUSED ? 2 : gnn::UP_CH;
     const int P = a.P, n = a.n;
     const int ncb = (n + UCB - 1) / UCB;
     const int s = item / ncb;
@@ -788,22 +565,14 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     const size_t base = (size_t)s * P * n + (cv ? c : 0);
     bool yzero = false;
     // the guard words and the table entry y_k comes from in the common case, issued together
-    // (DADMM_STEP_EARLY; y_source's walk only when the k - 1 guard fired): one round trip before
+    // (y_source's walk only when the k - 1 guard fired): one round trip before
     // the visit lists instead of the walk's flag -> table -> flag chain
-#if DADMM_STEP_EARLY
     const int f_prev = k > 0 ? __builtin_amdgcn_readfirstlane(flag_ld(a.flags + GNN_F_YNB(k - 1))) : 0;
     const int f_u = __builtin_amdgcn_readfirstlane(flag_ld(a.flags + GNN_F_UBAD(k)));
     float* const y_prev = a.yptr[k];
     const float* __restrict__ ys = (k > 0 && f_prev == 0) ? y_prev : y_source(a, k, yzero);
     const bool uzero = f_u != 0;
     float* const fix = (FUSED && k > 0 && f_prev != 0) ? y_prev : nullptr;
-#else
-    const float* __restrict__ ys = y_source(a, k, yzero);
-    const bool uzero = flag_ld(a.flags + GNN_F_UBAD(k)) != 0;
-    // the y_next guard of iteration k - 1 fired: Y[k-1] (= yptr[k], which holds the rejected
-    // y_next) is rewritten with y_k
-    float* const fix = (FUSED && k > 0 && flag_ld(a.flags + GNN_F_YNB(k - 1)) != 0) ? a.yptr[k] : nullptr;
-#endif
     float gclip, vclip;
     clips(a, k, gclip, vclip);
     float* yl = lds;                                  // [P][UCB] y_{k+1}
@@ -818,12 +587,10 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
     // row groups (RPI rows): wave w handles groups w, w + 4, ...; `half` selects the lane's row
     bool bad_y = false, bad_g = false;
-    constexpr int UMAX = KEEPU ? 4 : 1;               // 2 * WAVES * UP_CH * UMAX = 64 rows
-    f32x4 ukeep[UMAX][UP_CH];
-    auto phase1 = [&](int q0, int it) {
+    auto phase1 = [&](int q0) {
         f32x4 gv[UP_CH], yv[UP_CH];
         float alv[UP_CH];
-        if constexpr (FUSED && DADMM_STEP_NOBR) {
+        if constexpr (FUSED) {
             // every load unconditional (rows past P read agent P - 1, columns past n column 0 —
             // both valid addresses), the results selected afterwards: no load sits under a branch,
             // so the pass's loads stay in flight together instead of draining at each merge
@@ -857,7 +624,6 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
                     uv[u][r] = (ok && !uzero) ? uv[u][r] : 0.0f;
                     dv[u][r] = ok ? dv[u][r] : 0.0f;
                 }
-                if constexpr (KEEPU) ukeep[it][u] = uv[u];
                 const int p = RPI * (q0 + WAVES * u) + half;
                 if (ok && fix != nullptr) *(f32x4*)(fix + base + (size_t)p * n) = yv[u];
 #pragma unroll
@@ -869,42 +635,6 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
                     g = clamp_t(g, -gclip, gclip);
                     bad_g |= ok && g != g;                  // after the clamp only NaN (:216)
                     gv[u][r] = ok ? g : 0.0f;
-                }
-            }
-        } else if constexpr (FUSED) {
-            f32x4 tv[UP_CH], bv[UP_CH], uv[UP_CH], dv[UP_CH];
-#pragma unroll
-            for (int u = 0; u < UP_CH; ++u) {
-                const int p = RPI * (q0 + WAVES * u) + half;
-                tv[u] = bv[u] = uv[u] = dv[u] = yv[u] = z4;
-                if (p < P && cv) {
-                    const size_t off = base + (size_t)p * n;
-                    tv[u] = *(const f32x4*)(a.AtAy + off);
-                    bv[u] = *(const f32x4*)(a.Atb + off);
-                    if (!yzero) yv[u] = *(const f32x4*)(ys + off);
-                    if (!uzero) uv[u] = *(const f32x4*)(U + off);
-                    dv[u] = *(const f32x4*)(a.D + off);
-                }
-                if constexpr (KEEPU) ukeep[it][u] = uv[u];
-            }
-#pragma unroll
-            for (int u = 0; u < UP_CH; ++u) {
-                const int p = RPI * (q0 + WAVES * u) + half;
-                gv[u] = z4;
-                if (p < P && cv) {
-                    const float ta = hyp_at(a, s, 1, p), rh = hyp_at(a, s, 2, p);
-                    const float dg = a.deg[(a.graph_shared ? 0 : (size_t)s * P) + p];
-                    if (fix != nullptr) *(f32x4*)(fix + base + (size_t)p * n) = yv[u];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float g = tv[u][r] - bv[u][r];
-                        g = g + sign_times(yv[u][r], ta);   // sign(y) * tau
-                        g = g + uv[u][r] * dg;
-                        g = g + dv[u][r] * rh;
-                        g = clamp_t(g, -gclip, gclip);
-                        bad_g |= g != g;                    // after the clamp only NaN (:216)
-                        gv[u][r] = g;
-                    }
                 }
             }
         } else {   // resolve: the batch's gradient is zero (:216-218)
@@ -921,7 +651,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
             if (p < P) {
                 f32x4 v = z4;
                 if (cv) {
-                    const float al = (FUSED && DADMM_STEP_NOBR) ? alv[u] : hyp_at(a, s, 0, p);
+                    const float al = FUSED ? alv[u] : hyp_at(a, s, 0, p);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         v[r] = clamp_t(yv[u][r] - al * gv[u][r], -vclip, vclip);   // :221-225
@@ -933,24 +663,16 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
             }
         }
     };
-    if constexpr (KEEPU) {
-#pragma unroll
-        for (int it = 0; it < UMAX; ++it)
-            if (RPI * (w + it * WAVES * UP_CH) < P) phase1(w + it * WAVES * UP_CH, it);
-    } else {
-        for (int q0 = w; RPI * q0 < P; q0 += WAVES * UP_CH) phase1(q0, 0);
-    }
+    for (int q0 = w; RPI * q0 < P; q0 += WAVES * UP_CH) phase1(q0);
     __syncthreads();
     bool bad_u = false;
-    auto phase2 = [&](int q0, int it) {
+    auto phase2 = [&](int q0) {
         f32x4 uv[UP_CH];
         float etv[UP_CH];
 #pragma unroll
         for (int u = 0; u < UP_CH; ++u) {
             const int p = RPI * (q0 + WAVES * u) + half;
-            if constexpr (KEEPU) {
-                uv[u] = ukeep[it][u];
-            } else if constexpr (FUSED && DADMM_STEP_NOBR) {
+            if constexpr (FUSED) {
                 // unconditional (agent clamped), selected after, as in phase 1
                 const int pc = p < P ? p : P - 1;
                 const f32x4 t = *(const f32x4*)(U + base + (size_t)pc * n);
@@ -975,7 +697,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
                 const f32x4 yq = *(const f32x4*)(yl + (int)vl[t] * UCB + cl);
                 acc = acc + (yp - yq);
             }
-            const float et = (FUSED && DADMM_STEP_NOBR && !KEEPU) ? etv[u] : hyp_at(a, s, 3, p);
+            const float et = FUSED ? etv[u] : hyp_at(a, s, 3, p);
             f32x4 un;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -988,13 +710,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
             *(f32x4*)(a.D_next + off) = acc;
         }
     };
-    if constexpr (KEEPU) {
-#pragma unroll
-        for (int it = 0; it < UMAX; ++it)
-            if (RPI * (w + it * WAVES * UP_CH) < P) phase2(w + it * WAVES * UP_CH, it);
-    } else {
-        for (int q0 = w; RPI * q0 < P; q0 += WAVES * UP_CH) phase2(q0, 0);
-    }
+    for (int q0 = w; RPI * q0 < P; q0 += WAVES * UP_CH) phase2(q0);
     if (FUSED) {
         flag_or(a.flags + GNN_F_GBAD(k), bad_g);
         flag_or(a.flags + GNN_F_YNB_OPT(k), bad_y);
@@ -1008,10 +724,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
 // the fused pass: one workgroup per item
 __global__ __launch_bounds__(THREADS) void step_kernel(GnnArgs a, int k) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    if (DADMM_STEP_KEEPU && a.P <= RPI * WAVES * DADMM_STEP_UPCH * 4)
-        update_item<true, true>(a, k, blockIdx.x, lds);
-    else
-        update_item<true>(a, k, blockIdx.x, lds);
+    update_item<true>(a, k, blockIdx.x, lds);
 }
 
 // the resolve: a short grid (every workgroup reads one flag word); the g = 0 update, if needed,
@@ -1090,12 +803,8 @@ __global__ __launch_bounds__(THREADS) void step_backward_kernel(GnnArgs a, int k
     }
     __builtin_amdgcn_wave_barrier();
     auto accum = [&](int c, int p, float v) {   // wave-sum v into red[c][p or 0]
-        if constexpr (DADMM_SBW_DPP) {
-            v = wave_sum_dpp(v);
-        } else {
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-        }
+        v = wave_sum_dpp(v);
+    
         if (lane == 0) red[c * H + (H == 1 ? 0 : p)] += v;
     };
     // (round 4) no-alias views of the streams, so that the unrolled agent loops below can put
@@ -1327,13 +1036,13 @@ hipError_t gnn_launch_check0(const GnnArgs& a, const float* y0, hipStream_t st) 
     return hipGetLastError();
 }
 
-size_t gnn_gram_lds(int m_pad) { return 4 * (size_t)(BT * (m_pad + 4) + (DADMM_GRAM_XLDS ? 2 * BT * 64 : 0)); }
+size_t gnn_gram_lds(int m_pad) { return 4 * (size_t)(BT * (m_pad + 4) + 0); }
 
 hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* out, int mode,
                            hipStream_t st) {
     const int mbk = (a.m + 15) / 16;
     const int mq = mbk;
-    if (DADMM_GRAM_LDS && mode != 1 && mbk >= 1 && mbk <= 4 && gnn::gram_lds_bytes(mq, a.n_pad) <= 160 * 1024) {
+    if (mode != 1 && mbk >= 1 && mbk <= 4 && gnn::gram_lds_bytes(mq, a.n_pad) <= 160 * 1024) {
         // workgroups = P x S splits of the tiles; S minimises (rounds of workgroups over the CUs) x
         // (tiles each wave runs), preferring fewer workgroups on a tie
         // the current device's CU count, queried per call (the runtime caches the attribute; a
@@ -1375,13 +1084,6 @@ hipError_t gnn_launch_gram(const GnnArgs& a, int k, const float* x_raw, float* o
         return hipGetLastError();
     }
 item_kernel:
-    if (DADMM_GRAM_W1 && mbk <= 8) {
-        const int items = ((a.B + BT - 1) / BT) * a.P;
-        const int grid = (items + gnn::WAVES - 1) / gnn::WAVES;
-        auto kern = mbk <= 2 ? gnn::gram_w1_kernel<2> : mbk <= 4 ? gnn::gram_w1_kernel<4> : gnn::gram_w1_kernel<8>;
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(gnn::THREADS), 0, st, a, k, x_raw, out, mode);
-        return hipGetLastError();
-    }
     const size_t lds = gnn_gram_lds(a.m_pad);
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)gnn::gram_kernel<false>,
@@ -1389,7 +1091,7 @@ item_kernel:
         if (e != hipSuccess) return e;
     }
     const int items = ((a.B + BT - 1) / BT) * a.P;
-    if (DADMM_GRAM_SMALL && mode != 1 && a.m == 64 && a.m_pad == 64 && a.n_pad == 256 && items <= 512) {
+    if (mode != 1 && a.m == 64 && a.m_pad == 64 && a.n_pad == 256 && items <= 512) {
         hipLaunchKernelGGL(gnn::gram_kernel<true>, dim3(items), dim3(gnn::THREADS), lds, st, a, k, x_raw, out,
                            mode);
         return hipGetLastError();

@@ -44,17 +44,6 @@ constexpr int ZS = TN + 4;        // LDS row stride of the GCN epilogue tile (fl
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
-// Ablation knobs (timing builds only, never shipped): operand loads replaced by register values
-#ifdef HYPER_ABL_A_CONST
-#define HYPER_ABL_A(v) ((f32x4){(float)t, 0.5f, 0.25f, 0.125f})
-#else
-#define HYPER_ABL_A(v) (v)
-#endif
-#ifdef HYPER_ABL_W_CONST
-#define HYPER_ABL_W(v) ((f32x4){(float)u, 0.5f, 0.25f, 0.125f})
-#else
-#define HYPER_ABL_W(v) (v)
-#endif
 // scheduling barrier: pins where the ring's loads issue (between the steps' MFMAs)
 __device__ __forceinline__ void mem_fence() { __builtin_amdgcn_sched_barrier(0); }
 
@@ -62,18 +51,9 @@ __device__ __forceinline__ void mem_fence() { __builtin_amdgcn_sched_barrier(0);
 // -> LDS once (LDS-DMA, lane-linear 1 KB fragment images, DQ k-steps in flight) and every wave
 // reads its MFMA fragments from there; DMA = 0: each wave streams its own fragments into a
 // register ring (the two waves that share a row block, or a column block, both fetch it).
-#ifndef DADMM_HYPER_DMA
-#define DADMM_HYPER_DMA 1       // 0: never the DMA ring (A/B builds)
-#endif
-#ifndef DADMM_HYPER_DMA_MIN
-#define DADMM_HYPER_DMA_MIN 32  // k-steps per workgroup from which the DMA ring is used
-#endif
-#ifndef DADMM_HYPER_DQ
-#define DADMM_HYPER_DQ 4
-#endif
-#ifndef DADMM_HYPER_D1
-#define DADMM_HYPER_D1 4
-#endif
+constexpr int HYPER_DMA_MIN = 32;  // k-steps per workgroup from which the DMA ring is used
+constexpr int HYPER_DQ = 4;
+constexpr int HYPER_D1 = 4;
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, size_t bytes) {
@@ -131,9 +111,9 @@ template <int WR, int EPI, bool SPLIT, bool DMA, int KS>
 __global__ __launch_bounds__(THREADS * KS) void linear_kernel(HyperArgs a) {
     static_assert(KS == 1 || (KS == 2 && !DMA), "the K split runs on the register ring");
     constexpr int NT = THREADS * KS;               // threads per workgroup
-    // register ring depth (k-steps in flight; 2 waves/SIMD); DADMM_HYPER_D1: the depth of the
+    // register ring depth (k-steps in flight; 2 waves/SIMD); HYPER_D1: the depth of the
     // one-row-block tiles (small batches: one workgroup per CU, latency-bound K loops)
-    [[maybe_unused]] constexpr int D = WR >= 5 ? 3 : (WR == 1 ? DADMM_HYPER_D1 : 4);
+    [[maybe_unused]] constexpr int D = WR >= 5 ? 3 : (WR == 1 ? HYPER_D1 : 4);
     constexpr int TM = 32 * WR;                    // rows per workgroup tile
     extern __shared__ __attribute__((aligned(16))) float zt[];   // GCN epilogue (dynamic)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -207,9 +187,9 @@ __global__ __launch_bounds__(THREADS * KS) void linear_kernel(HyperArgs a) {
         f32x4 ar[D][WR], br[D][2];
         auto load = [&](int u, int t) {
 #pragma unroll
-            for (int i = 0; i < WR; ++i) ar[u][i] = HYPER_ABL_A(*(const f32x4*)(x + o[i] + (16 * t - koff)));
+            for (int i = 0; i < WR; ++i) ar[u][i] = *(const f32x4*)(x + o[i] + (16 * t - koff));
 #pragma unroll
-            for (int c = 0; c < 2; ++c) br[u][c] = HYPER_ABL_W(*(const f32x4*)(a.W + ow[c] + 16 * t));
+            for (int c = 0; c < 2; ++c) br[u][c] = *(const f32x4*)(a.W + ow[c] + 16 * t);
         };
         if (te - tb < D) {   // short segment: no ring
             for (int t = tb; t < te; ++t) {
@@ -257,7 +237,7 @@ __global__ __launch_bounds__(THREADS * KS) void linear_kernel(HyperArgs a) {
     [[maybe_unused]] float* pf = nullptr;
     [[maybe_unused]] const int SR = (a.S_t + 3) & ~3;
     if constexpr (EPI == HYPER_EPI_GCN_BWD) {
-        constexpr int RING = DMA ? DADMM_HYPER_DQ * (2 * WR + 4) * 256 : 0;   // floats
+        constexpr int RING = DMA ? HYPER_DQ * (2 * WR + 4) * 256 : 0;   // floats
         const int epi = TM * ZS + ((a.S_t * a.P * a.P + 3) & ~3) + 4 * TN;
         pf = zt + (RING > epi ? RING : epi);
         float* pst = pf + TM * TN;                                   // mean [SR][64], var [SR][64]
@@ -277,7 +257,7 @@ __global__ __launch_bounds__(THREADS * KS) void linear_kernel(HyperArgs a) {
     if constexpr (DMA) {
         // ring slot: the tile's NBA row blocks, then its 4 column blocks (16 x 16 floats each, as
         // lane-linear fragment images: lane (j, h) of block q holds row/column 16 q + j, k 4h..4h+3)
-        constexpr int DQ = DADMM_HYPER_DQ;
+        constexpr int DQ = HYPER_DQ;
         constexpr int NBA = 2 * WR, NB = NBA + 4, NBW = (NB + 3) / 4, SLOT = NB * 256;
         const int wu = __builtin_amdgcn_readfirstlane(w) & 3;   // provably uniform, in [0, 4)
         const int nbw = NB % 4 == 0 ? NB / 4 : (NB - wu + 3) / 4;   // blocks this wave copies per k-step
@@ -713,21 +693,9 @@ __global__ __launch_bounds__(THREADS * KS) void linear_kernel(HyperArgs a) {
 // (buffer range checks), so the loop is branch-free. The epilogue is linear_kernel's inference
 // GCN epilogue (mix with A_hat, the optional addend, bias, leaky_relu, BatchNorm) on the 256-row
 // Z tile.
-#ifndef DADMM_G32_DQ
-#define DADMM_G32_DQ 4          // LDS-DMA ring stages in flight (timing builds: 3, 5, 6)
-#endif
-constexpr int G32_TM = 256, G32_WAVES = 8, G32_DQ = DADMM_G32_DQ;
+constexpr int G32_TM = 256, G32_WAVES = 8, G32_DQ = 4;
 constexpr int G32_STAGE = (G32_TM + TN) * 16;                  // floats per ring stage
-#ifndef DADMM_G32_AHAT_LDS
-#define DADMM_G32_AHAT_LDS 0
-#endif
-#ifndef DADMM_G32_MIX_PF
-#define DADMM_G32_MIX_PF 1
-#endif
-#ifndef DADMM_G32_ABL_MIX
-#define DADMM_G32_ABL_MIX 0     // timing builds only: the mix reduced to one node (wrong results)
-#endif
-// DADMM_G32_MFMA_MIX=1: the per-sample mix sum_q A_hat[p][q] Z[q] runs on v_mfma_f32_16x16x4_f32
+// Measured and dropped: the per-sample mix sum_q A_hat[p][q] Z[q] on v_mfma_f32_16x16x4_f32
 // instead of VALU fma: output blocks of 16 rows x 16 columns, each summing over the node range of
 // the samples its rows belong to (A_hat entries of other samples are zero: a block-diagonal
 // operand, ~1.3 samples' width per block), Z from LDS (row stride ZM = 80 floats: the four k rows
@@ -735,14 +703,9 @@ constexpr int G32_STAGE = (G32_TM + TN) * 16;                  // floats per rin
 // VALU mix (an f32 MFMA is an fma chain in k order, and the zero entries leave it unchanged), but
 // slower: 91.9-92.0 vs 84.1-84.2 ms at the configs[4] shard forward (per-lane A_hat gathers and
 // one dependent chain per block; profiles/r04/variants_r04q_mfma_mix.txt), so off
-#ifndef DADMM_G32_MFMA_MIX
-#define DADMM_G32_MFMA_MIX 0
-#endif
-constexpr int ZM = 80;
 __host__ __device__ constexpr size_t g32_lds_bytes(int S_t, int P) {
     const size_t ring = 4 * (size_t)G32_DQ * G32_STAGE;
-    const size_t epi = DADMM_G32_MFMA_MIX ? 4 * (size_t)G32_TM * ZM
-        : 4 * ((size_t)G32_TM * ZS + (DADMM_G32_AHAT_LDS ? (((size_t)S_t * P * P + 3) & ~(size_t)3) : 0) + 4 * TN);
+    const size_t epi = 4 * ((size_t)G32_TM * ZS + 4 * TN);
     return ring > epi ? ring : epi;
 }
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -848,73 +811,6 @@ __global__ __launch_bounds__(64 * G32_WAVES) void gcn32_kernel(HyperArgs a) {
         }
         lds_barrier();   // the ring's last reads before the epilogue reuses the LDS
     }
-#if DADMM_G32_MFMA_MIX
-    {
-        // Z tile [256][ZM]: acc[rb] register e = row (e & 3) + 8 (e >> 2) + 4 kh of row block rb, column fi
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-            for (int e = 0; e < 16; ++e)
-                zt[(64 * wr + 32 * rb + (e & 3) + 8 * (e >> 2) + 4 * kh) * ZM + 32 * wc + fi] = acc[rb][e];
-        __syncthreads();
-        const int j = lane & 15, h = lane >> 4;
-        const int cols = a.N - col0 < TN ? a.N - col0 : TN;
-        const float* ahb = a.ahat + (a.ahat_per_sample ? (size_t)s0 * P * P : 0);
-        const int ahs = a.ahat_per_sample ? P * P : 0;
-        // 16 row blocks x 4 column blocks; wave w takes blocks w, w + 8, ...
-        for (int blk = w; blk < 64; blk += G32_WAVES) {
-            const int rb = blk >> 2, cb = blk & 3;
-            const int R0 = 16 * rb;
-            if (R0 >= rows_t || 16 * cb >= cols) continue;   // wave-uniform
-            const int slo = R0 / P, shi = min((R0 + 15) / P, ns - 1);
-            const int q0 = slo * P, q1 = (shi + 1) * P;        // the block's node range
-            // this lane's A row (tile row R0 + j) and its sample's node range
-            const int r = R0 + j;
-            const int sr = min(r / P, ns - 1);
-            const int qa = sr * P, qb = qa + P;
-            const bool rv = r < rows_t;
-            const float* arow = ahb + (size_t)sr * ahs + (size_t)(r - qa) * P - qa;   // arow[q] = A_hat[r][q - qa]
-            const int zc = 16 * cb + j;
-            f32x4 m = {0.0f, 0.0f, 0.0f, 0.0f};
-            for (int qt = q0; qt < q1; qt += 16) {             // four k-steps per trip (wave-uniform)
-                float av[4], bv[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int qq = qt + 4 * u + h;                 // k-step u's slot h
-                    av[u] = (rv && qq >= qa && qq < qb) ? arow[qq] : 0.0f;
-                    bv[u] = qq < q1 ? zt[qq * ZM + zc] : 0.0f;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) m = mfma4(av[u], bv[u], m);
-            }
-            // lane (j, h) holds rows R0 + 4 h + e of column col0 + 16 cb + j
-            const int col = col0 + zc;
-            if (col < a.N) {
-                float bias = 0.0f, bmean = 0.0f, bsc = 1.0f, bsh = 0.0f;
-                if (!a.raw) {
-                    bias = a.bias[col];
-                    bmean = a.bn_mean[col];
-                    bsc = (1.0f / sqrtf(a.bn_var[col] + a.bn_eps)) * a.bn_w[col];
-                    bsh = a.bn_b[col];
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int rr = R0 + 4 * h + e;
-                    if (rr >= rows_t) continue;
-                    float t = m[e];
-                    if (a.addend != nullptr) t = t + a.addend[(size_t)(row0 + rr) * a.ld_add + col];
-                    if (!a.raw) {
-                        t = t + bias;
-                        t = t > 0.0f ? t : t * a.slope;
-                        t = (t - bmean) * bsc + bsh;
-                    }
-                    a.y[(size_t)(row0 + rr) * a.ldy + col] = t;
-                }
-            }
-        }
-        return;
-    }
-#endif
     // Z tile: acc[rb] register e = row (e & 3) + 8 (e >> 2) + 4 kh of row block rb, column fi
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
@@ -922,25 +818,12 @@ __global__ __launch_bounds__(64 * G32_WAVES) void gcn32_kernel(HyperArgs a) {
         for (int e = 0; e < 16; ++e)
             zt[(64 * wr + 32 * rb + (e & 3) + 8 * (e >> 2) + 4 * kh) * ZS + 32 * wc + fi] = acc[rb][e];
     const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
-#if DADMM_G32_AHAT_LDS
-    float* ahs = zt + G32_TM * ZS;                       // [S_t][P][P]
-    float* colp = ahs + ((a.S_t * P * P + 3) & ~3);
-    const float* agl = a.ahat + (a.ahat_per_sample ? (size_t)s0 * P * P : 0);
-    if (a.ahat_per_sample) {
-        for (int i = threadIdx.x; i < ns * P * P; i += 64 * G32_WAVES) ahs[i] = agl[i];
-    } else {
-        for (int i = threadIdx.x; i < P * P; i += 64 * G32_WAVES)
-            for (int sl = 0; sl < ns; ++sl) ahs[sl * P * P + i] = agl[i];
-    }
-    const int ahs_stride = P * P;
-#else
     // A_hat read through the vector cache (the 16 lanes of a column quad group share each word):
     // the LDS then holds only the ring / Z tile, so two workgroups fit on a CU and one's epilogue
     // runs beside the other's MFMA loop
     const float* ahs = a.ahat + (a.ahat_per_sample ? (size_t)s0 * P * P : 0);
     const int ahs_stride = a.ahat_per_sample ? P * P : 0;
     float* colp = zt + G32_TM * ZS;
-#endif
     if (threadIdx.x < TN && !a.raw) {
         const int col = col0 + threadIdx.x < a.N ? col0 + threadIdx.x : a.N - 1;
         const float sc = (1.0f / sqrtf(a.bn_var[col] + a.bn_eps)) * a.bn_w[col];
@@ -963,11 +846,10 @@ __global__ __launch_bounds__(64 * G32_WAVES) void gcn32_kernel(HyperArgs a) {
         const float* zc = zt + sl * P * ZS + c;
         f32x4 v[4] = {zero, zero, zero, zero};
         int q = 0;
-#if DADMM_G32_MIX_PF
         // A_hat words four nodes at a time, the next four in flight under this group's fma (the
         // loads go through the vector cache: one dependent round trip per group without it)
         typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
-        const int P4 = DADMM_G32_ABL_MIX ? 0 : (P & ~3);
+        const int P4 = P & ~3;
         if (P4 > 0) {
             f32x4 an[4];
 #pragma unroll
@@ -988,8 +870,7 @@ __global__ __launch_bounds__(64 * G32_WAVES) void gcn32_kernel(HyperArgs a) {
                 }
             }
         }
-#endif
-        for (; q < (DADMM_G32_ABL_MIX ? 1 : P); ++q) {
+        for (; q < P; ++q) {
             const f32x4 z = *(const f32x4*)(zc + q * ZS);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = __builtin_elementwise_fma((f32x4)(at[e][q]), z, v[e]);
@@ -1096,7 +977,7 @@ __global__ __launch_bounds__(THREADS) void rownorm_kernel(RowNormArgs a) {
 
 template <int WR, int EPI, bool SPLIT, bool DMA, int KS = 1>
 hipError_t launch_one(int grid, const HyperArgs& a, hipStream_t st) {
-    size_t lds = DMA ? 4 * (size_t)DADMM_HYPER_DQ * (2 * WR + 4) * 256 : 0;   // the ring
+    size_t lds = DMA ? 4 * (size_t)HYPER_DQ * (2 * WR + 4) * 256 : 0;   // the ring
     if (EPI == HYPER_EPI_GCN || EPI == HYPER_EPI_GCN_TRAIN || EPI == HYPER_EPI_GCN_BWD) {   // the epilogue (reuses the ring)
         size_t e = 4 * ((size_t)32 * WR * ZS + (((size_t)a.S_t * a.P * a.P + 3) & ~(size_t)3) + 4 * TN);
         if (EPI == HYPER_EPI_GCN_TRAIN) e += 4 * ((size_t)32 * WR * ZS + 2 * (size_t)a.S_t * TN);
@@ -1136,7 +1017,7 @@ hipError_t launch_wr(int wr, bool dma, int ks, int grid, const HyperArgs& a, hip
 // GCN layers: 191 -> 200 us)
 static bool use_dma(int K, int splits) {
     const int per = (K / 16 + splits - 1) / splits;
-    return DADMM_HYPER_DMA && per >= DADMM_HYPER_DMA_MIN;
+    return per >= HYPER_DMA_MIN;
 }
 
 template <int EPI>
@@ -1248,9 +1129,7 @@ static bool try_gcn32(HyperArgs& a, hipStream_t st, hipError_t& err) {
 // alone. a.kwave: 0 = never (the decoder's linears), else the P whose whole-sample tiles pair
 // with this GEMM (the split needs 32-row tiles of whole samples: P <= 32).
 // DADMM_HYPER_KW=0 in the environment: never (A/B timing).
-#ifndef DADMM_HYPER_KW_MIN
-#define DADMM_HYPER_KW_MIN 8    // k-steps (16 k each) from which the K loop is split
-#endif
+constexpr int HYPER_KW_MIN = 8;    // k-steps (16 k each) from which the K loop is split
 static bool hyper_kwave(const HyperArgs& a, int epi, int rows) {
     static int enabled = -1;
     if (enabled < 0) {
@@ -1262,7 +1141,7 @@ static bool hyper_kwave(const HyperArgs& a, int epi, int rows) {
     // epilogue is shorter than the chain it would overlap; profiles/r05/kwave_r05kw.txt)
     if (epi == HYPER_EPI_GCN || (epi == HYPER_EPI_GCN_TRAIN && a.K < 256)) return false;
     const int steps = a.K / 16;
-    if (steps < DADMM_HYPER_KW_MIN || hyper::use_dma(a.K, 1)) return false;
+    if (steps < HYPER_KW_MIN || hyper::use_dma(a.K, 1)) return false;
     const long tiles = (long)((rows + 31) / 32) * ((a.N + hyper::TN - 1) / hyper::TN);
     return tiles < 480;
 }

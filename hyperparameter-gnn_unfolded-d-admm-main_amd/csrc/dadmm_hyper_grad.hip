@@ -2,16 +2,12 @@
 // hypernetwork (gnn_dlasso_models_progressive.py:9-72, :93-123; backward through them as the
 // reference's loss_final.backward(), gnn_dlasso_progressive.py:207-214), accumulated in place:
 //
-//   wgrad_kernel  : G[N][K] += dZ^T X  (the weight gradient of one nn.Linear / GCNConv.lin over R
+//   wgrad2_kernel : G[N][K] += dZ^T X  (the weight gradient of one nn.Linear / GCNConv.lin over R
 //                   rows: dZ [R][N] is the gradient of the linear's output, X [R][K] its input,
 //                   optionally read as two column segments, cat(AtAy, Atb) in place), and
-//                   g_bias[N] += sum_r dZ[r][n] (the bias gradient) from the same dZ reads.
-//                   f32 MFMA v_mfma_f32_16x16x4_f32 with the R rows as the reduction (k) dimension:
-//                   lane (i, h) feeds dZ[r + h][n0 + i] and X[r + h][k0 + i]. One workgroup per
-//                   32 x 32 output tile (and R-split): its WV waves (4, 8 or 16: more for fewer
-//                   tiles) take interleaved 4-row steps (RING in flight each) and add their
-//                   partial tiles through LDS in a fixed pairwise tree. Splits > 1 (only for very
-//                   long R) write partial tiles that reduce_kernel adds into G in split order.
+//                   g_bias[N] += sum_r dZ[r][n] (the bias gradient) from the same dZ reads, on
+//                   v_mfma_f32_32x32x2_f32 with the R rows as the reduction dimension (below).
+//                   Splits > 1 write partial tiles that reduce_kernel adds into G in split order.
 //   colsum_kernel : out[g][c] += sum_r part[g][r][c] — the per-block partial sums of the BatchNorm /
 //                   bias (dadmm_hyper_gcn_train_bwd) and LayerNorm (dadmm_hyper_rownorm_bwd) parameter
 //                   gradients: 16 columns x 16 row slices per workgroup, slices added in order.
@@ -30,23 +26,6 @@ namespace hgrad {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int THREADS = 256;
-constexpr int TN = 32, TK = 32;   // output tile (n x k) per workgroup; its waves split the rows
-constexpr int RING = 8;           // row steps (4 rows each) of operands in flight per wave
-#ifndef DADMM_W2_OCC             // wgrad2 occupancy hint (timing builds: __attribute__((amdgpu_waves_per_eu(3, 3))))
-#define DADMM_W2_OCC
-#endif
-#ifndef DADMM_W2_FAST
-#define DADMM_W2_FAST 1           // wgrad2: branch-free rings where no range / block test can trigger
-#endif
-#ifndef DADMM_WGRAD2
-#define DADMM_WGRAD2 1            // 0: wgrad_kernel (32 x 32 tiles, 16x16x4 MFMA) for A/B builds
-#endif
-#ifndef DADMM_W2_FILL
-#define DADMM_W2_FILL 1           // wgrad2 row splits: one full round of workgroups (0: powers of two)
-#endif
-#ifndef DADMM_W2_SHORT
-#define DADMM_W2_SHORT 1          // wgrad2: short row walks on small grids split further
-#endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -60,148 +39,9 @@ __device__ __forceinline__ int xcd_tile(int bid, int G) {
     return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
 }
 
-template <int WV>
-__global__ __launch_bounds__(64 * WV) void wgrad_kernel(WgradArgs a) {
-    __shared__ float red[WV / 2][17][64];   // the tree's upper-half partials (16 tile + 1 bias / lane)
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int i = lane & 15, h = lane >> 4;
-    const int gn = (a.N + TN - 1) / TN, gk = (a.K + TK - 1) / TK;
-    const int tl = xcd_tile(blockIdx.x, gridDim.x);
-    const int kt = tl % gk, nt = (tl / gk) % gn, split = tl / (gk * gn);
-    const int n0 = nt * TN, k0 = kt * TK;
-    const int sb = (a.R + 3) / 4;                  // row steps per batch block
-    const int steps = sb * a.nb;
-    const int per = (steps + a.splits - 1) / a.splits;
-    const int s_begin = split * per;
-    const int s_end = s_begin + per < steps ? s_begin + per : steps;
-
-    // operand columns of this lane (clamped: out-of-range columns compute garbage, never stored)
-    int nc[2];
-    const float* xs[2];
-    int ldx[2];
-    bool k_lo[2];   // column from x1 (else x2)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-        int n = n0 + 16 * b + i;
-        nc[b] = n < a.N ? n : a.N - 1;
-        int k = k0 + 16 * b + i;
-        k = k < a.K ? k : a.K - 1;
-        k_lo[b] = k < a.K1;
-        if (k < a.K1) {
-            xs[b] = a.x1 + k;
-            ldx[b] = a.ld1;
-        } else {
-            xs[b] = a.x2 + (k - a.K1);
-            ldx[b] = a.ld2;
-        }
-    }
-    const bool do_bias = a.gbias != nullptr && kt == 0;
-
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int x = 0; x < 2; ++x) acc[x][0] = acc[x][1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-    float bsum[2] = {0.0f, 0.0f};
-
-    // wave w: steps s_begin + w, + WV, ...
-    float ra[RING][2], rb[RING][2];
-    auto load = [&](int u, int st) {
-        const int bb = a.nb > 1 ? st / sb : 0;
-        const int r = 4 * (st - bb * sb) + h;
-        const bool ok = st < s_end && r < a.R;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            ra[u][b] = ok ? a.dz[(size_t)bb * a.zs + (size_t)r * a.ldz + nc[b]] : 0.0f;
-            rb[u][b] = ok ? xs[b][(size_t)bb * (k_lo[b] ? a.s1 : a.s2) + (size_t)r * ldx[b]] : 0.0f;
-        }
-    };
-    const int first = s_begin + w;
-#pragma unroll
-    for (int u = 0; u < RING; ++u) load(u, first + WV * u);
-    for (int st = first; st < s_end; st += WV * RING) {
-#pragma unroll
-        for (int u = 0; u < RING; ++u) {
-            if (st + WV * u < s_end) {
-#pragma unroll
-                for (int x = 0; x < 2; ++x)
-#pragma unroll
-                    for (int y = 0; y < 2; ++y) acc[x][y] = mfma4(ra[u][x], rb[u][y], acc[x][y]);
-                if (do_bias) {
-                    bsum[0] += ra[u][0];
-                    bsum[1] += ra[u][1];
-                }
-            }
-            load(u, st + WV * (u + RING));
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    // bias: the 4 row groups h of the wave, in order
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-        const float v1 = __shfl_down(bsum[b], 16), v2 = __shfl_down(bsum[b], 32), v3 = __shfl_down(bsum[b], 48);
-        bsum[b] = ((bsum[b] + v1) + v2) + v3;
-    }
-    // fixed pairwise tree over the waves: at each level the upper half hands its partials to the
-    // lower half (wave w adds wave w + half's)
-    // (the wave's bias sums sit in lanes h = 0; lane (i, h) carries that of column block h & 1)
-    const float b0 = __shfl(bsum[0], i), b1 = __shfl(bsum[1], i);
-    float bcol = (h & 1) ? b1 : b0;
-#pragma unroll
-    for (int half = WV / 2; half >= 1; half /= 2) {
-        if (w >= half && w < 2 * half) {
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-#pragma unroll
-                for (int y = 0; y < 2; ++y)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) red[w - half][8 * x + 4 * y + q][lane] = acc[x][y][q];
-            red[w - half][16][lane] = bcol;
-        }
-        __syncthreads();
-        if (w < half) {
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-#pragma unroll
-                for (int y = 0; y < 2; ++y)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) acc[x][y][q] += red[w][8 * x + 4 * y + q][lane];
-            bcol += red[w][16][lane];
-        }
-        __syncthreads();
-    }
-    if (w > 0) return;
-    bsum[0] = __shfl(bcol, i);
-    bsum[1] = __shfl(bcol, i + 16);
-    // acc[x][y]: lane (i, h) holds G rows n0 + 16 x + 4 h + q (q = 0..3), column k0 + 16 y + i
-    float* out = a.splits > 1 ? a.scratch + (size_t)split * a.N * a.K : a.g;
-    const bool accum = a.splits == 1 && a.beta != 0;
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y) {
-            const int k = k0 + 16 * y + i;
-            if (k >= a.K) continue;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int n = n0 + 16 * x + 4 * h + q;
-                if (n >= a.N) continue;
-                float* o = out + (size_t)n * a.K + k;
-                *o = accum ? *o + acc[x][y][q] : acc[x][y][q];
-            }
-        }
-    if (do_bias && h == 0) {
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const int n = n0 + 16 * b + i;
-            if (n >= a.N) continue;
-            if (a.splits > 1) a.scratch_bias[(size_t)split * a.N + n] = bsum[b];
-            else a.gbias[n] = a.beta != 0 ? a.gbias[n] + bsum[b] : bsum[b];
-        }
-    }
-}
-
 // ---- wgrad on 32x32x2 MFMA with coalesced row operands (round 4, the default) -------------------
-// wgrad_kernel's lanes load one float of 16-column segments (64-byte pieces) and its 32 x 32 tiles
-// cannot split the rows of the deferred batched gradients, so a 400 x 400 weight over B P K rows
+// The round-3 wgrad_kernel (16x16x4 MFMA, lanes loading one float of 16-column segments, 32 x 32
+// tiles; removed, in git history) could not split the rows of the deferred batched gradients, so a 400 x 400 weight over B P K rows
 // ran on 169 workgroups: the gradients took ~40 % of the B = 4096 training step. Here: 64 x 64
 // output tiles, 4 waves each owning the whole tile (four 32x32 accumulators: 4096 flop per MFMA,
 // 16 flop per operand byte) over interleaved row-pair steps; lane (i, kh) of a step reads row
@@ -209,16 +49,13 @@ __global__ __launch_bounds__(64 * WV) void wgrad_kernel(WgradArgs a) {
 // 128-byte row segment. The rows split over S workgroups per tile (partial tiles in scratch, added
 // in split order by reduce_kernel: deterministic); the four waves' partials add through LDS in a
 // fixed tree. The bias column sums come from the same dZ reads (k-tile 0).
-#ifndef DADMM_W2_RING
-#define DADMM_W2_RING 8
-#endif
-constexpr int W2_T = 64, W2_WAVES = 4, W2_RING = DADMM_W2_RING;
+constexpr int W2_T = 64, W2_WAVES = 4, W2_RING = 8;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-__global__ __launch_bounds__(64 * W2_WAVES) DADMM_W2_OCC void wgrad2_kernel(WgradArgs a) {
+__global__ __launch_bounds__(64 * W2_WAVES) void wgrad2_kernel(WgradArgs a) {
     __shared__ float red[2][4 * 16 + 1][64];          // two waves' partial tiles (+ bias) per tree level
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = lane & 31, kh = lane >> 5;
@@ -308,7 +145,7 @@ __global__ __launch_bounds__(64 * W2_WAVES) DADMM_W2_OCC void wgrad2_kernel(Wgra
         }
     };
     const int first = s_begin + wv;
-    if (first < s_end && DADMM_W2_FAST && spb >= W2_WAVES) {
+    if (first < s_end && spb >= W2_WAVES) {
         // Branch-free rings: the load cursor's four pointers move by a per-step delta chosen with
         // wave-uniform conditions (the next step inside the block: 8 rows; into the next block:
         // that block's first rows; past the wave's range: 0, the slot is never consumed), and every
@@ -513,9 +350,6 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(const float* __restrict
 // hundred rows), so the sum is latency-bound: each workgroup takes CS_C = 16 columns of one g and
 // splits the rows over CS_S = 16 slices (slice s: rows s, s + 16, ..., 8 loads in flight), then
 // adds the 16 slice sums in slice order through LDS — a fixed order, deterministic run to run.
-#ifndef DADMM_COLSUM_2STAGE
-#define DADMM_COLSUM_2STAGE 1
-#endif
 constexpr int CS_C = 16, CS_S = THREADS / CS_C;
 // bout (round 4, two-stage form for many batch blocks): workgroup (x, y) sums batch block y alone
 // and writes it to bout [G][nb][C]; a second colsum over bout (R = nb) adds the blocks in order.
@@ -585,7 +419,6 @@ hipError_t launch_transpose(const float* in, int rows, int cols, float* out, hip
 }
 
 namespace {
-int wgrad_waves(int tiles) { return tiles >= 256 ? 4 : tiles >= 128 ? 8 : 16; }
 // wgrad2 workgroups resident at once: 3 per CU (80 VGPRs + 64 AGPRs hold 3 waves per SIMD) x the
 // current device's CU count, queried per call (256 CUs on MI355X: 768)
 long w2_slots() {
@@ -598,67 +431,47 @@ long w2_slots() {
 }
 
 int wgrad_splits(int R, int N, int K) {
-    if (DADMM_WGRAD2) {
-        // 64 x 64 tiles; rows split until ~4 workgroups per CU or each wave walks < 64 row pairs
-        const long tiles = (long)((N + hgrad::W2_T - 1) / hgrad::W2_T) * ((K + hgrad::W2_T - 1) / hgrad::W2_T);
-        const long steps = ((long)R + 1) / 2;
-        int s = 1;
-        bool short_walk = false;   // the doubling stopped on the walk length, not the grid size
-        while (tiles * s * 2 <= 1024 && s < 64) {
-            if (steps / (hgrad::W2_WAVES * s * 2) < 64) {
-                short_walk = true;
-                break;
-            }
-            s *= 2;
-        }
-        // Short walks on a small grid (the output head's and the last decoder layer's gradients
-        // over B K rows: 16 and 64 workgroups whose waves walked ~100 row pairs at ~0.25 us each,
-        // the ring's memory round trips exposed): split further, to >= 16 row pairs per wave
-        // (28.8 -> 15.7 and 25.6 -> 15.6 us at B = 256). Grids of 224-512 workgroups measured no
-        // faster or slower split.
-        const long slots = w2_slots();
-        if (DADMM_W2_SHORT && short_walk && tiles * s <= 128) {
-            long f = slots / tiles;
-            const long fmax = steps / (hgrad::W2_WAVES * 16);
-            f = f < fmax ? f : fmax;
-            if (f > s) return (int)f;
-        }
-        // A grid past one round of resident workgroups (w2_slots(): 3 per CU, 80 VGPRs + 64 AGPRs hold 3
-        // waves per SIMD) ran its last 16-128 workgroups as a second round (784 for a 400 x 400
-        // weight, 896 for 400 x 200): such grids split to fill one round exactly instead, each
-        // wave walking >= 32 row pairs. (Filling the smaller grids too, 512 -> 768 workgroups for
-        // the 100 x 512 layer, measured slower: 87 vs 78 us.)
-        if (DADMM_W2_FILL && tiles * s > slots) {
-            long f = slots / tiles;
-            const long fmax = steps / (hgrad::W2_WAVES * 32);
-            f = f < fmax ? f : fmax;
-            return f > 1 ? (int)f : 1;
-        }
-        return s;
-    }
-    const int tiles = ((N + hgrad::TN - 1) / hgrad::TN) * ((K + hgrad::TK - 1) / hgrad::TK);
-    const int steps = (R + 3) / 4;
-    const int wv = wgrad_waves(tiles);
+    // 64 x 64 tiles; rows split until ~4 workgroups per CU or each wave walks < 64 row pairs
+    const long tiles = (long)((N + hgrad::W2_T - 1) / hgrad::W2_T) * ((K + hgrad::W2_T - 1) / hgrad::W2_T);
+    const long steps = ((long)R + 1) / 2;
     int s = 1;
-    // split the rows only when every wave would walk more than 128 row steps and the grid is
-    // short of 4 workgroups per CU
-    while (tiles * s < 1024 && steps / (wv * s) > 128) s *= 2;
+    bool short_walk = false;   // the doubling stopped on the walk length, not the grid size
+    while (tiles * s * 2 <= 1024 && s < 64) {
+        if (steps / (hgrad::W2_WAVES * s * 2) < 64) {
+            short_walk = true;
+            break;
+        }
+        s *= 2;
+    }
+    // Short walks on a small grid (the output head's and the last decoder layer's gradients
+    // over B K rows: 16 and 64 workgroups whose waves walked ~100 row pairs at ~0.25 us each,
+    // the ring's memory round trips exposed): split further, to >= 16 row pairs per wave
+    // (28.8 -> 15.7 and 25.6 -> 15.6 us at B = 256). Grids of 224-512 workgroups measured no
+    // faster or slower split.
+    const long slots = w2_slots();
+    if (short_walk && tiles * s <= 128) {
+        long f = slots / tiles;
+        const long fmax = steps / (hgrad::W2_WAVES * 16);
+        f = f < fmax ? f : fmax;
+        if (f > s) return (int)f;
+    }
+    // A grid past one round of resident workgroups (w2_slots(): 3 per CU, 80 VGPRs + 64 AGPRs hold 3
+    // waves per SIMD) ran its last 16-128 workgroups as a second round (784 for a 400 x 400
+    // weight, 896 for 400 x 200): such grids split to fill one round exactly instead, each
+    // wave walking >= 32 row pairs. (Filling the smaller grids too, 512 -> 768 workgroups for
+    // the 100 x 512 layer, measured slower: 87 vs 78 us.)
+    if (tiles * s > slots) {
+        long f = slots / tiles;
+        const long fmax = steps / (hgrad::W2_WAVES * 32);
+        f = f < fmax ? f : fmax;
+        return f > 1 ? (int)f : 1;
+    }
     return s;
 }
 
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st) {
-    if (DADMM_WGRAD2) {
-        const int tiles = ((a.N + hgrad::W2_T - 1) / hgrad::W2_T) * ((a.K + hgrad::W2_T - 1) / hgrad::W2_T);
-        hipLaunchKernelGGL(hgrad::wgrad2_kernel, dim3(tiles * a.splits), dim3(64 * hgrad::W2_WAVES), 0, st, a);
-    } else {
-    const int tiles = ((a.N + hgrad::TN - 1) / hgrad::TN) * ((a.K + hgrad::TK - 1) / hgrad::TK);
-    const dim3 grid(tiles * a.splits);
-    switch (wgrad_waves(tiles)) {
-        case 4: hipLaunchKernelGGL(hgrad::wgrad_kernel<4>, grid, dim3(256), 0, st, a); break;
-        case 8: hipLaunchKernelGGL(hgrad::wgrad_kernel<8>, grid, dim3(512), 0, st, a); break;
-        default: hipLaunchKernelGGL(hgrad::wgrad_kernel<16>, grid, dim3(1024), 0, st, a); break;
-    }
-    }
+    const int tiles = ((a.N + hgrad::W2_T - 1) / hgrad::W2_T) * ((a.K + hgrad::W2_T - 1) / hgrad::W2_T);
+    hipLaunchKernelGGL(hgrad::wgrad2_kernel, dim3(tiles * a.splits), dim3(64 * hgrad::W2_WAVES), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || a.splits == 1) return e;
     const size_t cnt = (size_t)a.N * a.K;
@@ -674,7 +487,7 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t st) {
 hipError_t launch_colsum(const float* part, int G, int R, int C, float* out, int beta, hipStream_t st, int nb,
                          size_t pstride, float* bscratch) {
     const int blocks = G * ((C + hgrad::CS_C - 1) / hgrad::CS_C);
-    if (bscratch && nb > 1 && DADMM_COLSUM_2STAGE) {
+    if (bscratch && nb > 1) {
         hipLaunchKernelGGL(hgrad::colsum_kernel, dim3(blocks, nb), dim3(hgrad::THREADS), 0, st, part, G, R, C,
                            out, beta, nb, pstride, bscratch);
         hipError_t e = hipGetLastError();

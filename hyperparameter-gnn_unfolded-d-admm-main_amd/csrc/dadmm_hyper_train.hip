@@ -33,16 +33,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int THREADS = 256;
 constexpr int CB = 64;   // columns per gcn_bwd workgroup
 // gcn_bwd workgroup size NT: its passes 1-2 use one lane per column (64), so at 256 threads three
-// waves idle until the mix. When the grid fills the chip (>= DADMM_GCNBWD_WIDE_MIN workgroups) the
+// waves idle until the mix. When the grid fills the chip (>= GCNBWD_WIDE_MIN workgroups) the
 // one-wave form wins on throughput (B = 4096 train step 61.2 -> 56.6 ms); on small grids the
 // 4-wave mix's shorter per-lane chain wins (B = 256: 10.3 vs 10.8-11.6 ms). Same sums either way.
-#ifndef DADMM_GCNBWD_WIDE_MIN
-#define DADMM_GCNBWD_WIDE_MIN 2048
-#endif
+constexpr int GCNBWD_WIDE_MIN = 2048;
 // PR: at P <= PR agents a lane's rows are loaded at once into registers (0: the per-row loop)
-#ifndef DADMM_GCNBWD_PR
-#define DADMM_GCNBWD_PR 8
-#endif
+constexpr int GCNBWD_PR = 8;
 
 // One workgroup per (sample, 64 columns). LDS: M, then dM [P][CB]; A_hat block [P][P].
 template <int NT, int PR>
@@ -446,10 +442,10 @@ hipError_t launch_gcn_bwd(const GcnBwdArgs& a, hipStream_t st) {
     const int ncb = (a.N + hyper_train::CB - 1) / hyper_train::CB;
     const int grid = a.B * ncb;
     constexpr int T4 = hyper_train::THREADS;
-    if (a.P <= DADMM_GCNBWD_PR)
-        return grid >= DADMM_GCNBWD_WIDE_MIN ? launch_gcn_bwd_nt<64, DADMM_GCNBWD_PR>(a, grid, lds, st)
-                                             : launch_gcn_bwd_nt<T4, DADMM_GCNBWD_PR>(a, grid, lds, st);
-    return grid >= DADMM_GCNBWD_WIDE_MIN ? launch_gcn_bwd_nt<64, 0>(a, grid, lds, st)
+    if (a.P <= hyper_train::GCNBWD_PR)
+        return grid >= hyper_train::GCNBWD_WIDE_MIN ? launch_gcn_bwd_nt<64, hyper_train::GCNBWD_PR>(a, grid, lds, st)
+                                             : launch_gcn_bwd_nt<T4, hyper_train::GCNBWD_PR>(a, grid, lds, st);
+    return grid >= hyper_train::GCNBWD_WIDE_MIN ? launch_gcn_bwd_nt<64, 0>(a, grid, lds, st)
                                          : launch_gcn_bwd_nt<T4, 0>(a, grid, lds, st);
 }
 

@@ -33,19 +33,9 @@ __device__ __forceinline__ float row16_sum_dpp(float v) {
 }
 
 // The LayerNorm row sums (rownorm forward / backward and the hypernetwork tail kernel's copies of
-// them, which must reduce identically): wave_sum_dpp unless built with -DDADMM_LN_DPP=0 (the
-// __shfl_xor butterfly).
-#ifndef DADMM_LN_DPP
-#define DADMM_LN_DPP 1
-#endif
+// them, which must reduce identically): wave_sum_dpp.
 __device__ __forceinline__ float ln_row_sum(float v) {
-#if DADMM_LN_DPP
     return wave_sum_dpp(v);
-#else
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-#endif
 }
 
 
@@ -63,10 +53,7 @@ constexpr int M_PAD = 64;    // rows per m-group (4 m-blocks of 16 rows); the fu
 constexpr int M_MAX = 1024;  // rows per agent accepted by the ABI (the stepwise path: any m-group count)
 // padded rows per agent of the prepared operator: whole m-groups of 64 rows
 __host__ __device__ constexpr int m_pad_of(int m) { return (m + M_PAD - 1) / M_PAD * M_PAD; }
-#ifndef DADMM_FUSED_WAVES
-#define DADMM_FUSED_WAVES 8
-#endif
-constexpr int FUSED_WAVES = DADMM_FUSED_WAVES;  // waves per workgroup of the fused kernel
+constexpr int FUSED_WAVES = 8;  // waves per workgroup of the fused kernel
 
 // Arguments of the fused kernel (device pointers; see include/dadmm.h for the layouts).
 struct FusedArgs {
@@ -95,10 +82,6 @@ enum { GRAPH_SHARED = 0, GRAPH_LANE = 1, GRAPH_ORDERED = 2 };
 fused_fn_ptr find_fused(int P, int nt, int graph);
 // Same shapes, recording the adjoint's trajectory (a.Grec / a.Urec must be set).
 fused_fn_ptr find_fused_rec(int P, int nt, int graph);
-// The agent-resident form of the same forward (dadmm_resident.hip: 4 waves, one per SIMD, each
-// owning whole agents; bit-identical to find_fused's kernels), or nullptr for shapes it does not
-// hold (it serves n_pad = 256 with P = 4 or 5, shared or per-sample ascending graphs).
-fused_fn_ptr find_resident(int P, int nt, int graph);
 
 // ---- the column-split forward for small batches (dadmm_split.hip) ------------------------------
 constexpr int SPLIT_COLS = 64;   // columns of n_pad per slice (one workgroup each)

@@ -15,7 +15,6 @@
 // Outputs may use a padded row length n_store >= n (padding columns are left untouched).
 
 #include <hip/hip_runtime.h>
-#include <hiprand/hiprand_kernel.h>
 #include <stdint.h>
 
 #include "dadmm_internal.h"
@@ -36,44 +35,27 @@ __device__ __forceinline__ float2 box_muller(unsigned x, unsigned y) {
     return make_float2(sn * s, cs * s);
 }
 
-__device__ __forceinline__ float4 normal4(hiprandStatePhilox4_32_10_t* st) {
-    const uint4 r = hiprand4(st);
-    const float2 a = box_muller(r.x, r.y), b = box_muller(r.z, r.w);
-    return make_float4(a.x, a.y, b.x, b.y);
-}
 
-// DADMM_RNG_DIRECT: the Philox counter of draw `it` of virtual thread idx is formed directly
+// The Philox counter of draw `it` of virtual thread idx is formed directly
 // (rocrand's engine state after hiprand_init(seed, idx, offset) and `it` next4() calls: counter =
 // (offset / 4 + it, subsequence idx) as a 128-bit sum, key = seed) and its ten rounds evaluated
 // once. hiprand4 also evaluates the NEXT counter eagerly after each call, one Philox of four per
 // thread that no element uses; and the last draw's second Box-Muller pair is skipped when none of
 // its elements exists. Same words, same floats (offset % 4 == 0, so next4 never interleaves).
-#ifndef DADMM_RNG_DIRECT
-#define DADMM_RNG_DIRECT 1
-#endif
 
 // The launch is bound by these rounds (~60 % of its time at the headline shape), so each round
 // is 2 v_mad_u64_u32 (both halves of a product in one instruction; __umulhi plus a separate low
 // multiply compiled to v_mul_hi_u32 + v_mul_lo_u32) and 2 gfx950 v_bitop3_b32 (LUT 0x96 =
 // a ^ b ^ c; LLVM leaves the 3-way xors as pairs of v_xor_b32). The key word is wave-uniform.
 // Same integer results.
-#ifndef DADMM_RNG_MAD
-#define DADMM_RNG_MAD 1
-#endif
 __device__ __forceinline__ unsigned xor3(unsigned a, unsigned b, unsigned c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 __device__ __forceinline__ uint4 philox_round(uint4 c, uint2 k) {
-#if DADMM_RNG_MAD
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     return make_uint4(xor3((unsigned)(p1 >> 32), c.y, k.x), (unsigned)p1,
                       xor3((unsigned)(p0 >> 32), c.w, k.y), (unsigned)p0);
-#else
-    const unsigned hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-    const unsigned hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-    return make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
-#endif
 }
 
 __device__ __forceinline__ uint4 philox10(uint4 c, uint2 k) {
@@ -109,37 +91,23 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
         // transformation::normal (val * std + mean), contracted as torch's build does
         out[o] = __builtin_fmaf(v, a.stddev, a.mean);
     };
-    if (DADMM_RNG_DIRECT) {
-        // counter after discard_subsequence(idx) then discard(offset): (x, y) = offset / 4,
-        // (z, w) = idx plus the carry out of y
-        const uint64_t c0 = (a.offset + (uint64_t)t * a.offset_step) / 4;
-        const uint2 key = make_uint2((unsigned)a.seed, (unsigned)(a.seed >> 32));
-        uint32_t li = idx;
-        for (uint32_t it = 0; it < iters; ++it, li += 4 * T) {
-            const uint64_t cx = c0 + it;                      // the counter's low 64 bits
-            const unsigned carry = cx < c0 ? 1u : 0u;         // into the subsequence words
-            const uint4 r = philox10(make_uint4((unsigned)cx, (unsigned)(cx >> 32), idx + carry,
-                                                (idx + carry < idx) ? 1u : 0u), key);
-            const float2 p0 = box_muller(r.x, r.y);
-            if (li < numel) put(li, p0.x);
-            if (li + T < numel) put(li + T, p0.y);
-            if (li + 2 * T < numel) {
-                const float2 p1 = box_muller(r.z, r.w);
-                put(li + 2 * T, p1.x);
-                if (li + 3 * T < numel) put(li + 3 * T, p1.y);
-            }
-        }
-        return;
-    }
-    hiprandStatePhilox4_32_10_t st;
-    hiprand_init(a.seed, (unsigned long long)idx, a.offset + (uint64_t)t * a.offset_step, &st);
+    // counter after discard_subsequence(idx) then discard(offset): (x, y) = offset / 4,
+    // (z, w) = idx plus the carry out of y
+    const uint64_t c0 = (a.offset + (uint64_t)t * a.offset_step) / 4;
+    const uint2 key = make_uint2((unsigned)a.seed, (unsigned)(a.seed >> 32));
     uint32_t li = idx;
-    for (uint32_t it = 0; it < iters; ++it) {
-        const float4 r = normal4(&st);
-        const float v[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii, li += T) {
-            if (li < numel) put(li, v[ii]);
+    for (uint32_t it = 0; it < iters; ++it, li += 4 * T) {
+        const uint64_t cx = c0 + it;                      // the counter's low 64 bits
+        const unsigned carry = cx < c0 ? 1u : 0u;         // into the subsequence words
+        const uint4 r = philox10(make_uint4((unsigned)cx, (unsigned)(cx >> 32), idx + carry,
+                                            (idx + carry < idx) ? 1u : 0u), key);
+        const float2 p0 = box_muller(r.x, r.y);
+        if (li < numel) put(li, p0.x);
+        if (li + T < numel) put(li + T, p0.y);
+        if (li + 2 * T < numel) {
+            const float2 p1 = box_muller(r.z, r.w);
+            put(li + 2 * T, p1.x);
+            if (li + 3 * T < numel) put(li + 3 * T, p1.y);
         }
     }
 }

@@ -49,45 +49,16 @@ constexpr int NW = 8;            // waves per workgroup (the default form; 16: o
 constexpr int CT = 2;            // 16-column MFMA tiles per step
 constexpr int CW = 16 * CT;      // columns per step
 constexpr int SLOTS = 3;         // y-block ring: the block of step bs + 2 is loaded during step bs
-// DADMM_ST_ABL (timing builds only, wrong results): 1 = no consensus walk, 2 = no operator loads,
-// 4 = no step-top wait / barrier, 8 = no Y / U stores, 16 = no y-block DMA
-#ifndef DADMM_ST_ABL
-#define DADMM_ST_ABL 0
-#endif
-// cache policy of the state streams (y-block copies, U, d0, Y and U stores); 2 = non-temporal (so
-// that they would not evict the operator from L2) measured no faster (6.04 vs 5.96 ms, configs[2])
-// DADMM_ST_PRIO=1: raise the wave's priority while it issues an MFMA chain (the arbiter then
-// prefers it, so the matrix pipe is fed while the other wave of the SIMD runs its VALU work):
-// 6.03-6.07 vs 6.09-6.14 ms at configs[2], four interleaved rounds, bit-identical
-// (profiles/r03/stream_prio_r03.jsonl)
-#ifndef DADMM_ST_PRIO
-#define DADMM_ST_PRIO 1
-#endif
-#ifndef DADMM_ST_QPF
-#define DADMM_ST_QPF 0
-#endif
-#ifndef DADMM_ST_DESYNC
-#define DADMM_ST_DESYNC 0
-#endif
-#ifndef DADMM_ST_AUX
-#define DADMM_ST_AUX 0
-#endif
-// DADMM_ST_AT_FROM_A=1: GEMM2's A^T fragments are read from the A_pad copy (4-byte loads, four
-// 64-byte row segments per instruction) instead of the At_pad copy: the tile's GEMM1 reads the
-// same 4 KB of A, so the operator the kernel keeps in L2 halves (A_pad and At_pad are the same
-// bytes twice: 2 x 2 MB at configs[2], a whole XCD's L2): 5.85-5.90 vs 6.04-6.10 ms at configs[2],
-// bit-identical (profiles/r04/variants_r04c.txt)
-#ifndef DADMM_ST_AT_FROM_A
-#define DADMM_ST_AT_FROM_A 1
-#endif
-// DADMM_ST_DELAY=1: a tile's U / Y (and recording) stores are issued after the NEXT tile's operand
-// loads, so that no wait for those loads includes them (vector-memory operations complete in
-// order and vmcnt counts stores): the stores get two tiles instead of one to drain. Bit-identical,
-// but the held values raise the spills 7 -> 17 VGPRs: 5.99-6.04 vs 5.87-5.89 ms at configs[2]
-// (profiles/r04/variants_r04p_stream_delay.txt), so off
-#ifndef DADMM_ST_DELAY
-#define DADMM_ST_DELAY 0
-#endif
+// Decisions measured at configs[2] (round 6 removed the A/B switches):
+//   * the wave's priority raised while it issues an MFMA chain (the arbiter then prefers it, so
+//     the matrix pipe is fed while the other wave of the SIMD runs its VALU work): 6.03-6.07 vs
+//     6.09-6.14 ms, bit-identical (profiles/r03/stream_prio_r03.jsonl);
+//   * GEMM2's A^T fragments read from the A_pad copy (4-byte loads, four 64-byte row segments per
+//     instruction) instead of At_pad: the tile's GEMM1 reads the same 4 KB of A, so the operator
+//     kept in L2 halves: 5.85-5.90 vs 6.04-6.10 ms (profiles/r04/variants_r04c.txt);
+//   * default cache policy on the state streams (non-temporal: 6.04 vs 5.96 ms); the stores of a
+//     tile issued right after it (behind the next tile's loads: 17 spilled VGPRs, 5.99-6.04 vs
+//     5.87-5.89 ms); the two waves of a SIMD in the same phase order; no extra operand prefetch.
 #define DADMM_STR_(x) #x
 #define DADMM_STR(x) DADMM_STR_(x)
 
@@ -103,11 +74,6 @@ __device__ __forceinline__ i32x4 rsrc_words(const void* base, uint32_t bytes) {
     const uint64_t b = (uint64_t)base;
     return (i32x4){(int)(uint32_t)b, (int)(uint32_t)(b >> 32) & 0xffff, (int)bytes, 0x00020000};
 }
-#if DADMM_ST_AUX == 2
-#define DADMM_ST_DMA_POL " nt"
-#else
-#define DADMM_ST_DMA_POL ""
-#endif
 // LDS-DMA of 16 bytes per lane into LDS at m0 + 16 lane, issued from inline asm: the compiler's
 // wait analysis then does not treat every later LDS read as a possible alias of the copy (it would
 // wait for the whole copy before the first such read, i.e. two steps too early); the kernel waits
@@ -115,7 +81,7 @@ __device__ __forceinline__ i32x4 rsrc_words(const void* base, uint32_t bytes) {
 // does not count only makes them wait longer. (m0 is a reserved register, so the compiler warns
 // about the clobber; no other instruction of this kernel reads m0 — checked in its ISA.)
 __device__ __forceinline__ void dma16(uint32_t lds_addr, uint32_t voff, i32x4 rsrc) {
-    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" DADMM_ST_DMA_POL " lds"
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" " lds"
                  :
                  : "s"(lds_addr), "v"(voff), "s"(rsrc)
                  : "memory", "m0");
@@ -241,7 +207,7 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
     // offset past the range, which the hardware returns as zeros)
     auto dma = [&](int k, int blk, float* slot) {
         const float* src = k <= 0 ? a.y0 : a.Y + (size_t)(k - 1) * S;
-        const i32x4 r = rsrc_words(src, (k <= kend && !(DADMM_ST_ABL & 16)) ? s_bytes : 0u);
+        const i32x4 r = rsrc_words(src, (k <= kend) ? s_bytes : 0u);
 #pragma unroll
         for (int ai = 0; ai < PW; ++ai) {
             const int q = w + NW * ai;
@@ -262,10 +228,9 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
     const uint32_t at_bytes = (uint32_t)((size_t)P * NP * 64 * 4);
     // launch-constant descriptors; a phase or lane without the operand gets an out-of-range offset
     // (zeros, no memory access) instead of a different descriptor
-    const rsrc_t dAt = make_rsrc(a.At, (DADMM_ST_ABL & 2) ? 0u : at_bytes);
-    const rsrc_t dA = make_rsrc(a.A, (DADMM_ST_ABL & 2) ? 0u : at_bytes);
+    const rsrc_t dA = make_rsrc(a.A, at_bytes);
     const rsrc_t dd0 = make_rsrc(a.d0, s_bytes), db = make_rsrc(a.b, (uint32_t)((size_t)B * P * m * 4));
-    const uint32_t vat = (uint32_t)((j * 64 + 4 * bq) * 4), vam = (uint32_t)((j * NP + 4 * bq) * 4);
+    const uint32_t vam = (uint32_t)((j * NP + 4 * bq) * 4);
     // the global operands of tile i = (agent i / CT, columns 16 (i % CT)) of step bs: fetch_a (A^T
     // rows, U_{k-1}, d0) is issued at the start of the previous tile, fetch_m (A rows, needed only at
     // the tile's end) after the previous tile's GEMM2, when its A^T registers are free
@@ -274,9 +239,6 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
         const int p = w + NW * ai;
         const bool pin = p < P;
         const int pc = pin ? p : 0;
-        const uint32_t vo = (k >= 0 && k < K && pin) ? vat : 0x80000000u;
-        const uint32_t sb = (uint32_t)((((size_t)pc * NP + c0 + 16 * ct) * 64) * 4);
-#if DADMM_ST_AT_FROM_A
         // lane (j, bq), m-block t: A_p rows 16 t + 4 bq + r, column c0 + 16 ct + j
         const uint32_t voa = (k >= 0 && k < K && pin) ? (uint32_t)(((4 * bq) * NP + j) * 4) : 0x80000000u;
         const uint32_t sba = (uint32_t)((((size_t)pc * 64) * NP + c0 + 16 * ct) * 4);
@@ -286,17 +248,12 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
             for (int r4 = 0; r4 < 4; ++r4)
                 r.at[t][r4] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                     dA, voa, sba + (uint32_t)((16 * t + r4) * NP * 4), 0));   // row step in soffset
-#else
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-            r.at[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dAt, vo + 64 * t, sb, 0));
-#endif
         const uint32_t off = (pin && col_ok(c0, ct)) ? (uint32_t)(elem(pc, c0, ct) * 4) : 0x80000000u;
         // U_{k-1} (k = 0: U0 itself; k = 1: U_0 = U0)
         r.u = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-            make_rsrc(k <= 1 ? a.U0 : a.Ubuf[0], s_bytes), k >= 0 ? off : 0x80000000u, 0, DADMM_ST_AUX));
+            make_rsrc(k <= 1 ? a.U0 : a.Ubuf[0], s_bytes), k >= 0 ? off : 0x80000000u, 0, 0));
         r.d = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dd0, k == 0 ? off : 0x80000000u, 0,
-                                                                              DADMM_ST_AUX));
+                                                                              0));
     };
     auto fetch_m = [&](int k, int c0, int i, Ring& r) {
         const int ai = i / CT, ct = i % CT;
@@ -326,32 +283,6 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
     // or an out-of-range offset disables one), because the compiler's wait analysis turns a memory
     // operation on one path of a merge into a full vmcnt wait after it. GEMM2 and the update run
     // in the phases without a primal update too (on A^T = 0; nothing is stored).
-    // the previous tile's stores (DADMM_ST_DELAY): values, offsets (out of range = none) and phase
-    typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
-    struct Pend {
-        f32x4 u, y, g;
-        uint32_t su, sy;
-        int k;
-    } pend;
-    pend.u = pend.y = pend.g = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-    pend.su = pend.sy = 0x80000000u;
-    pend.k = 0;
-    auto flush = [&]() {
-        const int pk = pend.k;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend.u),
-                                               make_rsrc(pk == K ? a.U_out : a.Ubuf[0], (DADMM_ST_ABL & 8) ? 0u : s_bytes),
-                                               pend.su, 0, DADMM_ST_AUX);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend.y),
-                                               make_rsrc(a.Y + (size_t)(pk < K ? pk : 0) * S, (DADMM_ST_ABL & 8) ? 0u : s_bytes),
-                                               pend.sy, 0, DADMM_ST_AUX);
-        if constexpr (REC) {
-            const size_t kS = (size_t)(pk < K ? pk : 0) * S;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend.g), make_rsrc(a.Grec + kS, s_bytes),
-                                                   pend.sy, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend.u), make_rsrc(a.Urec + kS, s_bytes),
-                                                   pend.sy, 0, 0);
-        }
-    };
     auto compute = [&](int k, int c0, const float* ys, int i, Ring& r, auto&& pre, auto&& mid) {
         const int ai = i / CT, ct = i % CT;
         const int p = w + NW * ai;
@@ -360,23 +291,13 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
         const f32x4 yo = *(const f32x4*)(ys + 4 * ((p * CT + ct) * 64 + lane));
         // delta_k = compute_delta(y_k) (unfolded_DLASSO.py:127-140): acc + (y_p - y_q) over p's visit
         // row, four entries per LDS word (no walk in phases -1 and 0)
-        const int D = (k >= 1 && !(DADMM_ST_ABL & 1)) ? __builtin_amdgcn_readfirstlane(dmx[p]) : 0;   // 0 for p >= P
+        const int D = (k >= 1) ? __builtin_amdgcn_readfirstlane(dmx[p]) : 0;   // 0 for p >= P
         const uint32_t* vrow = vt + (p * BT + j) * DP;
         const char* ybase = (const char*)(ys + 4 * (ct * 64 + lane));
         auto walk = [&]() {
             f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#if DADMM_ST_QPF
-            // the next four entries are read while this group's rows are in flight (one LDS round
-            // trip per group instead of two; the read past a row's end stays inside the table / dmx)
-            uint4 qn = *(const uint4*)vrow;
-#endif
             for (int t4 = 0; t4 < D; t4 += 4) {
-#if DADMM_ST_QPF
-                const uint4 qo = qn;
-                qn = *(const uint4*)(vrow + t4 + 4);
-#else
                 const uint4 qo = *(const uint4*)(vrow + t4);
-#endif
                 const uint32_t qa[4] = {qo.x, qo.y, qo.z, qo.w};
                 f32x4 yqs[4];   // the four neighbour reads in flight together
 #pragma unroll
@@ -393,31 +314,23 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
             return acc;
         };
         // GEMM2: A_p^T R_k, this tile's columns (16 dependent MFMAs, no input from the walk).
-        // DADMM_ST_DESYNC=1: the two waves of a SIMD (w and w + 4) take the walk and GEMM2 in opposite
-        // orders (one's VALU / LDS work beside the other's MFMA chain): measured 6.18-6.31 vs
-        // 6.13-6.19 ms at configs[2], so off.
+        // (The two waves of a SIMD taking the walk and GEMM2 in opposite orders measured 6.18-6.31
+        // vs 6.13-6.19 ms.)
         auto gemm2 = [&]() {
-            if (DADMM_ST_PRIO) __builtin_amdgcn_s_setprio(1);
+            __builtin_amdgcn_s_setprio(1);
             f32x4 g = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int r4 = 0; r4 < 4; ++r4) g = mfma4(r.at[t][r4], Rk[ai][t][r4], g);
-            if (DADMM_ST_PRIO) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(0);
             return g;
         };
-        f32x4 acc, gc;
-        if (DADMM_ST_DESYNC && (w & 4)) {
-            gc = gemm2();
-            acc = walk();
-        } else {
-            acc = walk();
-            gc = gemm2();
-        }
+        const f32x4 acc = walk();
+        const f32x4 gc = gemm2();
         // the next tile's A^T rows, U, d0 and A rows: issued at one program point (outside the branch)
         pre();
         mid();
-        if (DADMM_ST_DELAY) flush();   // the previous tile's stores, behind this tile's loads
         f32x4 dv = k == 0 ? r.d : acc;
         if (k >= 1 && a.variant != 0) {
 #pragma unroll
@@ -433,10 +346,9 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
         bad_u0 |= k == 0 && okc && !finite4(uv);
         // U_k after the next tile's A rows are issued: vector-memory operations complete in order,
         // so a load issued after a store waits for it
-        if (!DADMM_ST_DELAY)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, uv),
-                                                   make_rsrc(k == K ? a.U_out : a.Ubuf[0], (DADMM_ST_ABL & 8) ? 0u : s_bytes),
-                                                   k >= 1 ? soff : 0x80000000u, 0, DADMM_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, uv),
+                                               make_rsrc(k == K ? a.U_out : a.Ubuf[0], s_bytes),
+                                               k >= 1 ? soff : 0x80000000u, 0, 0);
         const bool upd = k >= 0 && k < K;
         f32x4 yn, grc;
 #pragma unroll
@@ -452,19 +364,10 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
             bad_y |= upd && okc && !finitef(v);
             yn[r4] = okc ? v : 0.0f;
         }
-        if (DADMM_ST_DELAY) {
-            pend.u = uv;
-            pend.y = yn;
-            pend.g = grc;
-            pend.su = k >= 1 ? soff : 0x80000000u;
-            pend.sy = upd ? soff : 0x80000000u;
-            pend.k = k;
-        } else {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, yn),
-                                               make_rsrc(a.Y + (size_t)(upd ? k : 0) * S, (DADMM_ST_ABL & 8) ? 0u : s_bytes),
-                                               upd ? soff : 0x80000000u, 0, DADMM_ST_AUX);
-        }
-        if constexpr (REC && !DADMM_ST_DELAY) {   // the adjoint's trajectory: Grec[k] (pre-clamp gradient), Urec[k] = U_k
+                                               make_rsrc(a.Y + (size_t)(upd ? k : 0) * S, s_bytes),
+                                               upd ? soff : 0x80000000u, 0, 0);
+        if constexpr (REC) {   // the adjoint's trajectory: Grec[k] (pre-clamp gradient), Urec[k] = U_k
             const size_t kS = (size_t)(upd ? k : 0) * S;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, grc),
                                                    make_rsrc(a.Grec + kS, s_bytes), upd ? soff : 0x80000000u, 0, 0);
@@ -475,12 +378,12 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
         // GEMM1: R_{k+1} += A_p[:, tile] y_{k+1}[tile] (phase -1: R_0 from y_0)
         const f32x4 gin = k == -1 ? yo : yn;
         if (k < K - 1) {
-            if (DADMM_ST_PRIO) __builtin_amdgcn_s_setprio(1);
+            __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int r4 = 0; r4 < 4; ++r4) Rn[ai][t] = mfma4(r.am[t][r4], gin[r4], Rn[ai][t]);
-            if (DADMM_ST_PRIO) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(0);
         }
     };
 
@@ -536,7 +439,7 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
             // step bs's block has landed (every wave's DMA), every wave is done with step bs - 1's
             // slot, and this wave's stores of step bs - 2 have completed (the ring reads Y[k - 1]'s
             // block NB - 2 >= 2 steps after it was written)
-            if (!(DADMM_ST_ABL & 4)) {
+            {
                 if (bs > 0) wait_prev_step(blk > 0 ? k : k - 1, K);
                 __syncthreads();
             }
@@ -576,7 +479,6 @@ __global__ __launch_bounds__(64 * NWT) void stream_kernel(TiledArgs a) {
             slot = slot == SLOTS - 1 ? 0 : slot + 1;
         }
     }
-    if (DADMM_ST_DELAY) flush();
     status |= (bad_y0 ? 1u : 0u) | (bad_u0 ? 2u : 0u) | (bad_g ? 4u : 0u) | ((bad_y || bad_h) ? 8u : 0u);
     if (a.status != nullptr) {
         uint32_t ws = status;

@@ -65,14 +65,11 @@ constexpr int ST = HALVES * BT;      // samples per workgroup
 // MB = m-groups of 64 rows per agent (m_pad = 64 MB; MB in {1, 2}). The update phase works in
 // chunks of CH = 2 / MB n-tiles, so that a chunk's A^T rows (CH x 4 MB vectors) take the same
 // registers for both; with MB = 2 the GEMM2 B operand (R) is read from LDS, not held.
-// DADMM_TILED_DB (MB = 1): chunks of one n-tile, double-buffered (chunk c + 1's loads in flight
+// MB = 1: chunks of one n-tile, double-buffered (chunk c + 1's loads in flight
 // under chunk c's update) in the registers one 2-tile chunk took (160 VGPRs instead of 192)
-#ifndef DADMM_TILED_DB
-#define DADMM_TILED_DB 1
-#endif
 template <int MB>
 struct Chunk {                       // one chunk's operands
-    static constexpr bool DB = DADMM_TILED_DB > 0 && MB == 1;
+    static constexpr bool DB = MB == 1;
     static constexpr int CH = DB ? 1 : 2 / MB;   // n-tiles per chunk of the update phase
     static constexpr int RG = CH * HALVES;       // row groups per chunk
     f32x4 yp[RG], up[RG], dv[RG];
@@ -494,11 +491,6 @@ __global__ __launch_bounds__(THREADS) void consensus_kernel(TiledArgs a, const f
 // visit list over the LDS rows (the consensus kernel's order), the deferred dual update, the
 // GEMM2 chain and the primal update, exactly as iter_kernel.
 constexpr int ST2 = 2 * BT;
-// DADMM_CS_ABL (timing builds only, wrong results): 1 = no consensus walk, 2 = no R / A^T loads,
-// 4 = no y-block DMA
-#ifndef DADMM_CS_ABL
-#define DADMM_CS_ABL 0
-#endif
 size_t colsplit_lds_bytes(int P, int CW, int vcap) {
     return 4 * (size_t)ST2 * P * CW + 4 * (size_t)(ST2 * P + 1) + (size_t)vcap + 4;
 }
@@ -532,8 +524,7 @@ __global__ __launch_bounds__(THREADS) void colupdate_kernel(TiledArgs a, int k, 
             const uint32_t off = (sl < ns && c < n)
                                      ? (uint32_t)((((size_t)(s0 + sl) * P + p) * n + c) * 4)
                                      : 0x80000000u;
-            if (!(DADMM_CS_ABL & 4))
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (lds_void*)(ys + 4 * base), 16, off, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (lds_void*)(ys + 4 * base), 16, off, 0, 0, 0);
         }
     }
     // visit lists of the tile's samples (one list for a shared graph)
@@ -614,17 +605,14 @@ __global__ __launch_bounds__(THREADS) void colupdate_kernel(TiledArgs a, int k, 
             dg[hh] = s < B ? a.deg[(a.graph_shared ? 0 : s * P) + p] : 0.0f;
 #pragma unroll
             for (int t = 0; t < TM; ++t)
-                rv[hh][t] = (!final_only && s < B && !(DADMM_CS_ABL & 2))
+                rv[hh][t] = (!final_only && s < B)
                                 ? *(const f32x4*)(a.R + ((size_t)s * P + p) * MP + 16 * t + 4 * h)
                                 : (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
         }
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int col = c0 + 16 * nt + 4 * h;
-            if (DADMM_CS_ABL & 2) {
-#pragma unroll
-                for (int t = 0; t < TM; ++t) at[nt][t] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-            } else if (!final_only) {
+            if (!final_only) {
                 const float* atp = a.At + ((size_t)p * NP + c0 + 16 * nt + j) * MP + 4 * h;
 #pragma unroll
                 for (int t = 0; t < TM; ++t) at[nt][t] = *(const f32x4*)(atp + 16 * t);
@@ -642,7 +630,7 @@ __global__ __launch_bounds__(THREADS) void colupdate_kernel(TiledArgs a, int k, 
                 yv[nt][hh] = yl(sl, p, 4 * nt + h);
             }
         }
-        if (k > 0 && !(DADMM_CS_ABL & 1)) {   // delta_k = compute_delta(y_k) (unfolded_DLASSO.py:127-140), both halves'
+        if (k > 0) {   // delta_k = compute_delta(y_k) (unfolded_DLASSO.py:127-140), both halves'
                        // lists walked together, each element's chain in its list's order
             int v0[HALVES], len[HALVES], lmax = 0;
 #pragma unroll
@@ -736,19 +724,13 @@ size_t tiled_lds_bytes(int n_pad, int m_pad) {
     return stage + 4 * (size_t)(tiled::ST * (m_pad + 4));
 }
 
-// DADMM_TILED_SPLIT=1 builds the column-split form (iter_kernel<., ., RONLY> + colupdate_kernel)
-// instead of the two-launch (consensus + iteration kernel) form. Bit-identical; measured slower at
-// configs[2] (7.4 vs 6.9 ms per forward), so off by default.
-#ifndef DADMM_TILED_SPLIT
-#define DADMM_TILED_SPLIT 0
-#endif
+// DADMM_TILED_SPLIT=1 in the environment selects the column-split form (iter_kernel<., ., RONLY> +
+// colupdate_kernel) instead of the two-launch (consensus + iteration kernel) form. Bit-identical;
+// measured slower at configs[2] (7.4 vs 6.9 ms per forward), so off by default.
 // the column block of the split path: the widest of 64 / 32 / 16 columns whose LDS (y block of
 // 32 samples x P agents + visit lists) keeps two workgroups per CU, else the narrowest that fits
 // one; 0 = the split path does not apply. The swizzle needs P CW / 4 to be a multiple of 16.
 static int colsplit_width(int P, int vcap) {
-#ifdef DADMM_CS_CW   // timing builds: a fixed column block
-    if (tiled::colsplit_lds_bytes(P, DADMM_CS_CW, vcap) <= 160 * 1024) return DADMM_CS_CW;
-#endif
     int best = 0;
     for (int cw : {64, 32, 16}) {
         if ((P * cw / 4) % 16 != 0) continue;
@@ -795,8 +777,8 @@ hipError_t launch_tiled(const TiledArgs& a, hipStream_t stream) {
     const char* senv = getenv("DADMM_TILED_STREAM");
     if ((senv == nullptr || atoi(senv) != 0) && stream_applies(a)) return launch_stream(a, stream);
     const size_t lds = tiled_lds_bytes(a.n_pad, a.m_pad);
-    const char* env = getenv("DADMM_TILED_SPLIT");   // runtime override of the build default
-    const bool split = env != nullptr ? atoi(env) != 0 : DADMM_TILED_SPLIT != 0;
+    const char* env = getenv("DADMM_TILED_SPLIT");
+    const bool split = env != nullptr && atoi(env) != 0;
     // the column-split update reads the visit lists as 32-bit words: a word-aligned base only
     // (a sharded view gb.vq[base:] may start anywhere; it takes the two-launch form)
     const bool vq_words = ((uintptr_t)a.vq & 3u) == 0;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU session: each step under its own time limit, chained with &&; the first failure ends
 # the session (no retries). Output under gpurun_out/$TAG/.
-#   TAG=name STEPS="tests:<pytest args> | ab | prologue | bench:<args> | prof:<bench args> | cmd:<shell>" bash scripts/session.sh
+#   TAG=name STEPS="tests:<pytest args> | prologue | bench:<args> | prof:<bench args> | cmd:<shell>" bash scripts/session.sh
 # (steps are split on "|": a cmd step must not contain one — chain with && instead)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -16,7 +16,6 @@ for st in "${ST[@]}"; do
   i=$((i + 1))
   case "$kind" in
     tests)    timeout -k 10 900 python -u -m pytest $arg -x -v --timeout 120 --timeout-method thread > "$O/tests_$i.txt" 2>&1 ;;
-    ab)       timeout -k 10 300 python -u scripts/time_headline.py $arg > "$O/ab_$i.txt" 2>&1 ;;
     prologue) for so in hyperparameter-gnn_unfolded-d-admm-main_amd/dadmm_hip/libdadmm.so build/var/libdadmm_rngold.so; do
                 DADMM_LIB_VARIANT=$PWD/$so timeout -k 10 120 python -u scripts/time_prologue.py >> "$O/prologue_$i.txt" 2>&1 || exit $?
               done ;;
