@@ -522,9 +522,9 @@ int dadmm_gnn_step(const dadmm_dims* d, int32_t k, const int32_t* visit_ptr, con
     if (rc) return rc;
     if (k < 0 || k >= d->K) return fail(DADMM_EINVAL, "k=%d outside [0, K)", k);
     if (d->B == 0) return ok();
-    if (!visit_ptr || !visit_q || !deg || !hyp_k || !yptr || !AtAy || !Atb || !U || !U_next || !G || !flags)
+    if (!visit_ptr || !visit_q || !deg || !hyp_k || !yptr || !AtAy || !Atb || !U || !D || !U_next ||
+        !D_next || !G || !flags)
         return fail(DADMM_EINVAL, "a required pointer is NULL");
-    if (!D && k == 0) return fail(DADMM_EINVAL, "D (delta_0) is required at k = 0");
     if (!aligned16(AtAy) || !aligned16(Atb) || !aligned16(U) || !aligned16(D) || !aligned16(G) ||
         !aligned16(U_next) || !aligned16(D_next))
         return fail(DADMM_EINVAL, "AtAy, Atb, U, D, U_next, D_next and G must be 16-byte aligned");

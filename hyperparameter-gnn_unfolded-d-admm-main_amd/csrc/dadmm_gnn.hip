@@ -521,11 +521,11 @@ __global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int 
     }
 }
 
-// ---- step: gradient, primal update, consensus and dual update of (sample, UC columns) -----------
-// One workgroup per (sample, UC = 128 columns; 64 in the RECOMP form below). A lane owns 4 columns of one agent row; a wave
+// ---- step: gradient, primal update, consensus and dual update of (sample, 128 columns) ----------
+// One workgroup per (sample, UCB = 128 columns). A lane owns 4 columns of one agent row; a wave
 // instruction covers two agent rows (lanes 0-31 and 32-63), so every global access is a 16-byte
 // vector and a wave keeps UP_CH row pairs of loads in flight. y_{k+1} of all P agents is staged in
-// LDS ([P][UC], 25.6 KB at P = 50) next to the sample's visit lists, and the consensus reads its
+// LDS ([P][UCB], 25.6 KB at P = 50) next to the sample's visit lists, and the consensus reads its
 // neighbours from there in the reference's visit order (one fp32 add chain per column from 0).
 // update_item<FUSED> on item (sample, column block). FUSED: the gradient g = clamp(((AtAy - Atb) + sign(y) tau) + U deg + delta rho) (:205-213) is
 //   formed from AtAy, Atb, y, U, delta in the same pass (its NaN sets GBAD(k)); the y_next / U
@@ -535,37 +535,32 @@ __global__ __launch_bounds__(64 * GL_WAVES) void gram_lds_kernel(GnnArgs a, int 
 //   optimistic flags, every block exits; else the update again with g = 0 (:216-218), writing the
 //   guard flags themselves.
 constexpr int UP_CH = 4;
-// UC, columns per item: 128 (a wave instruction covers 2 agent rows) or 64 (4 rows; half the LDS
-// per workgroup). RECOMP (round 6, the inference forward: dadmm_gnn_step with D == NULL at k >= 1,
-// D_next == NULL): delta_k is not read from HBM but recomputed from y_k as iteration k - 1 wrote it
-// (pre-guard, exactly the values that iteration's delta_{k+1} came from: same visit order, same
-// adds, same clamp — bit-identical), staged in LDS for all P agents of the column block before the
-// pass, and delta_{k+1} is not stored: 7 instead of 9 four-byte streams per element. The staging
-// doubles the item's LDS, so RECOMP runs 64-column items (measured as fast as 128 without it).
+// columns per item: 128 (a wave instruction covers 2 agent rows) or 64 (4 rows; half the LDS per
+// workgroup, so more workgroups fit per CU at large P)
+constexpr int UCB = 128;
+constexpr int RPI = 256 / UCB;    // agent rows per wave instruction (UCB / 4 lanes per row)
+static_assert(UCB == 64 || UCB == 128, "UCB");
 // Keeping phase 1's U rows in registers for phase 2 (one fewer HBM stream) was measured and
 // dropped: 97 instead of 82 VGPRs, four instead of five waves per SIMD, 86.1-86.4 vs 84.7-85.0 ms
 // at the configs[4] shard forward (profiles/r04/variants_r04o_step_keepu.txt)
 // LDS bytes for one sample's visit lists: at most 2 P entries per agent (each incident edge is
 // visited from both of its ends; a self-loop twice), one byte each
 __host__ __device__ constexpr int update_visit_words(int P) { return (2 * P * P + 3) / 4; }
-__host__ __device__ constexpr size_t update_lds_bytes(int P, int UC, bool recomp) {
-    return 4 * ((size_t)P * UC * (recomp ? 2 : 1) + (size_t)(P + 1) + update_visit_words(P));
+__host__ __device__ constexpr size_t update_lds_bytes(int P) {
+    return 4 * ((size_t)P * UCB + (size_t)(P + 1) + update_visit_words(P));
 }
-template <bool FUSED, int UC, bool RECOMP>
+template <bool FUSED>
 __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, float* lds) {
-    static_assert(UC == 64 || UC == 128, "UC");
-    static_assert(FUSED || !RECOMP, "the resolve never reads delta");
-    constexpr int RPI = 256 / UC;                     // agent rows per wave instruction
     // row pairs in flight per wave: the fused pass streams 5 state tensors, so fewer pairs keep
     // its registers at 4+ waves per SIMD
     constexpr int UP_CH = FUSED ? 2 : gnn::UP_CH;
     const int P = a.P, n = a.n;
-    const int ncb = (n + UC - 1) / UC;
+    const int ncb = (n + UCB - 1) / UCB;
     const int s = item / ncb;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int half = lane / (UC / 4);                // the lane's row within the instruction's RPI
-    const int c = (item % ncb) * UC + 4 * (lane % (UC / 4));
-    const int cl = 4 * (lane % (UC / 4));            // column within the block
+    const int half = lane / (UCB / 4);               // the lane's row within the instruction's RPI
+    const int c = (item % ncb) * UCB + 4 * (lane % (UCB / 4));
+    const int cl = 4 * (lane % (UCB / 4));                  // column within the block
     const bool cv = c < n;
     const size_t base = (size_t)s * P * n + (cv ? c : 0);
     bool yzero = false;
@@ -580,9 +575,8 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     float* const fix = (FUSED && k > 0 && f_prev != 0) ? y_prev : nullptr;
     float gclip, vclip;
     clips(a, k, gclip, vclip);
-    float* yl = lds;                                  // [P][UC] y_{k+1}
-    float* ylk = yl + P * UC;                         // [P][UC] y_k as iteration k - 1 wrote it (RECOMP)
-    int32_t* vpl = (int32_t*)(yl + P * UC * (RECOMP ? 2 : 1));   // [P + 1] list starts (sample-local)
+    float* yl = lds;                                  // [P][UCB] y_{k+1}
+    int32_t* vpl = (int32_t*)(yl + P * UCB);          // [P + 1] list starts (sample-local)
     uint8_t* vl = (uint8_t*)(vpl + P + 1);            // the sample's visit lists
     const int g0 = a.graph_shared ? 0 : s * P;
     const int vb = a.vptr[g0], vlen = a.vptr[g0 + P] - vb;
@@ -593,32 +587,6 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
     const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
     // row groups (RPI rows): wave w handles groups w, w + 4, ...; `half` selects the lane's row
     bool bad_y = false, bad_g = false;
-    // RECOMP: y_k rows of every agent (the fix below rewrites them after this barrier), then
-    // delta_k of a row from them in compute_delta's visit order (phase 2's sums, :227-229)
-    const bool y_in_lds = RECOMP && f_prev == 0;      // y_k itself is the staged block
-    if constexpr (RECOMP) {
-#pragma unroll 4
-        for (int q = w; RPI * q < P; q += WAVES) {
-            const int p = RPI * q + half;
-            const int pc = p < P ? p : P - 1;
-            const f32x4 v = *(const f32x4*)(y_prev + base + (size_t)pc * n);
-            if (p < P) *(f32x4*)(ylk + p * UC + cl) = cv ? v : z4;
-        }
-        __syncthreads();
-    }
-    auto delta_k = [&](int pc) {
-        const f32x4 yp = *(const f32x4*)(ylk + pc * UC + cl);
-        f32x4 acc = z4;
-        const int v0 = vpl[pc], v1 = vpl[pc + 1];
-        for (int t = v0; t < v1; ++t) {
-            const f32x4 yq = *(const f32x4*)(ylk + (int)vl[t] * UC + cl);
-            acc = acc + (yp - yq);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (a.variant != 0) acc[r] = clamp_t(acc[r], -20.0f, 20.0f);               // :229
-        return acc;
-    };
     auto phase1 = [&](int q0) {
         f32x4 gv[UP_CH], yv[UP_CH];
         float alv[UP_CH];
@@ -637,22 +605,13 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
                 const size_t off = base + (size_t)pc * n;
                 tv[u] = *(const f32x4*)(a.AtAy + off);
                 bv[u] = *(const f32x4*)(a.Atb + off);
-                if (!y_in_lds) yv[u] = *(const f32x4*)(ys + off);
+                yv[u] = *(const f32x4*)(ys + off);
                 uv[u] = *(const f32x4*)(U + off);
-                if constexpr (!RECOMP) dv[u] = *(const f32x4*)(a.D + off);
+                dv[u] = *(const f32x4*)(a.D + off);
                 tav[u] = hyp_at(a, s, 1, pc);
                 rhv[u] = hyp_at(a, s, 2, pc);
                 alv[u] = hyp_at(a, s, 0, pc);
                 dgv[u] = a.deg[(a.graph_shared ? 0 : (size_t)s * P) + pc];
-            }
-            if constexpr (RECOMP) {   // under the loads above
-#pragma unroll
-                for (int u = 0; u < UP_CH; ++u) {
-                    const int p = RPI * (q0 + WAVES * u) + half;
-                    const int pc = p < P ? p : P - 1;
-                    dv[u] = delta_k(pc);
-                    if (y_in_lds) yv[u] = *(const f32x4*)(ylk + pc * UC + cl);
-                }
             }
 #pragma unroll
             for (int u = 0; u < UP_CH; ++u) {
@@ -700,7 +659,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
                     }
                     *(f32x4*)(Yk + base + (size_t)p * n) = v;
                 }
-                *(f32x4*)(yl + p * UC + cl) = v;
+                *(f32x4*)(yl + p * UCB + cl) = v;
             }
         }
     };
@@ -729,13 +688,13 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
         for (int u = 0; u < UP_CH; ++u) {
             const int p = RPI * (q0 + WAVES * u) + half;
             if (p >= P || !cv) continue;
-            const f32x4 yp = *(const f32x4*)(yl + p * UC + cl);
+            const f32x4 yp = *(const f32x4*)(yl + p * UCB + cl);
             f32x4 acc = z4;
             const int v0 = vpl[p], v1 = vpl[p + 1];
             // whole-vector ops: two v_pk_add_f32 / v_pk_add_f32(neg) per visit instead of eight
             // scalar instructions, each lane of the pair rounded exactly as the scalar op
             for (int t = v0; t < v1; ++t) {
-                const f32x4 yq = *(const f32x4*)(yl + (int)vl[t] * UC + cl);
+                const f32x4 yq = *(const f32x4*)(yl + (int)vl[t] * UCB + cl);
                 acc = acc + (yp - yq);
             }
             const float et = FUSED ? etv[u] : hyp_at(a, s, 3, p);
@@ -748,7 +707,7 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
             }
             const size_t off = base + (size_t)p * n;
             *(f32x4*)(a.U_next + off) = un;
-            if (a.D_next != nullptr) *(f32x4*)(a.D_next + off) = acc;
+            *(f32x4*)(a.D_next + off) = acc;
         }
     };
     for (int q0 = w; RPI * q0 < P; q0 += WAVES * UP_CH) phase2(q0);
@@ -763,15 +722,13 @@ __device__ __forceinline__ void update_item(const GnnArgs& a, int k, int item, f
 }
 
 // the fused pass: one workgroup per item
-template <int UC, bool RECOMP>
 __global__ __launch_bounds__(THREADS) void step_kernel(GnnArgs a, int k) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    update_item<true, UC, RECOMP>(a, k, blockIdx.x, lds);
+    update_item<true>(a, k, blockIdx.x, lds);
 }
 
 // the resolve: a short grid (every workgroup reads one flag word); the g = 0 update, if needed,
 // strides over the items
-template <int UC>
 __global__ __launch_bounds__(THREADS) void resolve_kernel(GnnArgs a, int k, int items) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (!flag_ld(a.flags + GNN_F_GBAD(k))) {
@@ -782,7 +739,7 @@ __global__ __launch_bounds__(THREADS) void resolve_kernel(GnnArgs a, int k, int 
         return;
     }
     for (int item = blockIdx.x; item < items; item += gridDim.x) {
-        update_item<false, UC, false>(a, k, item, lds);
+        update_item<false>(a, k, item, lds);
         __syncthreads();   // the LDS tile is reused by the next item
     }
 }
@@ -1144,29 +1101,21 @@ item_kernel:
     return hipGetLastError();
 }
 
-template <int UC, bool RECOMP>
-static hipError_t launch_step_uc(const GnnArgs& a, int k, hipStream_t st) {
-    const int items = a.B * ((a.n + UC - 1) / UC);
-    const size_t lds = gnn::update_lds_bytes(a.P, UC, RECOMP);
+hipError_t gnn_launch_step(const GnnArgs& a, int k, hipStream_t st) {
+    const int items = a.B * ((a.n + gnn::UCB - 1) / gnn::UCB);
+    const size_t lds = gnn::update_lds_bytes(a.P);
     if (lds > 64 * 1024) {
-        for (const void* f : {(const void*)gnn::step_kernel<UC, RECOMP>, (const void*)gnn::resolve_kernel<UC>}) {
+        for (const void* f : {(const void*)gnn::step_kernel, (const void*)gnn::resolve_kernel}) {
             hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
     }
-    hipLaunchKernelGGL((gnn::step_kernel<UC, RECOMP>), dim3(items), dim3(gnn::THREADS), lds, st, a, k);
+    hipLaunchKernelGGL(gnn::step_kernel, dim3(items), dim3(gnn::THREADS), lds, st, a, k);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int rg = items < 256 ? items : 256;
-    hipLaunchKernelGGL(gnn::resolve_kernel<UC>, dim3(rg), dim3(gnn::THREADS), lds, st, a, k, items);
+    hipLaunchKernelGGL(gnn::resolve_kernel, dim3(rg), dim3(gnn::THREADS), lds, st, a, k, items);
     return hipGetLastError();
-}
-
-size_t gnn_step_lds_bytes(int P, bool recomp) { return gnn::update_lds_bytes(P, recomp ? 64 : 128, recomp); }
-
-hipError_t gnn_launch_step(const GnnArgs& a, int k, hipStream_t st) {
-    // D == NULL (k >= 1, checked by the ABI): delta_k recomputed from y_k (RECOMP above)
-    return a.D == nullptr ? launch_step_uc<64, true>(a, k, st) : launch_step_uc<128, false>(a, k, st);
 }
 
 hipError_t gnn_launch_finish(const GnnArgs& a, hipStream_t st) {

@@ -51,12 +51,7 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef const __attribute__((address_space(4))) float cfloat;
 
 constexpr int NS = SPLIT_COLS;          // columns (rows of y) per slice
-// Waves per workgroup: 16 (four per SIMD, agent groups q = w / 4 owning agents q, q + 4, ...)
-// where that fits 128 VGPRs without spills, else 8 (two per SIMD, agents q, q + 2, ...).
-template <int P, int GRAPH>
-constexpr int split_waves() {
-    return (P <= 4 || (P == 5 && GRAPH != GRAPH_ORDERED) || (P == 6 && GRAPH == GRAPH_SHARED)) ? 16 : 8;
-}
+constexpr int WV = 8;                   // waves per workgroup (2 per SIMD)
 // LDS row strides (floats). The operator slice is read two ways: GEMM1 takes A rows (ds_read_b128
 // of 4 columns), GEMM2 takes A^T fragments (ds_read_b32 of one column, 4 rows apart per k-group):
 // stride 68 keeps the b32 reads conflict-free (2 cycles) at a 2-way b128 conflict; 72 would swap
@@ -113,14 +108,13 @@ __device__ __forceinline__ bool wait_tiles(const uint32_t* const (&words)[TH > 0
     }
 }
 
-// One wave's share of the split forward. Q = w / 4: agents Q, Q + QN, ... (TH of them); GEMM1
-// m-block mb = w % 4 of those agents, GEMM2 / state n-tile nt = w % 4 of the slice.
-template <int P, int NT, int GRAPH, int Q, int WV>
+// One wave's share of the split forward. HALF = w / 4: agents HALF, HALF + 2, ... (TH of them);
+// GEMM1 m-block mb = w % 4 of those agents, GEMM2 / state n-tile nt = w % 4 of the slice.
+template <int P, int NT, int GRAPH, int HALF>
 __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restrict__ lds, const int w) {
     constexpr int S = NT;                            // slices of n_pad = 64 NT
     constexpr int NP = NT * 64;
-    constexpr int QN = WV / 4;                       // agent groups
-    constexpr int TH = P > Q ? (P - Q + QN - 1) / QN : 0;   // agents of this wave
+    constexpr int TH = (P - HALF + 1) / 2;           // agents of this wave
     constexpr int THA = TH > 0 ? TH : 1;
     const FusedArgs& a = sa.f;
     float* __restrict__ Alds = lds;                          // [P][64 m][AST]  A_p[:, slice]
@@ -196,7 +190,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
             bool bad_y = false, bad_u = false;
 #pragma unroll
             for (int i = 0; i < TH; ++i) {
-                const int p = Q + QN * i;
+                const int p = HALF + 2 * i;
                 const uint32_t off = (uint32_t)(((s * P + p) * n + n0) * 4);
                 f32x4 vy = {0, 0, 0, 0}, vu = {0, 0, 0, 0}, vd = {0, 0, 0, 0};
                 if (rows_ok) {
@@ -221,7 +215,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
         f32x4 bseed[THA];
 #pragma unroll
         for (int i = 0; i < TH; ++i) {
-            const int p = Q + QN * i;
+            const int p = HALF + 2 * i;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int mi = 16 * mb + 4 * h + r;
@@ -241,7 +235,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
             float al[THA], ta[THA], rh[THA], et[THA];
 #pragma unroll
             for (int i = 0; i < TH; ++i) {
-                const int p = Q + QN * i;
+                const int p = HALF + 2 * i;
                 const cfloat* hp = (const cfloat*)a.hyp + ((size_t)k * a.hyp_rows + (a.hyp_rows == 1 ? 0 : p)) * 4;
                 al[i] = hp[0]; ta[i] = hp[1]; rh[i] = hp[2]; et[i] = hp[3];
             }
@@ -260,7 +254,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
             f32x4 part[THA];
 #pragma unroll
             for (int i = 0; i < TH; ++i) {
-                const int p = Q + QN * i;
+                const int p = HALF + 2 * i;
                 f32x4 acc = bseed[i];
 #pragma unroll
                 for (int t = 0; t < NS / 16; ++t) {
@@ -274,14 +268,14 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
                 if (i > 0) {
                     asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
                     if (lane == 0)
-                        __hip_atomic_store((gu32*)(flag_at(Q + QN * (i - 1)) + slice), epoch,
+                        __hip_atomic_store((gu32*)(flag_at(HALF + 2 * (i - 1)) + slice), epoch,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             if (TH > 0) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0)
-                    __hip_atomic_store((gu32*)(flag_at(Q + QN * (TH - 1)) + slice), epoch,
+                    __hip_atomic_store((gu32*)(flag_at(HALF + 2 * (TH - 1)) + slice), epoch,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
 
@@ -299,7 +293,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
                 consensus_any<P, GRAPH>(yy, dd, msk, ord);
 #pragma unroll
                 for (int i = 0; i < TH; ++i) {
-                    const int p = Q + QN * i;
+                    const int p = HALF + 2 * i;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const float d = mclamp(dd[p][r], -dlim, dlim);
@@ -316,7 +310,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
             {
                 const uint32_t* words[THA];
 #pragma unroll
-                for (int i = 0; i < TH; ++i) words[i] = flag_at(Q + QN * i);
+                for (int i = 0; i < TH; ++i) words[i] = flag_at(HALF + 2 * i);
                 if (!aborted) aborted = !wait_tiles<S, TH>(words, epoch, abortw, sa.spin_ticks, lane, slice);
             }
             f32x4 c[THA][S];
@@ -324,10 +318,10 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
             for (int i = 0; i < TH; ++i)
 #pragma unroll
                 for (int s2 = 0; s2 < S; ++s2)
-                    c[i][s2] = s2 == slice ? part[i] : bload4<16>(rX, xtile_off(slot, Q + QN * i, s2));
+                    c[i][s2] = s2 == slice ? part[i] : bload4<16>(rX, xtile_off(slot, HALF + 2 * i, s2));
 #pragma unroll
             for (int i = 0; i < TH; ++i) {
-                const int p = Q + QN * i;
+                const int p = HALF + 2 * i;
                 f32x4 rsum = c[i][0];
 #pragma unroll
                 for (int s2 = 1; s2 < S; ++s2) rsum = rsum + c[i][s2];
@@ -341,7 +335,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
             bool bad_g = false;
 #pragma unroll
             for (int i = 0; i < TH; ++i) {
-                const int p = Q + QN * i;
+                const int p = HALF + 2 * i;
                 f32x4 gp = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
                 for (int t = 0; t < M_PAD / 16; ++t) {
@@ -389,7 +383,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
             const rsrc_t rU = make_rsrc(a.U_out, state_bytes);
 #pragma unroll
             for (int i = 0; i < TH; ++i) {
-                const int p = Q + QN * i;
+                const int p = HALF + 2 * i;
                 f32x4 v;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -410,25 +404,18 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
     }
 }
 
-template <int P, int NT, int GRAPH, int WV = split_waves<P, GRAPH>()>
+template <int P, int NT, int GRAPH>
 __global__ __launch_bounds__(WV * 64) void split_forward_kernel(SplitArgs sa) {
     __shared__ __attribute__((aligned(16))) float lds[P * M_PAD * AST + P * BT * (YS + RS)];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (w < 4)
-        split_body<P, NT, GRAPH, 0, WV>(sa, lds, w);
-    else if (w < 8)
-        split_body<P, NT, GRAPH, 1, WV>(sa, lds, w);
-    else if constexpr (WV == 16) {
-        if (w < 12)
-            split_body<P, NT, GRAPH, 2, WV>(sa, lds, w);
-        else
-            split_body<P, NT, GRAPH, 3, WV>(sa, lds, w);
-    }
+        split_body<P, NT, GRAPH, 0>(sa, lds, w);
+    else
+        split_body<P, NT, GRAPH, 1>(sa, lds, w);
 }
 
 template <int P, int NT, int GRAPH>
 hipError_t launch_split(const SplitArgs& sa, hipStream_t stream) {
-    constexpr int WV = split_waves<P, GRAPH>();
     hipLaunchKernelGGL((split_forward_kernel<P, NT, GRAPH>), dim3(sa.groups * NT), dim3(WV * 64), 0,
                        stream, sa);
     return hipGetLastError();

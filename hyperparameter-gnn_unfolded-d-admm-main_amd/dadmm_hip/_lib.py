@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # scripts/time_variants.sh); it is still the HIP library, there is no other path
 LIB_PATH = os.environ.get("DADMM_LIB_VARIANT") or os.path.join(_HERE, "libdadmm.so")
 
-ABI_VERSION = 19
+ABI_VERSION = 18
 DADMM_OK, DADMM_EINVAL, DADMM_EUNSUPPORTED, DADMM_EHIP = 0, -1, -2, -3
 VARIANT_UNFOLDED, VARIANT_GNN = 0, 1
 STATUS_Y_NONFINITE, STATUS_U_NONFINITE, STATUS_GRAD_NAN, STATUS_YNEXT_NAN = 1, 2, 4, 8

@@ -8,7 +8,6 @@ forward (K iterations) as one autograd node.
 """
 from __future__ import annotations
 
-import os
 import ctypes
 
 import torch
@@ -16,9 +15,6 @@ import torch
 from . import _lib
 from .graph import GraphBatch
 from .ops import PreparedOperator, _dev_check, _pad_n, _ptr, _stream
-
-
-_AB_STORE_DELTA = os.environ.get("DADMM_AB_STORE_DELTA") == "1"   # TEMP A/B
 
 
 class GnnRun:
@@ -89,19 +85,15 @@ class GnnRun:
                 _stream(self.dev)))
         return out
 
-    def step(self, k: int, AtAy, hyp_k, U, D, delta: bool = True):
-        """One iteration; returns (y_{k+1}, U_{k+1}, delta_{k+1}). ``delta=False`` (inference):
-        delta_{k+1} is not stored (None is returned) and, at k >= 1, delta_k is recomputed from
-        y_k inside the step (``D`` is ignored) — bit-identical, two fewer state streams."""
+    def step(self, k: int, AtAy, hyp_k, U, D):
+        """One iteration; returns (y_{k+1}, U_{k+1}, delta_{k+1})."""
         g = self.graphs
-        delta = delta or _AB_STORE_DELTA
         U_next = torch.empty_like(U)
-        D_next = torch.empty_like(U) if delta else None
-        D_in = D if (delta or k == 0) else None
+        D_next = torch.empty_like(D)
         with torch.cuda.device(self.dev):
             _lib.check("dadmm_gnn_step", self.L.dadmm_gnn_step(
                 ctypes.byref(self.d), k, _ptr(g.vptr), _ptr(g.vq), _ptr(g.deg), _ptr(hyp_k),
-                _ptr(self.yptr), _ptr(AtAy), _ptr(self.Atb), _ptr(U), _ptr(D_in), _ptr(U_next),
+                _ptr(self.yptr), _ptr(AtAy), _ptr(self.Atb), _ptr(U), _ptr(D), _ptr(U_next),
                 _ptr(D_next), _ptr(self.G), _ptr(self.flags), _stream(self.dev)))
         return self.ys[k + 1], U_next, D_next
 

@@ -309,10 +309,7 @@ class DLASSO_GNNHyp3_Progressive(nn.Module):
                 hyp_k = torch.stack([alpha_k, tau_k, rho_k, eta_k], dim=1).reshape(batch_size, 4, H)
             if self.on_hyp is not None:
                 self.on_hyp(AtAy[..., :n], Atb, (alpha_k, tau_k, rho_k, eta_k))
-            if torch.is_grad_enabled():
-                y, U, D = StepFn.apply(y, U, D, AtAy, hyp_k.contiguous(), run, k)
-            else:   # inference: delta recomputed inside the step, never stored (GnnRun.step)
-                y, U, D = run.step(k, AtAy, hyp_k.contiguous(), U, D, delta=False)
+            y, U, D = StepFn.apply(y, U, D, AtAy, hyp_k.contiguous(), run, k)
             ys.append(y)
         if train_hip:   # the K iterations' BatchNorm running-statistics updates, in call order
             hyper_ops.flush_running_stats(self)
@@ -448,7 +445,7 @@ class _EvalGraphPlan:
             for k in range(K):
                 AtAy = run.gram(k)
                 hyper_ops.hypernetwork_eval(model, AtAy, run.Atb, n, self.ahat, per_sample, self.bufs)
-                y, U, D = run.step(k, AtAy, self.bufs.hyp, U, D, delta=False)
+                y, U, D = run.step(k, AtAy, self.bufs.hyp, U, D)
             run.finish()
 
         cur = torch.cuda.current_stream(dev)

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define DADMM_ABI_VERSION 19
+#define DADMM_ABI_VERSION 18
 
 enum {
     DADMM_OK = 0,
@@ -330,9 +330,7 @@ int dadmm_gnn_gram_acc(const dadmm_dims* d, const void* op, const float* x, floa
                        void* stream);
 /* One iteration: reads y_k (resolved), U_k (U, reset by the guard), delta_k (D), AtAy_k, Atb and
  * hyp_k [B][4][H]; writes y_{k+1} to yptr[k+1], U_{k+1} to U_next, delta_{k+1} to D_next.
- * G: [B][P][n] scratch. ABI 19: D == NULL at k >= 1 recomputes delta_k from yptr[k] as iteration
- * k - 1 left it (bit-identical to passing that iteration's D_next), and D_next == NULL skips the
- * delta_{k+1} store — the inference forward's form, two fewer state streams per iteration. */
+ * G: [B][P][n] scratch. */
 int dadmm_gnn_step(const dadmm_dims* d, int32_t k, const int32_t* visit_ptr, const uint8_t* visit_q,
                    const float* deg, const float* hyp_k, float* const* yptr, const float* AtAy,
                    const float* Atb, const float* U, const float* D, float* U_next, float* D_next,

@@ -427,49 +427,3 @@ def test_train_mode_step_updates_bn_and_trains(cuda):
     grads = [p.grad for p in model.parameters() if p.grad is not None]
     assert grads and all(torch.isfinite(g).all() for g in grads)
     opt.step()
-
-
-@pytest.mark.parametrize("P,m,n,B,K,bad", [(5, 32, 64, 24, 6, None), (13, 40, 200, 9, 5, "alpha"),
-                                           (5, 64, 256, 20, 5, "tau"), (50, 32, 1024, 3, 4, None),
-                                           (4, 16, 32, 8, 5, "y0")])
-def test_step_delta_recompute_bit_identical(cuda, P, m, n, B, K, bad):
-    """dadmm_gnn_step with D = NULL at k >= 1 and D_next = NULL (the inference form, ABI 19:
-    delta_k recomputed from y_k in the step) gives the iterates and U_k of the form that stores
-    and reloads delta, bit for bit — also when the y_next guard (NaN alpha), the gradient guard
-    (NaN tau: the resolve launch) or the k = 0 guard (non-finite y0) fires."""
-    from dadmm_hip import _lib
-    from dadmm_hip.gnn_ops import GnnRun
-    from dadmm_hip.graph import ingest
-    model, A, b, x, graphs, inits = _setup(cuda, P, m, n, B, K, "diff", True, seed=4)
-    y0, U0, d0 = (v.copy() for v in inits)
-    if bad == "y0":
-        y0[2, 1, 3] = np.nan
-    rng = np.random.default_rng(P + K)
-    hyp = (0.05 + 0.9 * rng.random((K, B, 4, P))).astype(np.float32)
-    hyp[:, :, 0] *= 0.1
-    if bad == "alpha":
-        hyp[2, 3, 0, 1] = np.nan
-    if bad == "tau":
-        hyp[1, 4, 1, 2] = np.nan
-    g = ingest(graphs, P, B, cuda)
-    out = {}
-    for delta in (True, False):
-        run = GnnRun(model.operator(), _t(b, cuda), g, K, P, _lib.VARIANT_GNN,
-                     *(_t(v, cuda) for v in (y0, U0, d0)), False)
-        U, D = run.U0, run.d0
-        Us = []
-        for k in range(K):
-            AtAy = run.gram(k)
-            _, U, D = run.step(k, AtAy, _t(hyp[k], cuda), U, D, delta=delta)
-            assert (D is None) == (not delta)
-            Us.append(U)
-        st = run.finish()
-        torch.cuda.synchronize()
-        out[delta] = (run.Y.clone(), torch.stack(Us), int(st.item()))
-    (Ya, Ua, sa), (Yb, Ub, sb) = out[True], out[False]
-    assert sa == sb
-    if bad is not None:
-        assert sa != 0
-    # bitwise (U_k holds the NaNs a guard then resets: torch.equal treats NaN as unequal)
-    assert torch.equal(Ya[..., :n].contiguous().view(torch.int32), Yb[..., :n].contiguous().view(torch.int32))
-    assert torch.equal(Ua[..., :n].contiguous().view(torch.int32), Ub[..., :n].contiguous().view(torch.int32))
