@@ -8,7 +8,7 @@
 // subsequence = idx, offset) and, for it = 0, 1, ..., writes hiprand_normal4's four values to
 // elements idx + T (4 it + ii) (T = 256 G); each call advances the generator's offset by
 // 4 ceil(numel / 4T). This kernel replays exactly that mapping for all three tensors at once (one
-// real thread per (tensor, virtual idx)), so its output is bit-identical to
+// real thread per virtual idx, drawing for the three tensors), so its output is bit-identical to
 //   torch.randn(shape) * 1e-2  ==  torch.empty(shape).normal_(0, 1e-2)
 // (tests/test_gpu_parity.py::test_prologue_draws_match_torch), and zeroes `nzero` int32 words
 // (the status word and the stepwise guard flags) — replacing 3 RNG launches, 2 fills and a memset.
@@ -70,44 +70,58 @@ __device__ __forceinline__ uint4 philox10(uint4 c, uint2 k) {
 
 // 32-bit index arithmetic (numel < 2^31 is checked by the launcher): the 64-bit divisions of a
 // straightforward port cost more than the Philox rounds themselves.
+// One real thread per virtual thread idx draws for all three tensors (round 6): the three
+// counters' Philox rounds are independent, so they interleave in one instruction stream, and the
+// grid is torch's T threads (2048 workgroups of 256 on 256 CUs: one dispatch round) instead of
+// 3 T. At B = 1024 every virtual thread draws one block per tensor, and the 6,144 short
+// workgroups of the per-(tensor, idx) form were paced by workgroup dispatch, not by the rounds.
 template <bool PADDED>
 __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
     const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
-    if (gid < (uint32_t)a.nzero) a.zero[gid] = 0;
+    for (uint32_t i = gid; i < (uint32_t)a.nzero; i += gridDim.x * 256u) a.zero[i] = 0;
     if (a.numel == 0) return;
     const uint32_t T = (uint32_t)a.threads;       // torch's 256 G virtual threads per tensor
-    const uint32_t t = gid / T;                   // tensor 0, 1, 2 = y0, U0, delta0
-    if (t >= 3) return;
-    const uint32_t idx = gid - t * T;
-    float* out = t == 0 ? a.y0 : (t == 1 ? a.U0 : a.d0);
+    if (gid >= T) return;
+    const uint32_t idx = gid;
+    float* const out[3] = {a.y0, a.U0, a.d0};
     const uint32_t numel = (uint32_t)a.numel, n = (uint32_t)a.n, ns = (uint32_t)a.n_store;
     const uint32_t iters = (numel - 1) / (T * 4) + 1;
-    auto put = [&](uint32_t li, float v) {
+    auto put = [&](int t, uint32_t li, float v) {
         uint32_t o = li;
         if (PADDED) {
             const uint32_t row = li / n;
             o = row * ns + (li - row * n);
         }
         // transformation::normal (val * std + mean), contracted as torch's build does
-        out[o] = __builtin_fmaf(v, a.stddev, a.mean);
+        out[t][o] = __builtin_fmaf(v, a.stddev, a.mean);
     };
-    // counter after discard_subsequence(idx) then discard(offset): (x, y) = offset / 4,
-    // (z, w) = idx plus the carry out of y
-    const uint64_t c0 = (a.offset + (uint64_t)t * a.offset_step) / 4;
+    // tensor t's counter after discard_subsequence(idx) then discard(offset_t): (x, y) =
+    // offset_t / 4, (z, w) = idx plus the carry out of y; offset_t = offset + t * offset_step
+    // (the generator advanced by each torch call in turn)
+    uint64_t c0[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) c0[t] = (a.offset + (uint64_t)t * a.offset_step) / 4;
     const uint2 key = make_uint2((unsigned)a.seed, (unsigned)(a.seed >> 32));
     uint32_t li = idx;
     for (uint32_t it = 0; it < iters; ++it, li += 4 * T) {
-        const uint64_t cx = c0 + it;                      // the counter's low 64 bits
-        const unsigned carry = cx < c0 ? 1u : 0u;         // into the subsequence words
-        const uint4 r = philox10(make_uint4((unsigned)cx, (unsigned)(cx >> 32), idx + carry,
-                                            (idx + carry < idx) ? 1u : 0u), key);
-        const float2 p0 = box_muller(r.x, r.y);
-        if (li < numel) put(li, p0.x);
-        if (li + T < numel) put(li + T, p0.y);
-        if (li + 2 * T < numel) {
-            const float2 p1 = box_muller(r.z, r.w);
-            put(li + 2 * T, p1.x);
-            if (li + 3 * T < numel) put(li + 3 * T, p1.y);
+        uint4 r[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const uint64_t cx = c0[t] + it;                   // the counter's low 64 bits
+            const unsigned carry = cx < c0[t] ? 1u : 0u;      // into the subsequence words
+            r[t] = philox10(make_uint4((unsigned)cx, (unsigned)(cx >> 32), idx + carry,
+                                       (idx + carry < idx) ? 1u : 0u), key);
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const float2 p0 = box_muller(r[t].x, r[t].y);
+            if (li < numel) put(t, li, p0.x);
+            if (li + T < numel) put(t, li + T, p0.y);
+            if (li + 2 * T < numel) {
+                const float2 p1 = box_muller(r[t].z, r[t].w);
+                put(t, li + 2 * T, p1.x);
+                if (li + 3 * T < numel) put(t, li + 3 * T, p1.y);
+            }
         }
     }
 }
@@ -115,8 +129,8 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
 }  // namespace
 
 hipError_t launch_prologue(const PrologueArgs& a, hipStream_t stream) {
-    int64_t work = a.numel > 0 ? 3 * a.threads : 0;
-    if (work < a.nzero) work = a.nzero;
+    int64_t work = a.numel > 0 ? a.threads : 0;
+    if (work < a.nzero) work = a.nzero < 2048 * 256 ? a.nzero : 2048 * 256;   // the zeroing strides
     if (work == 0) return hipSuccess;
     if (a.numel >= ((int64_t)1 << 31) || work >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     if (a.n_store != a.n)
