@@ -252,6 +252,11 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
             //      chain at a time: stored write-through (sc1); chain i-1's epoch word after chain
             //      i's store (every VMEM op but that store has completed: vmcnt counts in order) --
             f32x4 part[THA];
+            // the wave's priority raised while it issues its MFMA chains (the arbiter then prefers
+            // it, so the matrix pipe stays fed while the SIMD's other wave runs VALU work): 187.8-191.1
+            // vs 192.3-196.9 us per configs[1] forward; the second-dispatched half raised for the
+            // whole loop instead (dadmm_fused.hip's choice) measured 216-220 us
+            __builtin_amdgcn_s_setprio(2);
 #pragma unroll
             for (int i = 0; i < TH; ++i) {
                 const int p = HALF + 2 * i;
@@ -272,6 +277,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
+            __builtin_amdgcn_s_setprio(0);
             if (TH > 0) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0)
@@ -333,6 +339,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
             //      update (:69-93) -> Ylds and Y[k] ---------------------------------------------
             const rsrc_t rY = make_rsrc(a.Y + (size_t)k * B * P * n, state_bytes);
             bool bad_g = false;
+            __builtin_amdgcn_s_setprio(2);
 #pragma unroll
             for (int i = 0; i < TH; ++i) {
                 const int p = HALF + 2 * i;
@@ -363,6 +370,7 @@ __device__ __forceinline__ void split_body(const SplitArgs& sa, float* __restric
                 *(f32x4*)yrow = yn;
                 bstore4<16>(yn, rY, rows_ok ? voffY + (uint32_t)(p * n * 4) : 0x80000000u);
             }
+            __builtin_amdgcn_s_setprio(0);
             status |= bad_g ? 4u : 0u;
 #pragma unroll
             for (int i = 0; i < TH; ++i) et_prev[i] = et[i];
